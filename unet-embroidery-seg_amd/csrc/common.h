@@ -1,0 +1,93 @@
+// Shared definitions for the unetseg HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdio>
+#include <string>
+
+#define UNETSEG_API extern "C" __attribute__((visibility("default")))
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+enum { DT_F32 = 0, DT_BF16 = 1 };
+
+// ---- error handling: thread-local message, int status ------------------------------------
+void unetseg_set_error(const char* fmt, ...);
+
+#define US_CHECK_ARG(cond, ...)            \
+  do {                                     \
+    if (!(cond)) {                         \
+      unetseg_set_error(__VA_ARGS__);      \
+      return 1;                            \
+    }                                      \
+  } while (0)
+
+#define US_LAUNCH_CHECK(name)                                                        \
+  do {                                                                               \
+    hipError_t _e = hipGetLastError();                                               \
+    if (_e != hipSuccess) {                                                          \
+      unetseg_set_error("%s: launch failed: %s", name, hipGetErrorString(_e));       \
+      return 2;                                                                      \
+    }                                                                                \
+  } while (0)
+
+// ---- element conversion ------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ float to_f(T v) { return (float)v; }
+template <typename T>
+__device__ __forceinline__ T from_f(float v) { return (T)v; }
+
+// 16-byte vector of T
+template <typename T>
+struct Vec {
+  static constexpr int N = 16 / sizeof(T);
+};
+
+template <typename T>
+__device__ __forceinline__ void load_vec(const T* p, float (&out)[16 / sizeof(T)]) {
+  uint4 raw = *reinterpret_cast<const uint4*>(p);
+  const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+  for (int i = 0; i < 16 / (int)sizeof(T); ++i) out[i] = (float)e[i];
+}
+
+template <typename T>
+__device__ __forceinline__ void store_vec(T* p, const float (&in)[16 / sizeof(T)]) {
+  uint4 raw;
+  T* e = reinterpret_cast<T*>(&raw);
+#pragma unroll
+  for (int i = 0; i < 16 / (int)sizeof(T); ++i) e[i] = (T)in[i];
+  *reinterpret_cast<uint4*>(p) = raw;
+}
+
+// ---- wave / block reductions (wave64) ------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// block-wide sum over blockDim.x threads (multiple of 64, <= 1024); every thread gets the result
+template <typename F>
+__device__ __forceinline__ F block_sum(F v, F* scratch /* >= 16 entries */) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  F t = 0;
+  for (int i = 0; i < nw; ++i) t += scratch[i];
+  return t;
+}
+
+static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,657 @@
+// Implicit-GEMM 2-D convolution for NHWC activations on CDNA4 MFMA (gfx950).
+//
+// Replaces every nn.Conv2d of the reference hot path:
+//   model/resnet_backbone.py:19,33,126,167   model/unet_resnet.py:17,19,72,74,78
+//   model/unet_plain.py:9,12,69              model/unet_attention.py:16,20,24,76
+//   model/unet_multitask.py:17-18,62,64,69
+//
+// Three GEMM views of one conv (x: [N,H,W,Cin] NHWC, y: [N,P,Q,Cout], w: [Cout][Cin][R][S]):
+//   fwd   : Y[m=(n,p,q)][k_out]  = sum_{(r,s,c)} X[n][p*st-pad+r][q*st-pad+s][c] * Wk[k_out][r][s][c]
+//   dgrad : dX[m=(n,h,w)][c]     = sum_{(r,s,k)} dY[n][(h+pad-r)/st][(w+pad-s)/st][k] * Wt[c][r][s][k]
+//           (stride 2: four output-parity classes, each a stride-1 gather over its own tap subset)
+//   wgrad : dW[k_out][(r,s,c)]   = sum_{m=(n,p,q)} dY[m][k_out] * X[n][p*st-pad+r][q*st-pad+s][c]
+// fwd and dgrad are the same "TN" kernel (both operands K-contiguous, gathered with 16-B loads);
+// wgrad has both operands pixel-major and reads MFMA fragments with ds_read_b64_tr_b16.
+//
+// bf16 path: v_mfma_f32_16x16x32_bf16, fp32 accumulate.  fp32 path (parity mode):
+// v_mfma_f32_16x16x4_f32 (exact f32 fma chain).  256 threads = 4 waves in 2x2, one 16x16
+// accumulator per (i,j) subtile; register-staged global->LDS double buffering, one barrier per
+// K step; LDS rows are 128 B (TN) / 256 B (wgrad) with XOR chunk swizzles chosen so that the
+// fragment reads are bank-conflict free.
+#include "common.h"
+
+namespace {
+
+constexpr int kBM = 128;  // GEMM M tile of the TN kernel (also the BN-statistics row tile)
+
+// TN kernel LDS image: [row][8 x 16B chunks], chunk swizzle makes ds_read_b128 fragment reads
+// (16 rows x one chunk per 16-lane group) conflict free.
+__device__ __forceinline__ int swz8(int row, int ch) { return ch ^ ((row >> 1) & 7); }
+// wgrad LDS image: [k row][>=16 chunks]; rows {q, 8+q} (q<4) land on distinct chunk pairs so
+// the transposed 4x16 reads of a 32-lane half are conflict free.
+__device__ __forceinline__ int swz_tr(int row) { return ((row & 3) | ((row >> 1) & 4)) << 1; }
+
+struct IgemmArgs {
+  const void* x1;
+  const void* x2;
+  int c1, c2, ldc1, ldc2;  // concat sources (c2 may be 0); channel counts and pixel strides
+  int N, H, W;             // gather-source tensor
+  int hc, wc;              // GEMM-row pixel grid per image
+  int istride;             // source row = hh*istride + dh
+  int r0, rs, nr, dh0, dhs;
+  int s0, ss, ns, dw0, dws;
+  int S;                   // kernel width of the weight image
+  int cin;                 // GEMM K per tap = c1 + c2
+  const void* wt;
+  long ldw;                // weight row length (R*S*cin)
+  int Ng;                  // GEMM N
+  int ostride, ph, pw, OH, OW;  // output pixel = (n, hh*ostride+ph, ww*ostride+pw)
+  void* y;
+  int ldy, accumulate;
+  const float* bias;
+  int relu;
+  float* stats;            // [2][Ng][stats_ld] (sum, M2 about the tile mean) per M tile
+  int stats_ld;
+  int M;
+};
+
+template <typename T, int BN>
+__global__ __launch_bounds__(256) void igemm_tn_kernel(IgemmArgs a) {
+  constexpr bool kBF = sizeof(T) == 2;
+  constexpr int VE = 16 / sizeof(T);
+  constexpr int BK = 8 * VE;
+  constexpr int BM = kBM;
+  constexpr int A_PER = BM / 32, B_PER = BN / 32;
+  constexpr int FM = BM / 32, FN = BN / 32;
+  __shared__ __attribute__((aligned(16))) uint4 lds[2][(BM + BN) * 8];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kv = tid & 7, rb = tid >> 3;
+  const int hw = a.hc * a.wc;
+
+  int a_nb[A_PER], a_ih[A_PER], a_iw[A_PER];
+  bool a_ok[A_PER];
+#pragma unroll
+  for (int i = 0; i < A_PER; ++i) {
+    int m = m0 + rb + 32 * i;
+    a_ok[i] = m < a.M;
+    int mm = a_ok[i] ? m : 0;
+    int nb = mm / hw, rem = mm - nb * hw;
+    int hh = rem / a.wc, ww = rem - hh * a.wc;
+    a_nb[i] = nb * a.H;
+    a_ih[i] = hh * a.istride;
+    a_iw[i] = ww * a.istride;
+  }
+  const T* x1 = (const T*)a.x1;
+  const T* x2 = (const T*)a.x2;
+  const T* wt = (const T*)a.wt;
+
+  int kc = kv * VE, jr = 0, js = 0;
+  while (kc >= a.cin) {
+    kc -= a.cin;
+    if (++js == a.ns) { js = 0; ++jr; }
+  }
+  const long Ktot = (long)a.nr * a.ns * a.cin;
+  const int nkt = (int)((Ktot + BK - 1) / BK);
+
+  uint4 ra[A_PER], rbv[B_PER];
+  auto gload = [&]() {
+    const bool kok = jr < a.nr;
+    const int r = a.r0 + a.rs * jr, s = a.s0 + a.ss * js;
+    const int dh = a.dh0 + a.dhs * jr, dw = a.dw0 + a.dws * js;
+    const bool first = kc < a.c1;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
+      bool ok = kok && a_ok[i] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (ok) {
+        long pix = (long)(a_nb[i] + ih) * a.W + iw;
+        const T* p = first ? x1 + pix * a.ldc1 + kc : x2 + pix * a.ldc2 + (kc - a.c1);
+        v = *reinterpret_cast<const uint4*>(p);
+      }
+      ra[i] = v;
+    }
+    const long wofs = (long)(r * a.S + s) * a.cin + kc;
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      int n = n0 + rb + 32 * i;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (kok && n < a.Ng) v = *reinterpret_cast<const uint4*>(wt + (long)n * a.ldw + wofs);
+      rbv[i] = v;
+    }
+    kc += BK;
+    while (kc >= a.cin) {
+      kc -= a.cin;
+      if (++js == a.ns) { js = 0; ++jr; }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      int row = rb + 32 * i;
+      lds[buf][row * 8 + swz8(row, kv)] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      int row = rb + 32 * i;
+      lds[buf][(BM + row) * 8 + swz8(row, kv)] = rbv[i];
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nkt > 0) {
+    gload();
+    sstore(0);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) gload();
+    const uint4* As = &lds[cur][0];
+    const uint4* Bs = &lds[cur][BM * 8];
+    if constexpr (kBF) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ch = kk * 4 + (lane >> 4);
+        bf16x8 af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          int row = wm * (BM / 2) + i * 16 + (lane & 15);
+          uint4 v = As[row * 8 + swz8(row, ch)];
+          af[i] = *reinterpret_cast<bf16x8*>(&v);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          int row = wn * (BN / 2) + j * 16 + (lane & 15);
+          uint4 v = Bs[row * 8 + swz8(row, ch)];
+          bfr[j] = *reinterpret_cast<bf16x8*>(&v);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      const float* Af = reinterpret_cast<const float*>(As);
+      const float* Bf = reinterpret_cast<const float*>(Bs);
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        float af[FM], bfr[FN];
+        const int e = lane >> 4;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          int row = wm * (BM / 2) + i * 16 + (lane & 15);
+          af[i] = Af[(row * 8 + swz8(row, kk)) * 4 + e];
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          int row = wn * (BN / 2) + j * 16 + (lane & 15);
+          bfr[j] = Bf[(row * 8 + swz8(row, kk)) * 4 + e];
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nkt) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------
+  T* y = (T*)a.y;
+  const int ohw = a.hc * a.wc;
+  float colsum[FN], colm2[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) colsum[j] = colm2[j] = 0.f;
+  float vals[FM][FN][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + e;
+      const bool mok = m < a.M;
+      long opix = 0;
+      if (mok) {
+        int nb = m / ohw, rem = m - nb * ohw;
+        int hh = rem / a.wc, ww = rem - hh * a.wc;
+        opix = ((long)nb * a.OH + hh * a.ostride + a.ph) * a.OW + ww * a.ostride + a.pw;
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
+        float v = acc[i][j][e];
+        float vr = 0.f;
+        if (mok && n < a.Ng) {
+          if (a.bias) v += a.bias[n];
+          if (a.relu) v = fmaxf(v, 0.f);
+          T* p = y + opix * a.ldy + n;
+          if (a.accumulate) v += (float)(*p);
+          T t = (T)v;
+          *p = t;
+          vr = (float)t;
+          colsum[j] += vr;
+        }
+        vals[i][j][e] = vr;
+      }
+    }
+  }
+  if (a.stats) {  // per-tile column sum and M2 about the tile mean (Chan merge in bn_finalize)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(&lds[0][0]);  // [0,2BN): sums per (wm, col); [2BN,4BN): M2
+    const int cnt = min(BM, a.M - m0);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float s = colsum[j];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (lane < 16) red[wm * BN + wn * (BN / 2) + j * 16 + lane] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wn * (BN / 2) + j * 16 + (lane & 15);
+      const float mean = (red[col] + red[BN + col]) / (float)cnt;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + e;
+          if (m < a.M) {
+            const float d = vals[i][j][e] - mean;
+            q += d * d;
+          }
+        }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      colm2[j] = q;
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      if (lane < 16) red[2 * BN + wm * BN + wn * (BN / 2) + j * 16 + lane] = colm2[j];
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      const int n = n0 + c;
+      if (n < a.Ng) {
+        a.stats[(long)n * a.stats_ld + blockIdx.x] = red[c] + red[BN + c];
+        a.stats[((long)a.Ng + n) * a.stats_ld + blockIdx.x] = red[2 * BN + c] + red[3 * BN + c];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// wgrad: C[k_out][(r,s,c)] = sum_pix dY[pix][k_out] * im2col(X)[pix][(r,s,c)], split-K over pixels
+// ---------------------------------------------------------------------------------------
+struct WgradArgs {
+  const void* x1;
+  const void* x2;
+  int c1, c2, ldc1, ldc2;
+  int N, H, W, P, Q, stride, pad, R, S;
+  const void* dy;
+  int ldy, Cout;
+  int cin, Ng;
+  long Kpix;
+  int kt_per_split;
+  float* ws;  // [split][Cout][Ng]
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
+  constexpr bool kBF = sizeof(T) == 2;
+  constexpr int VE = 16 / sizeof(T);
+  constexpr int BM = 128, BN = 128;
+  constexpr int CPR = BM * (int)sizeof(T) / 16;  // 16-B chunks per LDS row
+  constexpr int BKW = kBF ? 32 : 16;             // pixels per K step
+  constexpr int RPP = 256 / CPR;                 // rows per load pass
+  constexpr int PASSES = BKW / RPP;
+  constexpr int FM = 4, FN = 4;
+  __shared__ __attribute__((aligned(16))) uint4 lds[2][2 * BKW * CPR];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int cv = tid % CPR, rr = tid / CPR;
+  const long nkt_total = (a.Kpix + BKW - 1) / BKW;
+  const long kt0 = (long)blockIdx.z * a.kt_per_split;
+  const long kt1 = min(nkt_total, kt0 + a.kt_per_split);
+
+  const T* dy = (const T*)a.dy;
+  const int cout = m0 + cv * VE;
+  const bool a_col_ok = cout < a.Cout;
+  const int nn = n0 + cv * VE;
+  const bool b_col_ok = nn < a.Ng;
+  int tap = b_col_ok ? nn / a.cin : 0;
+  int cc = b_col_ok ? nn - tap * a.cin : 0;
+  const int rr_ = tap / a.S, ss_ = tap - rr_ * a.S;
+  const int dh = rr_ - a.pad, dw = ss_ - a.pad;
+  const bool first = cc < a.c1;
+  const T* xb = first ? (const T*)a.x1 + cc : (const T*)a.x2 + (cc - a.c1);
+  const int ldx = first ? a.ldc1 : a.ldc2;
+
+  // pixel state of each of this thread's rows
+  int pn[PASSES], pp[PASSES], pq[PASSES];
+  long pk[PASSES];
+#pragma unroll
+  for (int i = 0; i < PASSES; ++i) {
+    long k = kt0 * BKW + rr + RPP * i;
+    pk[i] = k;
+    long kk = k < a.Kpix ? k : 0;
+    int nb = (int)(kk / ((long)a.P * a.Q));
+    int rem = (int)(kk - (long)nb * a.P * a.Q);
+    pn[i] = nb;
+    pp[i] = rem / a.Q;
+    pq[i] = rem - pp[i] * a.Q;
+  }
+  uint4 ra[PASSES], rbv[PASSES];
+  auto gload = [&]() {
+#pragma unroll
+    for (int i = 0; i < PASSES; ++i) {
+      const bool kok = pk[i] < a.Kpix;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (kok && a_col_ok) v = *reinterpret_cast<const uint4*>(dy + pk[i] * a.ldy + cout);
+      ra[i] = v;
+      uint4 u = make_uint4(0, 0, 0, 0);
+      const int ih = pp[i] * a.stride + dh, iw = pq[i] * a.stride + dw;
+      if (kok && b_col_ok && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+        u = *reinterpret_cast<const uint4*>(xb + ((long)(pn[i] * a.H + ih) * a.W + iw) * ldx);
+      rbv[i] = u;
+      pk[i] += BKW;
+      pq[i] += BKW;
+      while (pq[i] >= a.Q) {
+        pq[i] -= a.Q;
+        if (++pp[i] >= a.P) { pp[i] = 0; ++pn[i]; }
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < PASSES; ++i) {
+      const int row = rr + RPP * i;
+      lds[buf][row * CPR + (cv ^ swz_tr(row))] = ra[i];
+      lds[buf][(BKW + row) * CPR + (cv ^ swz_tr(row))] = rbv[i];
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = (int)(kt1 - kt0);
+  if (nkt > 0) {
+    gload();
+    sstore(0);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) gload();
+    const uint4* As = &lds[cur][0];
+    const uint4* Bs = &lds[cur][BKW * CPR];
+    if constexpr (kBF) {
+      const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+      bf16x8 af[FM], bfr[FN];
+      auto trfrag = [&](const uint4* base, int col0) -> bf16x8 {
+        const int chunk = (col0 >> 3) + (p >> 1);
+        const int r_a = 8 * g + q, r_b = 8 * g + q + 4;
+        const char* b = reinterpret_cast<const char*>(base);
+        const char* pa = b + r_a * (CPR * 16) + ((chunk ^ swz_tr(r_a)) * 16) + (p & 1) * 8;
+        const char* pb = b + r_b * (CPR * 16) + ((chunk ^ swz_tr(r_b)) * 16) + (p & 1) * 8;
+        s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(pa));
+        s16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(pb));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        s16x8 v = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
+        return *reinterpret_cast<bf16x8*>(&v);
+      };
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = trfrag(As, wm * 64 + i * 16);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = trfrag(Bs, wn * 64 + j * 16);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+      const float* Af = reinterpret_cast<const float*>(As);
+      const float* Bf = reinterpret_cast<const float*>(Bs);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int k = kk * 4 + (lane >> 4);
+        float af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int m = wm * 64 + i * 16 + (lane & 15);
+          af[i] = Af[k * (CPR * 4) + (((m >> 2) ^ swz_tr(k)) << 2) + (m & 3)];
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int n = wn * 64 + j * 16 + (lane & 15);
+          bfr[j] = Bf[k * (CPR * 4) + (((n >> 2) ^ swz_tr(k)) << 2) + (n & 3)];
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nkt) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  float* ws = a.ws + (long)blockIdx.z * a.Cout * a.Ng;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + e;
+      if (m >= a.Cout) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+        if (n < a.Ng) ws[(long)m * a.Ng + n] = acc[i][j][e];
+      }
+    }
+}
+
+// dW[k][c][r][s] (+)= sum_z ws[z][k][(r*S+s)*cin + c]
+__global__ void wgrad_reduce_kernel(const float* ws, int splits, int Cout, int cin, int R, int S,
+                                    float* dw, int dw_c, int accumulate) {
+  const long total = (long)Cout * dw_c * R * S;
+  const long Ng = (long)R * S * cin;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long t = i;
+    const int s = (int)(t % S); t /= S;
+    const int r = (int)(t % R); t /= R;
+    const int c = (int)(t % dw_c); t /= dw_c;
+    const int k = (int)t;
+    const long src = (long)k * Ng + (long)(r * S + s) * cin + c;
+    float v = 0.f;
+    for (int z = 0; z < splits; ++z) v += ws[(long)z * Cout * Ng + src];
+    dw[i] = accumulate ? dw[i] + v : v;
+  }
+}
+
+// fp32 [K][C][R][S] -> T [K][R][S][Cpad] (zero-padded channels) and optionally T [C][R][S][K]
+template <typename T>
+__global__ void pack_weights_kernel(const float* w, int K, int C, int R, int S, int Cpad, T* wk, T* wt) {
+  const long total = (long)K * R * S * Cpad;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long t = i;
+    const int c = (int)(t % Cpad); t /= Cpad;
+    const int s = (int)(t % S); t /= S;
+    const int r = (int)(t % R); t /= R;
+    const int k = (int)t;
+    float v = c < C ? w[(((long)k * C + c) * R + r) * S + s] : 0.f;
+    wk[i] = (T)v;
+    if (wt && c < C) wt[(((long)c * R + r) * S + s) * K + k] = (T)v;
+  }
+}
+
+template <typename T>
+int launch_tn(IgemmArgs a, hipStream_t st) {
+  if (a.M <= 0 || a.Ng <= 0) return 0;
+  dim3 grid(ceil_div(a.M, kBM), 1, 1);
+  if (a.Ng <= 64) {
+    grid.y = ceil_div(a.Ng, 64);
+    hipLaunchKernelGGL((igemm_tn_kernel<T, 64>), grid, dim3(256), 0, st, a);
+  } else {
+    grid.y = ceil_div(a.Ng, 128);
+    hipLaunchKernelGGL((igemm_tn_kernel<T, 128>), grid, dim3(256), 0, st, a);
+  }
+  US_LAUNCH_CHECK("igemm_tn");
+  return 0;
+}
+
+}  // namespace
+
+// =========================================================================================
+// C ABI
+// =========================================================================================
+
+UNETSEG_API int unetseg_conv_tile_m(void) { return kBM; }
+
+// Forward conv.  x = cat([x1 (c1 ch, pixel stride ldc1), x2 (c2 ch, ldc2)], C) NHWC [n,h,w,*];
+// wk: dtype [cout][r][s][c1+c2]; y: NHWC [n,p,q,*] pixel stride ldy.
+// Epilogue: + bias[cout] (fp32, may be NULL), ReLU if relu, and when stats != NULL the per-M-tile
+// BN partials stats[2][cout][ceil(M/128)] (column sum, M2 about the tile mean) of the rounded y.
+UNETSEG_API int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2,
+                                   int n, int h, int w, const void* wk, int cout, int r, int s, int stride,
+                                   int pad, const float* bias, int relu, void* y, int ldy, float* stats,
+                                   void* stream) {
+  US_CHECK_ARG(x1 && wk && y, "conv2d_fwd: null pointer");
+  US_CHECK_ARG((c1 + c2) % 8 == 0 && c1 % 8 == 0, "conv2d_fwd: channels must be multiples of 8 (c1=%d c2=%d)", c1, c2);
+  US_CHECK_ARG(c2 == 0 || x2, "conv2d_fwd: c2>0 needs x2");
+  US_CHECK_ARG(ldc1 % 8 == 0 && (c2 == 0 || ldc2 % 8 == 0) && ldy >= cout, "conv2d_fwd: bad strides");
+  US_CHECK_ARG(dtype == DT_F32 || dtype == DT_BF16, "conv2d_fwd: bad dtype");
+  const int p = (h + 2 * pad - r) / stride + 1, q = (w + 2 * pad - s) / stride + 1;
+  IgemmArgs a{};
+  a.x1 = x1; a.x2 = x2; a.c1 = c1; a.c2 = c2; a.ldc1 = ldc1; a.ldc2 = ldc2;
+  a.N = n; a.H = h; a.W = w; a.hc = p; a.wc = q; a.istride = stride;
+  a.r0 = 0; a.rs = 1; a.nr = r; a.dh0 = -pad; a.dhs = 1;
+  a.s0 = 0; a.ss = 1; a.ns = s; a.dw0 = -pad; a.dws = 1;
+  a.S = s; a.cin = c1 + c2; a.wt = wk; a.ldw = (long)r * s * (c1 + c2); a.Ng = cout;
+  a.ostride = 1; a.ph = 0; a.pw = 0; a.OH = p; a.OW = q;
+  a.y = y; a.ldy = ldy; a.accumulate = 0; a.bias = bias; a.relu = relu;
+  a.M = n * p * q; a.stats = stats; a.stats_ld = ceil_div(a.M, kBM);
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DT_BF16 ? launch_tn<bf16>(a, st) : launch_tn<float>(a, st);
+}
+
+// Data gradient.  dy: NHWC [n,p,q,cout] (pixel stride ldy); wt: dtype [cin][r][s][cout];
+// dx: NHWC [n,h,w,*] pixel stride ldx, written (or added to when accumulate).
+UNETSEG_API int unetseg_conv2d_dgrad(int dtype, const void* dy, int ldy, int n, int p, int q, const void* wt,
+                                     int cout, int cin, int r, int s, int stride, int pad, void* dx, int ldx,
+                                     int h, int w, int accumulate, void* stream) {
+  US_CHECK_ARG(dy && wt && dx, "conv2d_dgrad: null pointer");
+  US_CHECK_ARG(cout % 8 == 0 && ldy % 8 == 0, "conv2d_dgrad: cout/ldy must be multiples of 8");
+  US_CHECK_ARG(stride == 1 || stride == 2, "conv2d_dgrad: stride must be 1 or 2");
+  US_CHECK_ARG(p == (h + 2 * pad - r) / stride + 1 && q == (w + 2 * pad - s) / stride + 1, "conv2d_dgrad: shape mismatch");
+  hipStream_t st = (hipStream_t)stream;
+  for (int ph = 0; ph < stride; ++ph)
+    for (int pw = 0; pw < stride; ++pw) {
+      IgemmArgs a{};
+      a.x1 = dy; a.x2 = nullptr; a.c1 = cout; a.c2 = 0; a.ldc1 = ldy; a.ldc2 = 0;
+      a.N = n; a.H = p; a.W = q; a.istride = 1;
+      a.hc = (h - ph + stride - 1) / stride; a.wc = (w - pw + stride - 1) / stride;
+      if (a.hc <= 0 || a.wc <= 0) continue;
+      a.r0 = (ph + pad) % stride; a.rs = stride; a.nr = (r - a.r0 + stride - 1) / stride;
+      a.dh0 = (ph + pad - a.r0) / stride; a.dhs = -1;
+      a.s0 = (pw + pad) % stride; a.ss = stride; a.ns = (s - a.s0 + stride - 1) / stride;
+      a.dw0 = (pw + pad - a.s0) / stride; a.dws = -1;
+      if (a.nr < 0) a.nr = 0;
+      if (a.ns <= 0) { a.ns = 1; a.nr = 0; }
+      a.S = s; a.cin = cout; a.wt = wt; a.ldw = (long)r * s * cout; a.Ng = cin;
+      a.ostride = stride; a.ph = ph; a.pw = pw; a.OH = h; a.OW = w;
+      a.y = dx; a.ldy = ldx; a.accumulate = accumulate; a.bias = nullptr; a.relu = 0;
+      a.M = n * a.hc * a.wc; a.stats = nullptr;
+      int rc = dtype == DT_BF16 ? launch_tn<bf16>(a, st) : launch_tn<float>(a, st);
+      if (rc) return rc;
+    }
+  return 0;
+}
+
+static int wgrad_splits(int Cout, int Ng, long Kpix, int bkw) {
+  const int tiles = ceil_div(Cout, 128) * ceil_div(Ng, 128);
+  const long nkt = (Kpix + bkw - 1) / bkw;
+  int sp = ceil_div(768, tiles);
+  if (sp < 1) sp = 1;
+  const long max_sp = nkt / 8 > 0 ? nkt / 8 : 1;  // keep >= 8 K steps per split
+  if (sp > max_sp) sp = (int)max_sp;
+  if (sp > 64) sp = 64;
+  return sp;
+}
+
+UNETSEG_API size_t unetseg_conv2d_wgrad_workspace(int dtype, int n, int p, int q, int cout, int cin, int r, int s) {
+  const int bkw = dtype == DT_BF16 ? 32 : 16;
+  const int Ng = r * s * cin;
+  return (size_t)wgrad_splits(cout, Ng, (long)n * p * q, bkw) * cout * Ng * sizeof(float);
+}
+
+// Weight gradient.  x = cat([x1, x2]) NHWC [n,h,w,*]; dy NHWC [n,p,q,cout] (pixel stride ldy);
+// dw: fp32 [cout][dw_c][r][s] (PyTorch layout; dw_c <= c1+c2 drops zero-padded input channels),
+// written or accumulated.  ws: fp32 workspace of
+// unetseg_conv2d_wgrad_workspace() bytes.
+UNETSEG_API int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2,
+                                     int n, int h, int w, const void* dy, int ldy, int cout, int r, int s,
+                                     int stride, int pad, float* ws, size_t ws_bytes, float* dw, int dw_c,
+                                     int accumulate, void* stream) {
+  US_CHECK_ARG(x1 && dy && ws && dw, "conv2d_wgrad: null pointer");
+  US_CHECK_ARG((c1 + c2) % 8 == 0 && c1 % 8 == 0 && cout % 8 == 0 && ldy % 8 == 0, "conv2d_wgrad: channel counts must be multiples of 8");
+  const int p = (h + 2 * pad - r) / stride + 1, q = (w + 2 * pad - s) / stride + 1;
+  const int bkw = dtype == DT_BF16 ? 32 : 16;
+  WgradArgs a{};
+  a.x1 = x1; a.x2 = x2; a.c1 = c1; a.c2 = c2; a.ldc1 = ldc1; a.ldc2 = ldc2;
+  a.N = n; a.H = h; a.W = w; a.P = p; a.Q = q; a.stride = stride; a.pad = pad; a.R = r; a.S = s;
+  a.dy = dy; a.ldy = ldy; a.Cout = cout; a.cin = c1 + c2; a.Ng = r * s * (c1 + c2);
+  a.Kpix = (long)n * p * q;
+  const int splits = wgrad_splits(cout, a.Ng, a.Kpix, bkw);
+  US_CHECK_ARG(ws_bytes >= (size_t)splits * cout * a.Ng * sizeof(float), "conv2d_wgrad: workspace too small");
+  const long nkt = (a.Kpix + bkw - 1) / bkw;
+  a.kt_per_split = (int)((nkt + splits - 1) / splits);
+  a.ws = ws;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(ceil_div(cout, 128), ceil_div(a.Ng, 128), splits);
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, a);
+  US_LAUNCH_CHECK("wgrad");
+  US_CHECK_ARG(dw_c > 0 && dw_c <= a.cin, "conv2d_wgrad: bad dw_c");
+  const long total = (long)cout * dw_c * r * s;
+  int blocks = ceil_div(total, 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, cout, a.cin, r, s, dw, dw_c,
+                     accumulate);
+  US_LAUNCH_CHECK("wgrad_reduce");
+  return 0;
+}
+
+// fp32 [K][C][R][S] -> dtype [K][R][S][Cpad] (+ optional dtype [C][R][S][K] for dgrad)
+UNETSEG_API int unetseg_pack_conv_weight(int dtype, const float* w, int K, int C, int R, int S, int Cpad, void* wk,
+                                         void* wt, void* stream) {
+  US_CHECK_ARG(w && wk && Cpad >= C, "pack_conv_weight: bad args");
+  const long total = (long)K * R * S * Cpad;
+  int blocks = ceil_div(total, 256);
+  if (blocks > 8192) blocks = 8192;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(pack_weights_kernel<bf16>, dim3(blocks), dim3(256), 0, st, w, K, C, R, S, Cpad, (bf16*)wk, (bf16*)wt);
+  else
+    hipLaunchKernelGGL(pack_weights_kernel<float>, dim3(blocks), dim3(256), 0, st, w, K, C, R, S, Cpad, (float*)wk, (float*)wt);
+  US_LAUNCH_CHECK("pack_weights");
+  return 0;
+}

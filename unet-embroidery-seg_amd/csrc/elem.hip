@@ -1,0 +1,1101 @@
+// Memory-bound NHWC kernels of the U-Net hot path: BatchNorm (train/eval), ReLU, residual add,
+// max-pool, bilinear x2 upsample, input packing, small-Cout 1x1 convs and the attention gate.
+//
+// Reference ops replaced:
+//   BatchNorm2d      model/resnet_backbone.py:64-70,127,169  model/unet_plain.py:10,13
+//                    model/unet_attention.py:17,21,25
+//   ReLU / residual  model/resnet_backbone.py:95,100,110,113  model/unet_resnet.py:37,40,73,75
+//   MaxPool2d        model/resnet_backbone.py:131 (3x3/s2 ceil)  model/unet_plain.py:25 (2x2)
+//   Upsample x2      model/unet_resnet.py:21,71 (align_corners=True)  model/unet_plain.py:36 (False)
+//   AttentionGate    model/unet_attention.py:30-35
+//
+// Layout: activations NHWC with an explicit pixel stride ("ld", elements) so channel slices of a
+// concat buffer are addressed in place.  Element type T is bf16 or fp32; all arithmetic is fp32.
+// Every per-channel reduction is two-stage (per-block partials -> finalize) and deterministic.
+#include "common.h"
+
+namespace {
+
+template <typename T>
+constexpr int VE = 16 / sizeof(T);
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm finalize (train): partials [2][C][G] = (sum, M2 about the tile mean) with tile
+// count min(tile, M - g*tile).  Chan's parallel merge in fp64.  Updates running stats exactly as
+// nn.BatchNorm2d (momentum 0.1, unbiased running var) and emits scale/shift for the apply pass.
+// ------------------------------------------------------------------------------------------
+__global__ void bn_finalize_kernel(const float* part, int C, int G, long M, int tile, const float* gamma,
+                                   const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
+                                   float eps, float* mean_out, float* invstd_out, float* scale, float* shift) {
+  __shared__ double sc[16];
+  const int c = blockIdx.x;
+  const float* s = part + (long)c * G;
+  const float* q = part + ((long)C + c) * G;
+  double tsum = 0.0;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) tsum += s[g];
+  tsum = block_sum(tsum, sc);
+  const double mean = tsum / (double)M;
+  double m2 = 0.0;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    const long cnt = min((long)tile, M - (long)g * tile);
+    const double mg = (double)s[g] / (double)cnt;
+    m2 += (double)q[g] + (double)cnt * (mg - mean) * (mg - mean);
+  }
+  m2 = block_sum(m2, sc);
+  if (threadIdx.x == 0) {
+    const double var = m2 / (double)M;
+    const double inv = 1.0 / sqrt(var + (double)eps);
+    mean_out[c] = (float)mean;
+    invstd_out[c] = (float)inv;
+    const float sca = (float)(gamma[c] * inv);
+    scale[c] = sca;
+    shift[c] = (float)(beta[c] - mean * gamma[c] * inv);
+    if (rmean) {
+      const double unb = M > 1 ? m2 / (double)(M - 1) : var;
+      rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+      rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+    }
+    if (nbt && c == 0) nbt[0] += 1;
+  }
+}
+
+__global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                               float eps, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = 1.0f / sqrtf(rvar[c] + eps);
+  scale[c] = gamma[c] * inv;
+  shift[c] = beta[c] - rmean[c] * gamma[c] * inv;
+}
+
+// out = act(y*sc + sh + res); res: 0 none, 1 raw tensor r, 2 r*sc2 + sh2
+template <typename T>
+__global__ void bn_apply_kernel(const T* y, int ldy, const float* sc, const float* sh, const T* r, int ldr,
+                                const float* sc2, const float* sh2, int res_mode, int relu, T* out, int ldo, long M,
+                                int C) {
+  constexpr int V = VE<T>;
+  const int cv = C / V;
+  const long total = M * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long pix = i / cv;
+    const int c0 = (int)(i - pix * cv) * V;
+    float v[V], rv[V];
+    load_vec(y + pix * ldy + c0, v);
+#pragma unroll
+    for (int e = 0; e < V; ++e) v[e] = v[e] * sc[c0 + e] + sh[c0 + e];
+    if (res_mode) {
+      load_vec(r + pix * ldr + c0, rv);
+      if (res_mode == 2) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) rv[e] = rv[e] * sc2[c0 + e] + sh2[c0 + e];
+      }
+#pragma unroll
+      for (int e = 0; e < V; ++e) v[e] += rv[e];
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    store_vec(out + pix * ldo + c0, v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm backward, pass 1: per-(channel, pixel tile) partials of
+//   sum dz, sum dz*xhat1, sum dz*xhat2     where dz = dA * (A > 0 if A else 1)
+// Block = tv channel-vectors x rows pixels; grid = (pixel tiles, channel groups).
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void bn_bwd_reduce_kernel(const T* dA, int ldd, const T* A, int lda, const T* y1, int ld1,
+                                     const float* mean1, const float* inv1, const T* y2, int ld2,
+                                     const float* mean2, const float* inv2, long M, int C, int tv, int pix_per_block,
+                                     float* part, int G) {
+  constexpr int V = VE<T>;
+  __shared__ float red[3][256][V];
+  const int tx = threadIdx.x % tv, ty = threadIdx.x / tv, rows = blockDim.x / tv;
+  const int c0 = (blockIdx.y * tv + tx) * V;
+  const long p0 = (long)blockIdx.x * pix_per_block;
+  const long p1 = min(M, p0 + pix_per_block);
+  float s0[V], s1[V], s2[V], m1[V], i1[V], m2v[V], i2v[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    s0[e] = s1[e] = s2[e] = 0.f;
+    m1[e] = mean1[c0 + e];
+    i1[e] = inv1[c0 + e];
+    m2v[e] = y2 ? mean2[c0 + e] : 0.f;
+    i2v[e] = y2 ? inv2[c0 + e] : 0.f;
+  }
+  for (long p = p0 + ty; p < p1; p += rows) {
+    float d[V], a[V], x[V];
+    load_vec(dA + p * ldd + c0, d);
+    if (A) {
+      load_vec(A + p * lda + c0, a);
+#pragma unroll
+      for (int e = 0; e < V; ++e) d[e] = a[e] > 0.f ? d[e] : 0.f;
+    }
+    load_vec(y1 + p * ld1 + c0, x);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      s0[e] += d[e];
+      s1[e] += d[e] * (x[e] - m1[e]) * i1[e];
+    }
+    if (y2) {
+      load_vec(y2 + p * ld2 + c0, x);
+#pragma unroll
+      for (int e = 0; e < V; ++e) s2[e] += d[e] * (x[e] - m2v[e]) * i2v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    red[0][threadIdx.x][e] = s0[e];
+    red[1][threadIdx.x][e] = s1[e];
+    red[2][threadIdx.x][e] = s2[e];
+  }
+  __syncthreads();
+  if (ty == 0) {
+    for (int r = 1; r < rows; ++r)
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        s0[e] += red[0][r * tv + tx][e];
+        s1[e] += red[1][r * tv + tx][e];
+        s2[e] += red[2][r * tv + tx][e];
+      }
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      part[((long)0 * C + c0 + e) * G + blockIdx.x] = s0[e];
+      part[((long)1 * C + c0 + e) * G + blockIdx.x] = s1[e];
+      part[((long)2 * C + c0 + e) * G + blockIdx.x] = s2[e];
+    }
+  }
+}
+
+// pass 2: coefficients.  For branch b (1 or 2): dgamma_b += sum dz*xhat_b, dbeta_b += sum dz;
+// coef[b][0][c] = gamma_b*invstd_b, coef[b][1][c] = mean(dz), coef[b][2][c] = mean(dz*xhat_b)
+__global__ void bn_bwd_finalize_kernel(const float* part, int C, int G, long M, int nbranch, const float* g1,
+                                       const float* inv1, float* dg1, float* db1, const float* g2, const float* inv2,
+                                       float* dg2, float* db2, float* coef) {
+  __shared__ double sc[16];
+  const int c = blockIdx.x;
+  double t[3] = {0, 0, 0};
+  for (int k = 0; k < 1 + nbranch; ++k) {
+    double acc = 0.0;
+    for (int g = threadIdx.x; g < G; g += blockDim.x) acc += part[((long)k * C + c) * G + g];
+    t[k] = block_sum(acc, sc);
+  }
+  if (threadIdx.x == 0) {
+    const double sdz = t[0];
+    dg1[c] += (float)t[1];
+    db1[c] += (float)sdz;
+    coef[0 * C + c] = g1[c] * inv1[c];
+    coef[1 * C + c] = (float)(sdz / (double)M);
+    coef[2 * C + c] = (float)(t[1] / (double)M);
+    if (nbranch == 2) {
+      dg2[c] += (float)t[2];
+      db2[c] += (float)sdz;
+      coef[3 * C + c] = g2[c] * inv2[c];
+      coef[4 * C + c] = (float)(sdz / (double)M);
+      coef[5 * C + c] = (float)(t[2] / (double)M);
+    }
+  }
+}
+
+// pass 3: dy_b = coef_a*(dz - mean(dz) - xhat_b*mean(dz*xhat_b)); optional dzout (+)= dz
+template <typename T>
+__global__ void bn_bwd_apply_kernel(const T* dA, int ldd, const T* A, int lda, const T* y1, int ld1,
+                                    const float* mean1, const float* inv1, T* dy1, int ldo1, const T* y2, int ld2,
+                                    const float* mean2, const float* inv2, T* dy2, int ldo2, const float* coef,
+                                    T* dzout, int ldz, int dz_acc, long M, int C) {
+  constexpr int V = VE<T>;
+  const int cv = C / V;
+  const long total = M * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long pix = i / cv;
+    const int c0 = (int)(i - pix * cv) * V;
+    float d[V], a[V], x[V], o[V];
+    load_vec(dA + pix * ldd + c0, d);
+    if (A) {
+      load_vec(A + pix * lda + c0, a);
+#pragma unroll
+      for (int e = 0; e < V; ++e) d[e] = a[e] > 0.f ? d[e] : 0.f;
+    }
+    load_vec(y1 + pix * ld1 + c0, x);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int c = c0 + e;
+      const float xh = (x[e] - mean1[c]) * inv1[c];
+      o[e] = coef[c] * (d[e] - coef[C + c] - xh * coef[2 * C + c]);
+    }
+    store_vec(dy1 + pix * ldo1 + c0, o);
+    if (y2) {
+      load_vec(y2 + pix * ld2 + c0, x);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int c = c0 + e;
+        const float xh = (x[e] - mean2[c]) * inv2[c];
+        o[e] = coef[3 * C + c] * (d[e] - coef[4 * C + c] - xh * coef[5 * C + c]);
+      }
+      store_vec(dy2 + pix * ldo2 + c0, o);
+    }
+    if (dzout) {
+      if (dz_acc) {
+        load_vec(dzout + pix * ldz + c0, o);
+#pragma unroll
+        for (int e = 0; e < V; ++e) o[e] += d[e];
+        store_vec(dzout + pix * ldz + c0, o);
+      } else {
+        store_vec(dzout + pix * ldz + c0, d);
+      }
+    }
+  }
+}
+
+// dY = dA * (A > 0) and per-tile column sums of dY (bias gradient partials [C][G])
+template <typename T>
+__global__ void relu_bwd_bias_kernel(const T* dA, int ldd, const T* A, int lda, T* dY, int ldy, long M, int C, int tv,
+                                     int pix_per_block, float* part, int G) {
+  constexpr int V = VE<T>;
+  __shared__ float red[256][V];
+  const int tx = threadIdx.x % tv, ty = threadIdx.x / tv, rows = blockDim.x / tv;
+  const int c0 = (blockIdx.y * tv + tx) * V;
+  const long p0 = (long)blockIdx.x * pix_per_block;
+  const long p1 = min(M, p0 + pix_per_block);
+  float s[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) s[e] = 0.f;
+  for (long p = p0 + ty; p < p1; p += rows) {
+    float d[V], a[V];
+    load_vec(dA + p * ldd + c0, d);
+    load_vec(A + p * lda + c0, a);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      d[e] = a[e] > 0.f ? d[e] : 0.f;
+    }
+    // round like the stored gradient so db == sum of the dY actually fed to wgrad
+    T tmp[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      tmp[e] = (T)d[e];
+      s[e] += (float)tmp[e];
+    }
+    *reinterpret_cast<uint4*>(dY + p * ldy + c0) = *reinterpret_cast<uint4*>(tmp);
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) red[threadIdx.x][e] = s[e];
+  __syncthreads();
+  if (ty == 0) {
+    for (int r = 1; r < rows; ++r)
+#pragma unroll
+      for (int e = 0; e < V; ++e) s[e] += red[r * tv + tx][e];
+#pragma unroll
+    for (int e = 0; e < V; ++e) part[(long)(c0 + e) * G + blockIdx.x] = s[e];
+  }
+}
+
+// out[c] (+)= sum_g part[c][g]   (fp64 accumulation, fixed order)
+__global__ void colsum_finalize_kernel(const float* part, int C, int G, float* out, int accumulate) {
+  __shared__ double sc[16];
+  const int c = blockIdx.x;
+  double acc = 0.0;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) acc += part[(long)c * G + g];
+  acc = block_sum(acc, sc);
+  if (threadIdx.x == 0) out[c] = accumulate ? out[c] + (float)acc : (float)acc;
+}
+
+// ------------------------------------------------------------------------------------------
+// Max pool (pad 0), NHWC.  idx = argmax position inside the k x k window (first max wins, the
+// scan order of ATen's CPU kernel), stored as uint8.
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void maxpool_fwd_kernel(const T* x, int ldx, int N, int H, int W, int C, int k, int s, int P, int Q, T* y,
+                                   int ldy, uint8_t* idx) {
+  constexpr int V = VE<T>;
+  const int cv = C / V;
+  const long total = (long)N * P * Q * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long t = i;
+    const int v = (int)(t % cv); t /= cv;
+    const int q = (int)(t % Q); t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    const int c0 = v * V;
+    float best[V];
+    uint8_t bi[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int r = 0; r < k; ++r) {
+      const int h = p * s + r;
+      if (h >= H) break;
+      for (int u = 0; u < k; ++u) {
+        const int w = q * s + u;
+        if (w >= W) break;
+        float xv[V];
+        load_vec(x + ((long)(n * H + h) * W + w) * ldx + c0, xv);
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          if (xv[e] > best[e] || isnan(xv[e])) {
+            if (!isnan(best[e])) { best[e] = xv[e]; bi[e] = (uint8_t)(r * k + u); }
+          }
+      }
+    }
+    const long opix = ((long)(n * P + p) * Q + q);
+    store_vec(y + opix * ldy + c0, best);
+#pragma unroll
+    for (int e = 0; e < V; ++e) idx[opix * C + c0 + e] = bi[e];
+  }
+}
+
+// gather form: dx[h][w] (+)= sum over windows containing (h,w) whose argmax is (h,w)
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* dy, int ldy, const uint8_t* idx, int N, int H, int W, int C, int k, int s,
+                                   int P, int Q, T* dx, int ldx, int accumulate) {
+  constexpr int V = VE<T>;
+  const int cv = C / V;
+  const long total = (long)N * H * W * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long t = i;
+    const int v = (int)(t % cv); t /= cv;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    const int c0 = v * V;
+    float acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = 0.f;
+    const int plo = max(0, (h - k + s) / s), phi = min(P - 1, h / s);
+    const int qlo = max(0, (w - k + s) / s), qhi = min(Q - 1, w / s);
+    for (int p = plo; p <= phi; ++p) {
+      const int r = h - p * s;
+      if (r < 0 || r >= k) continue;
+      for (int q = qlo; q <= qhi; ++q) {
+        const int u = w - q * s;
+        if (u < 0 || u >= k) continue;
+        const long opix = ((long)(n * P + p) * Q + q);
+        const uint8_t want = (uint8_t)(r * k + u);
+        float g[V];
+        load_vec(dy + opix * ldy + c0, g);
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          if (idx[opix * C + c0 + e] == want) acc[e] += g[e];
+      }
+    }
+    T* o = dx + ((long)(n * H + h) * W + w) * ldx + c0;
+    if (accumulate) {
+      float old[V];
+      load_vec(o, old);
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] += old[e];
+    }
+    store_vec(o, acc);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Bilinear x2 upsample, NHWC.  align_corners=True: src = dst*(in-1)/(out-1);
+// False: src = max((dst+0.5)/2 - 0.5, 0)  (ATen area_pixel_compute_source_index, scale 0.5)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void up_src(int d, int in, int out, int align, int& i0, int& i1, float& l1) {
+  float src;
+  if (align) {
+    const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;  // ATen area_pixel_compute_scale
+    src = scale * (float)d;
+  } else {
+    src = ((float)d + 0.5f) * 0.5f - 0.5f;
+    if (src < 0.f) src = 0.f;
+  }
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + 1 < in ? i0 + 1 : in - 1;
+  l1 = src - (float)i0;
+}
+
+template <typename T>
+__global__ void upsample_fwd_kernel(const T* x, int ldx, int N, int H, int W, int C, int align, T* y, int ldy) {
+  constexpr int V = VE<T>;
+  const int cv = C / V, OH = 2 * H, OW = 2 * W;
+  const long total = (long)N * OH * OW * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long t = i;
+    const int v = (int)(t % cv); t /= cv;
+    const int ow = (int)(t % OW); t /= OW;
+    const int oh = (int)(t % OH);
+    const int n = (int)(t / OH);
+    int h0, h1, w0, w1;
+    float lh, lw;
+    up_src(oh, H, OH, align, h0, h1, lh);
+    up_src(ow, W, OW, align, w0, w1, lw);
+    const int c0 = v * V;
+    float a[V], b[V], c[V], d[V], o[V];
+    const long base = (long)n * H * W;
+    load_vec(x + (base + (long)h0 * W + w0) * ldx + c0, a);
+    load_vec(x + (base + (long)h0 * W + w1) * ldx + c0, b);
+    load_vec(x + (base + (long)h1 * W + w0) * ldx + c0, c);
+    load_vec(x + (base + (long)h1 * W + w1) * ldx + c0, d);
+    const float hl0 = 1.f - lh, wl0 = 1.f - lw;
+#pragma unroll
+    for (int e = 0; e < V; ++e) o[e] = hl0 * (wl0 * a[e] + lw * b[e]) + lh * (wl0 * c[e] + lw * d[e]);
+    store_vec(y + ((long)(n * OH + oh) * OW + ow) * ldy + c0, o);
+  }
+}
+
+// weight of output index d on input index i along one axis
+__device__ __forceinline__ float up_w(int d, int i, int in, int out, int align) {
+  int i0, i1;
+  float l1;
+  up_src(d, in, out, align, i0, i1, l1);
+  float w = 0.f;
+  if (i0 == i) w += 1.f - l1;
+  if (i1 == i) w += l1;
+  return w;
+}
+
+// gather form of the adjoint: dx[h][w] (+)= sum_{oh,ow} wh(oh,h) ww(ow,w) dy[oh][ow]
+template <typename T>
+__global__ void upsample_bwd_kernel(const T* dy, int ldy, int N, int H, int W, int C, int align, T* dx, int ldx,
+                                    int accumulate) {
+  constexpr int V = VE<T>;
+  const int cv = C / V, OH = 2 * H, OW = 2 * W;
+  const long total = (long)N * H * W * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long t = i;
+    const int v = (int)(t % cv); t /= cv;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    const int c0 = v * V;
+    // candidate output ranges (a superset; exact weights decide)
+    int ohl, ohh, owl, owh;
+    if (align) {
+      ohl = H > 1 ? (int)floorf((float)(h - 1) * (OH - 1) / (float)(H - 1)) : 0;
+      ohh = H > 1 ? (int)ceilf((float)(h + 1) * (OH - 1) / (float)(H - 1)) : OH - 1;
+      owl = W > 1 ? (int)floorf((float)(w - 1) * (OW - 1) / (float)(W - 1)) : 0;
+      owh = W > 1 ? (int)ceilf((float)(w + 1) * (OW - 1) / (float)(W - 1)) : OW - 1;
+    } else {
+      ohl = 2 * h - 2; ohh = 2 * h + 2;
+      owl = 2 * w - 2; owh = 2 * w + 2;
+      if (h == H - 1) ohh = OH - 1;
+      if (w == W - 1) owh = OW - 1;
+    }
+    ohl = max(ohl, 0); owl = max(owl, 0);
+    ohh = min(ohh, OH - 1); owh = min(owh, OW - 1);
+    float acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = 0.f;
+    for (int oh = ohl; oh <= ohh; ++oh) {
+      const float wh = up_w(oh, h, H, OH, align);
+      if (wh == 0.f) continue;
+      for (int ow = owl; ow <= owh; ++ow) {
+        const float ww = up_w(ow, w, W, OW, align);
+        if (ww == 0.f) continue;
+        float g[V];
+        load_vec(dy + ((long)(n * OH + oh) * OW + ow) * ldy + c0, g);
+        const float wt = wh * ww;
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] += wt * g[e];
+      }
+    }
+    T* o = dx + ((long)(n * H + h) * W + w) * ldx + c0;
+    if (accumulate) {
+      float old[V];
+      load_vec(o, old);
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] += old[e];
+    }
+    store_vec(o, acc);
+  }
+}
+
+// NCHW fp32 [N][3][H][W] -> NHWC T [N][H][W][Cpad] (zero padded)
+template <typename T>
+__global__ void pack_input_kernel(const float* x, int N, int C, int H, int W, int Cpad, T* y) {
+  const long total = (long)N * H * W;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / ((long)H * W), hw = i - n * H * W;
+    T* o = y + i * Cpad;
+    for (int c = 0; c < Cpad; ++c) o[c] = (T)(c < C ? x[(n * C + c) * (long)H * W + hw] : 0.f);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// 1x1 conv with tiny Cout (final 64->2, seg_head 64->1, attention psi inter->1).
+// Forward: one wave per 64/ (C/V) pixels; output fp32 planar [N][K][HW] (== [M] for K=1);
+// optional BN partial stats of channel 0 per block (for psi: [2][1][G], tile = pixels/block).
+// ------------------------------------------------------------------------------------------
+template <typename T, int K>
+__global__ void pw_small_fwd_kernel(const T* x, int ldx, long M, int HW, int C, const float* w, const float* b,
+                                    float* y, float* stats, int pix_per_block) {
+  constexpr int V = VE<T>;
+  __shared__ double sred[16];
+  const int cv = C / V;  // lanes per pixel (C/V <= 64, power of two)
+  const int ppw = 64 / cv;  // pixels per wave pass
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int sub = lane / cv, v = lane % cv;
+  const long p0 = (long)blockIdx.x * pix_per_block;
+  const long p1 = min(M, p0 + pix_per_block);
+  float wv[K][V];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int e = 0; e < V; ++e) wv[k][e] = w[k * C + v * V + e];
+  double lsum = 0.0;
+  // pass 1: outputs
+  for (long pbase = p0 + (long)wid * ppw; pbase < p1; pbase += (long)nw * ppw) {
+    const long p = pbase + sub;
+    float xv[V];
+    float acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.f;
+    if (p < p1) {
+      load_vec(x + p * ldx + v * V, xv);
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[k] += xv[e] * wv[k][e];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      for (int o = 1; o < cv; o <<= 1) acc[k] += __shfl_xor(acc[k], o, 64);
+    if (p < p1 && v == 0) {
+      const long n = p / HW, hw = p - n * HW;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float val = acc[k] + (b ? b[k] : 0.f);
+        y[(n * K + k) * HW + hw] = val;
+        if (k == 0) lsum += val;
+      }
+    }
+  }
+  if (!stats) return;
+  const double tot = block_sum(lsum, sred);
+  const long cnt = p1 - p0;
+  const double mean = tot / (double)cnt;
+  __syncthreads();
+  double lm2 = 0.0;
+  for (long p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+    const long n = p / HW, hw = p - n * HW;
+    const double d = (double)y[(n * K) * HW + hw] - mean;
+    lm2 += d * d;
+  }
+  const double m2 = block_sum(lm2, sred);
+  if (threadIdx.x == 0) {
+    stats[blockIdx.x] = (float)tot;
+    stats[gridDim.x + blockIdx.x] = (float)m2;
+  }
+}
+
+// Backward of the tiny-Cout 1x1 conv.  dy fp32 planar [N][K][HW].
+//   dx (+)= dy . W  (T, NHWC, ld), partials for dW [K][C][G] and db [K][G]
+template <typename T, int K>
+__global__ void pw_small_bwd_kernel(const float* dy, const T* x, int ldx, long M, int HW, int C, const float* w,
+                                    T* dx, int lddx, int dx_acc, float* part_w, float* part_b, int G,
+                                    int pix_per_block) {
+  constexpr int V = VE<T>;
+  __shared__ float red[256][V];
+  __shared__ float redb[256];
+  const int cv = C / V;
+  const int tv = cv, rows = blockDim.x / tv;
+  const int tx = threadIdx.x % tv, ty = threadIdx.x / tv;
+  const int c0 = tx * V;
+  const long p0 = (long)blockIdx.x * pix_per_block;
+  const long p1 = min(M, p0 + pix_per_block);
+  float wv[K][V];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int e = 0; e < V; ++e) wv[k][e] = w[k * C + c0 + e];
+  float sw[K][V], sb[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    sb[k] = 0.f;
+#pragma unroll
+    for (int e = 0; e < V; ++e) sw[k][e] = 0.f;
+  }
+  for (long p = p0 + ty; p < p1; p += rows) {
+    const long n = p / HW, hw = p - n * HW;
+    float g[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) g[k] = dy[(n * K + k) * HW + hw];
+    float xv[V], o[V];
+    load_vec(x + p * ldx + c0, xv);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        s += g[k] * wv[k][e];
+        sw[k][e] += g[k] * xv[e];
+      }
+      o[e] = s;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) sb[k] += g[k];
+    if (dx) {
+      T* dp = dx + p * lddx + c0;
+      if (dx_acc) {
+        float old[V];
+        load_vec(dp, old);
+#pragma unroll
+        for (int e = 0; e < V; ++e) o[e] += old[e];
+      }
+      store_vec(dp, o);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < V; ++e) red[threadIdx.x][e] = sw[k][e];
+    redb[threadIdx.x] = sb[k];
+    __syncthreads();
+    if (ty == 0) {
+      float s[V];
+      float bs = 0.f;
+#pragma unroll
+      for (int e = 0; e < V; ++e) s[e] = 0.f;
+      for (int r = 0; r < rows; ++r) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) s[e] += red[r * tv + tx][e];
+        bs += redb[r * tv + tx];
+      }
+#pragma unroll
+      for (int e = 0; e < V; ++e) part_w[((long)k * C + c0 + e) * G + blockIdx.x] = s[e];
+      if (tx == 0) part_b[(long)k * G + blockIdx.x] = bs;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Attention gate (model/unet_attention.py:30-35):
+//   alpha = sigmoid(psi*sc + sh) (per pixel), gated = skip * alpha
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void attn_apply_kernel(const T* skip, int lds_, const float* psi, const float* sc, const float* sh,
+                                  float* alpha, T* gated, int ldg, long M, int C) {
+  constexpr int V = VE<T>;
+  const int cv = C / V;
+  const long total = M * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / cv;
+    const int c0 = (int)(i - p * cv) * V;
+    const float z = psi[p] * sc[0] + sh[0];
+    const float al = 1.f / (1.f + expf(-z));
+    if (c0 == 0) alpha[p] = al;
+    float v[V];
+    load_vec(skip + p * lds_ + c0, v);
+#pragma unroll
+    for (int e = 0; e < V; ++e) v[e] *= al;
+    store_vec(gated + p * ldg + c0, v);
+  }
+}
+
+// backward 1: d_skip (+)= dg * alpha ; dpsibn[p] = (sum_c dg*skip) * alpha*(1-alpha);
+// partials [2][1][G]: sum dpsibn, sum dpsibn * xhat(psi)
+template <typename T>
+__global__ void attn_bwd1_kernel(const T* dg, int ldg, const T* skip, int lds_, const float* alpha, const float* psi,
+                                 const float* mean, const float* inv, T* dskip, int ldds, int ds_acc, float* dpsibn,
+                                 long M, int C, int pix_per_block, float* part, int G) {
+  constexpr int V = VE<T>;
+  __shared__ double sred[16];
+  const int cvt = C / V;                 // vectors per pixel
+  const int cv = cvt < 64 ? cvt : 64;    // lanes per pixel (power of two)
+  const int nchunk = cvt / cv;
+  const int ppw = 64 / cv;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int sub = lane / cv, v = lane % cv;
+  const long p0 = (long)blockIdx.x * pix_per_block;
+  const long p1 = min(M, p0 + pix_per_block);
+  double s0 = 0.0, s1 = 0.0;
+  for (long pbase = p0 + (long)wid * ppw; pbase < p1; pbase += (long)nw * ppw) {
+    const long p = pbase + sub;
+    float dot = 0.f;
+    float al = 0.f;
+    if (p < p1) {
+      al = alpha[p];
+      for (int ch = 0; ch < nchunk; ++ch) {
+        const int c0 = (ch * cv + v) * V;
+        float g[V], sk[V], o[V];
+        load_vec(dg + p * ldg + c0, g);
+        load_vec(skip + p * lds_ + c0, sk);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          dot += g[e] * sk[e];
+          o[e] = g[e] * al;
+        }
+        T* dp = dskip + p * ldds + c0;
+        if (ds_acc) {
+          float old[V];
+          load_vec(dp, old);
+#pragma unroll
+          for (int e = 0; e < V; ++e) o[e] += old[e];
+        }
+        store_vec(dp, o);
+      }
+    }
+    for (int o = 1; o < cv; o <<= 1) dot += __shfl_xor(dot, o, 64);
+    if (p < p1 && v == 0) {
+      const float d = dot * al * (1.f - al);
+      dpsibn[p] = d;
+      s0 += d;
+      s1 += (double)d * (psi[p] - mean[0]) * inv[0];
+    }
+  }
+  s0 = block_sum(s0, sred);
+  s1 = block_sum(s1, sred);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = (float)s0;
+    part[G + blockIdx.x] = (float)s1;
+  }
+}
+
+// backward 2: dpsi = coef0*(dpsibn - coef1 - xhat*coef2); dz_f = dpsi * w_psi * (f > 0);
+// partials: dW_psi [C][G] = sum dpsi * f, db_psi [G] = sum dpsi
+template <typename T>
+__global__ void attn_bwd2_kernel(const float* dpsibn, const float* psi, const float* mean, const float* inv,
+                                 const float* coef, const T* f, int ldf, const float* wpsi, T* dzf, int lddz, long M,
+                                 int C, int tv, int pix_per_block, float* part_w, float* part_b, int G) {
+  constexpr int V = VE<T>;
+  __shared__ float red[256][V];
+  __shared__ float redb[256];
+  const int tx = threadIdx.x % tv, ty = threadIdx.x / tv, rows = blockDim.x / tv;
+  const int c0 = tx * V;
+  const long p0 = (long)blockIdx.x * pix_per_block;
+  const long p1 = min(M, p0 + pix_per_block);
+  float wv[V], sw[V];
+  float sb = 0.f;
+#pragma unroll
+  for (int e = 0; e < V; ++e) { wv[e] = wpsi[c0 + e]; sw[e] = 0.f; }
+  for (long p = p0 + ty; p < p1; p += rows) {
+    const float xh = (psi[p] - mean[0]) * inv[0];
+    const float dp = coef[0] * (dpsibn[p] - coef[1] - xh * coef[2]);
+    float fv[V], o[V];
+    load_vec(f + p * ldf + c0, fv);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      sw[e] += dp * fv[e];
+      o[e] = fv[e] > 0.f ? dp * wv[e] : 0.f;
+    }
+    if (tx == 0) sb += dp;
+    store_vec(dzf + p * lddz + c0, o);
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) red[threadIdx.x][e] = sw[e];
+  redb[threadIdx.x] = sb;
+  __syncthreads();
+  if (ty == 0) {
+    float s[V];
+    float bs = 0.f;
+#pragma unroll
+    for (int e = 0; e < V; ++e) s[e] = 0.f;
+    for (int r = 0; r < rows; ++r) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) s[e] += red[r * tv + tx][e];
+      bs += redb[r * tv + tx];
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) part_w[(long)(c0 + e) * G + blockIdx.x] = s[e];
+    if (tx == 0) part_b[blockIdx.x] = bs;
+  }
+}
+
+// elementwise add of NHWC tensors: out (+)= x
+template <typename T>
+__global__ void add_kernel(const T* x, int ldx, T* out, int ldo, long M, int C) {
+  constexpr int V = VE<T>;
+  const int cv = C / V;
+  const long total = M * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / cv;
+    const int c0 = (int)(i - p * cv) * V;
+    float a[V], b[V];
+    load_vec(x + p * ldx + c0, a);
+    load_vec(out + p * ldo + c0, b);
+#pragma unroll
+    for (int e = 0; e < V; ++e) b[e] += a[e];
+    store_vec(out + p * ldo + c0, b);
+  }
+}
+
+inline int grid_for(long work, int per_block = 256, int cap = 16384) {
+  long b = (work + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (int)b;
+}
+
+inline int pow2_le(int v, int cap) {
+  int t = 1;
+  while (t * 2 <= v && t * 2 <= cap && v % (t * 2) == 0) t *= 2;
+  return t;
+}
+
+}  // namespace
+
+// =========================================================================================
+// C ABI
+// =========================================================================================
+#define DISPATCH_T(dtype, ...)            \
+  do {                                    \
+    if ((dtype) == DT_BF16) {             \
+      typedef bf16 T;                     \
+      __VA_ARGS__;                        \
+    } else {                              \
+      typedef float T;                    \
+      __VA_ARGS__;                        \
+    }                                     \
+  } while (0)
+
+#define CHECK_VEC(dtype, C, name) \
+  US_CHECK_ARG((C) % ((dtype) == DT_BF16 ? 8 : 4) == 0, "%s: channels (%d) must be a multiple of the 16-B vector", name, (int)(C))
+
+UNETSEG_API int unetseg_bn_finalize(const float* part, int C, int G, long M, int tile, const float* gamma,
+                                    const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
+                                    float eps, float* mean, float* invstd, float* scale, float* shift, void* stream) {
+  US_CHECK_ARG(part && gamma && beta && mean && invstd && scale && shift && M > 0, "bn_finalize: bad args");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, C, G, M, tile, gamma, beta,
+                     rmean, rvar, nbt, momentum, eps, mean, invstd, scale, shift);
+  US_LAUNCH_CHECK("bn_finalize");
+  return 0;
+}
+
+UNETSEG_API int unetseg_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rmean,
+                                       const float* rvar, float eps, float* scale, float* shift, void* stream) {
+  hipLaunchKernelGGL(bn_eval_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, (hipStream_t)stream, C, gamma, beta, rmean,
+                     rvar, eps, scale, shift);
+  US_LAUNCH_CHECK("bn_eval");
+  return 0;
+}
+
+UNETSEG_API int unetseg_bn_apply(int dtype, const void* y, int ldy, const float* sc, const float* sh, const void* r,
+                                 int ldr, const float* sc2, const float* sh2, int res_mode, int relu, void* out,
+                                 int ldo, long M, int C, void* stream) {
+  CHECK_VEC(dtype, C, "bn_apply");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(M * C / VE<T>)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)y, ldy, sc, sh, (const T*)r, ldr, sc2, sh2,
+                                       res_mode, relu, (T*)out, ldo, M, C));
+  US_LAUNCH_CHECK("bn_apply");
+  return 0;
+}
+
+// geometry of the channel-reduction kernels (also used by the host to size partial buffers)
+UNETSEG_API int unetseg_reduce_tiles(int dtype, long M, int C, int* tv_out, int* ppb_out) {
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  const int cv = C / V;
+  const int tv = pow2_le(cv, 64);
+  const int rows = 256 / tv;
+  int ppb = rows * 16;
+  if (ppb < 256) ppb = 256;
+  if (tv_out) *tv_out = tv;
+  if (ppb_out) *ppb_out = ppb;
+  return ceil_div(M, ppb);
+}
+
+UNETSEG_API int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const void* A, int lda, const void* y1,
+                                      int ld1, const float* mean1, const float* inv1, const void* y2, int ld2,
+                                      const float* mean2, const float* inv2, long M, int C, float* part, int G,
+                                      void* stream) {
+  CHECK_VEC(dtype, C, "bn_bwd_reduce");
+  int tv, ppb;
+  const int g = unetseg_reduce_tiles(dtype, M, C, &tv, &ppb);
+  US_CHECK_ARG(g == G, "bn_bwd_reduce: G mismatch (%d vs %d)", G, g);
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  dim3 grid(G, C / V / tv);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)dA,
+                                       ldd, (const T*)A, lda, (const T*)y1, ld1, mean1, inv1, (const T*)y2, ld2, mean2,
+                                       inv2, M, C, tv, ppb, part, G));
+  US_LAUNCH_CHECK("bn_bwd_reduce");
+  return 0;
+}
+
+UNETSEG_API int unetseg_bn_bwd_finalize(const float* part, int C, int G, long M, int nbranch, const float* g1,
+                                        const float* inv1, float* dg1, float* db1, const float* g2, const float* inv2,
+                                        float* dg2, float* db2, float* coef, void* stream) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, C, G, M, nbranch, g1,
+                     inv1, dg1, db1, g2, inv2, dg2, db2, coef);
+  US_LAUNCH_CHECK("bn_bwd_finalize");
+  return 0;
+}
+
+UNETSEG_API int unetseg_bn_bwd_apply(int dtype, const void* dA, int ldd, const void* A, int lda, const void* y1,
+                                     int ld1, const float* mean1, const float* inv1, void* dy1, int ldo1,
+                                     const void* y2, int ld2, const float* mean2, const float* inv2, void* dy2,
+                                     int ldo2, const float* coef, void* dzout, int ldz, int dz_acc, long M, int C,
+                                     void* stream) {
+  CHECK_VEC(dtype, C, "bn_bwd_apply");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(M * C / VE<T>)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)dA, ldd, (const T*)A, lda, (const T*)y1, ld1,
+                                       mean1, inv1, (T*)dy1, ldo1, (const T*)y2, ld2, mean2, inv2, (T*)dy2, ldo2, coef,
+                                       (T*)dzout, ldz, dz_acc, M, C));
+  US_LAUNCH_CHECK("bn_bwd_apply");
+  return 0;
+}
+
+UNETSEG_API int unetseg_relu_bwd_bias(int dtype, const void* dA, int ldd, const void* A, int lda, void* dY, int ldy,
+                                      long M, int C, float* part, int G, void* stream) {
+  CHECK_VEC(dtype, C, "relu_bwd_bias");
+  int tv, ppb;
+  const int g = unetseg_reduce_tiles(dtype, M, C, &tv, &ppb);
+  US_CHECK_ARG(g == G, "relu_bwd_bias: G mismatch");
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  dim3 grid(G, C / V / tv);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(relu_bwd_bias_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream,
+                                       (const T*)dA, ldd, (const T*)A, lda, (T*)dY, ldy, M, C, tv, ppb, part, G));
+  US_LAUNCH_CHECK("relu_bwd_bias");
+  return 0;
+}
+
+UNETSEG_API int unetseg_colsum_finalize(const float* part, int C, int G, float* out, int accumulate, void* stream) {
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, C, G, out, accumulate);
+  US_LAUNCH_CHECK("colsum_finalize");
+  return 0;
+}
+
+UNETSEG_API int unetseg_maxpool_fwd(int dtype, const void* x, int ldx, int n, int h, int w, int c, int k, int s,
+                                    int ceil_mode, void* y, int ldy, uint8_t* idx, int* p_out, int* q_out,
+                                    void* stream) {
+  CHECK_VEC(dtype, c, "maxpool_fwd");
+  int p = ceil_mode ? (h - k + s - 1) / s + 1 : (h - k) / s + 1;
+  int q = ceil_mode ? (w - k + s - 1) / s + 1 : (w - k) / s + 1;
+  if (ceil_mode) {  // last window must start inside the input (ATen pooling_output_shape)
+    if ((p - 1) * s >= h) --p;
+    if ((q - 1) * s >= w) --q;
+  }
+  if (p_out) *p_out = p;
+  if (q_out) *q_out = q;
+  if (!y) return 0;  // shape query
+  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(grid_for((long)n * p * q * c / VE<T>)), dim3(256),
+                                       0, (hipStream_t)stream, (const T*)x, ldx, n, h, w, c, k, s, p, q, (T*)y, ldy,
+                                       idx));
+  US_LAUNCH_CHECK("maxpool_fwd");
+  return 0;
+}
+
+UNETSEG_API int unetseg_maxpool_bwd(int dtype, const void* dy, int ldy, const uint8_t* idx, int n, int h, int w,
+                                    int c, int k, int s, int p, int q, void* dx, int ldx, int accumulate,
+                                    void* stream) {
+  CHECK_VEC(dtype, c, "maxpool_bwd");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for((long)n * h * w * c / VE<T>)), dim3(256),
+                                       0, (hipStream_t)stream, (const T*)dy, ldy, idx, n, h, w, c, k, s, p, q, (T*)dx,
+                                       ldx, accumulate));
+  US_LAUNCH_CHECK("maxpool_bwd");
+  return 0;
+}
+
+UNETSEG_API int unetseg_upsample2x_fwd(int dtype, const void* x, int ldx, int n, int h, int w, int c,
+                                       int align_corners, void* y, int ldy, void* stream) {
+  CHECK_VEC(dtype, c, "upsample_fwd");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(upsample_fwd_kernel<T>, dim3(grid_for((long)n * 4 * h * w * c / VE<T>)),
+                                       dim3(256), 0, (hipStream_t)stream, (const T*)x, ldx, n, h, w, c, align_corners,
+                                       (T*)y, ldy));
+  US_LAUNCH_CHECK("upsample_fwd");
+  return 0;
+}
+
+UNETSEG_API int unetseg_upsample2x_bwd(int dtype, const void* dy, int ldy, int n, int h, int w, int c,
+                                       int align_corners, void* dx, int ldx, int accumulate, void* stream) {
+  CHECK_VEC(dtype, c, "upsample_bwd");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(upsample_bwd_kernel<T>, dim3(grid_for((long)n * h * w * c / VE<T>)), dim3(256),
+                                       0, (hipStream_t)stream, (const T*)dy, ldy, n, h, w, c, align_corners, (T*)dx,
+                                       ldx, accumulate));
+  US_LAUNCH_CHECK("upsample_bwd");
+  return 0;
+}
+
+UNETSEG_API int unetseg_pack_input(int dtype, const float* x, int n, int c, int h, int w, int cpad, void* y,
+                                   void* stream) {
+  US_CHECK_ARG(cpad >= c, "pack_input: cpad < c");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(pack_input_kernel<T>, dim3(grid_for((long)n * h * w)), dim3(256), 0,
+                                       (hipStream_t)stream, x, n, c, h, w, cpad, (T*)y));
+  US_LAUNCH_CHECK("pack_input");
+  return 0;
+}
+
+UNETSEG_API int unetseg_pw_small_tiles(long M) { return ceil_div(M, 2048); }
+
+// y fp32 planar [n][k][hw]; stats (k==1 only, may be NULL): [2][G], G = unetseg_pw_small_tiles(M), tile 2048 px
+UNETSEG_API int unetseg_pw_small_fwd(int dtype, const void* x, int ldx, long M, int hw, int c, int k, const float* w,
+                                     const float* b, float* y, float* stats, void* stream) {
+  CHECK_VEC(dtype, c, "pw_small_fwd");
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  US_CHECK_ARG(c / V <= 64 && ((c / V) & (c / V - 1)) == 0, "pw_small_fwd: C/V must be a power of two <= 64");
+  US_CHECK_ARG(k == 1 || k == 2, "pw_small_fwd: k must be 1 or 2");
+  US_CHECK_ARG(!stats || k == 1, "pw_small_fwd: stats only for k==1");
+  const int G = unetseg_pw_small_tiles(M);
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    if (k == 1)
+      hipLaunchKernelGGL((pw_small_fwd_kernel<T, 1>), dim3(G), dim3(256), 0, st, (const T*)x, ldx, M, hw, c, w, b, y,
+                         stats, 2048);
+    else
+      hipLaunchKernelGGL((pw_small_fwd_kernel<T, 2>), dim3(G), dim3(256), 0, st, (const T*)x, ldx, M, hw, c, w, b, y,
+                         stats, 2048);
+  });
+  US_LAUNCH_CHECK("pw_small_fwd");
+  return 0;
+}
+
+// dx (may be NULL) (+)= dy . W ; part_w [k][c][G], part_b [k][G]  (G = unetseg_pw_small_tiles(M))
+UNETSEG_API int unetseg_pw_small_bwd(int dtype, const float* dy, const void* x, int ldx, long M, int hw, int c, int k,
+                                     const float* w, void* dx, int lddx, int dx_acc, float* part_w, float* part_b,
+                                     void* stream) {
+  CHECK_VEC(dtype, c, "pw_small_bwd");
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  US_CHECK_ARG(c / V <= 256 && 256 % (c / V) == 0, "pw_small_bwd: bad C");
+  const int G = unetseg_pw_small_tiles(M);
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    if (k == 1)
+      hipLaunchKernelGGL((pw_small_bwd_kernel<T, 1>), dim3(G), dim3(256), 0, st, dy, (const T*)x, ldx, M, hw, c, w,
+                         (T*)dx, lddx, dx_acc, part_w, part_b, G, 2048);
+    else
+      hipLaunchKernelGGL((pw_small_bwd_kernel<T, 2>), dim3(G), dim3(256), 0, st, dy, (const T*)x, ldx, M, hw, c, w,
+                         (T*)dx, lddx, dx_acc, part_w, part_b, G, 2048);
+  });
+  US_LAUNCH_CHECK("pw_small_bwd");
+  return 0;
+}
+
+UNETSEG_API int unetseg_attn_apply(int dtype, const void* skip, int lds_, const float* psi, const float* sc,
+                                   const float* sh, float* alpha, void* gated, int ldg, long M, int c, void* stream) {
+  CHECK_VEC(dtype, c, "attn_apply");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(attn_apply_kernel<T>, dim3(grid_for(M * c / VE<T>)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)skip, lds_, psi, sc, sh, alpha, (T*)gated, ldg, M,
+                                       c));
+  US_LAUNCH_CHECK("attn_apply");
+  return 0;
+}
+
+UNETSEG_API int unetseg_attn_bwd1(int dtype, const void* dg, int ldg, const void* skip, int lds_, const float* alpha,
+                                  const float* psi, const float* mean, const float* inv, void* dskip, int ldds,
+                                  int ds_acc, float* dpsibn, long M, int c, float* part, void* stream) {
+  CHECK_VEC(dtype, c, "attn_bwd1");
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  US_CHECK_ARG(((c / V) & (c / V - 1)) == 0, "attn_bwd1: C/V must be a power of two");
+  const int G = unetseg_pw_small_tiles(M);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(attn_bwd1_kernel<T>, dim3(G), dim3(256), 0, (hipStream_t)stream, (const T*)dg,
+                                       ldg, (const T*)skip, lds_, alpha, psi, mean, inv, (T*)dskip, ldds, ds_acc, dpsibn,
+                                       M, c, 2048, part, G));
+  US_LAUNCH_CHECK("attn_bwd1");
+  return 0;
+}
+
+UNETSEG_API int unetseg_attn_bwd2(int dtype, const float* dpsibn, const float* psi, const float* mean,
+                                  const float* inv, const float* coef, const void* f, int ldf, const float* wpsi,
+                                  void* dzf, int lddz, long M, int c, float* part_w, float* part_b, void* stream) {
+  CHECK_VEC(dtype, c, "attn_bwd2");
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  const int cv = c / V;
+  US_CHECK_ARG(cv <= 256 && 256 % cv == 0, "attn_bwd2: bad C");
+  const int G = unetseg_pw_small_tiles(M);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(attn_bwd2_kernel<T>, dim3(G), dim3(256), 0, (hipStream_t)stream, dpsibn, psi,
+                                       mean, inv, coef, (const T*)f, ldf, wpsi, (T*)dzf, lddz, M, c, cv, 2048, part_w,
+                                       part_b, G));
+  US_LAUNCH_CHECK("attn_bwd2");
+  return 0;
+}
+
+UNETSEG_API int unetseg_add(int dtype, const void* x, int ldx, void* out, int ldo, long M, int c, void* stream) {
+  CHECK_VEC(dtype, c, "add");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(add_kernel<T>, dim3(grid_for(M * c / VE<T>)), dim3(256), 0, (hipStream_t)stream,
+                                       (const T*)x, ldx, (T*)out, ldo, M, c));
+  US_LAUNCH_CHECK("add");
+  return 0;
+}

@@ -1,0 +1,568 @@
+// Loss, metric and optimizer kernels of the U-Net hot path.
+//
+//   Lovasz hinge   model/unet_training.py:219-280  (per-image sort desc, Jaccard grad, dot)
+//   BCE w/ logits  model/unet_training.py:205-216, utils/train_and_eval.py:155-182
+//   2-class->1     utils/train_and_eval.py:106-113 (z = o1 - o0, fused into the loss kernels)
+//   CE + cls head  model/unet_multitask.py:73-80,109-139
+//   confusion      utils/train_and_eval.py:116-152, train.py:330-340
+//   Adam           train.py:62-78 (torch.optim.Adam, coupled L2 weight decay)
+//
+// The Lovasz sort is a segmented, stable LSD radix sort (4 x 8-bit passes) on 32-bit keys that
+// order the hinge errors descending; ties keep ascending pixel order (the reference's
+// torch.sort is not stable, so only the loss VALUE is tie-order independent).
+#include "common.h"
+
+namespace {
+
+constexpr int kTile = 4096;  // keys per radix tile (256 threads x 16)
+
+__device__ __forceinline__ uint32_t desc_key(float f) {
+  uint32_t u = __float_as_uint(f);
+  uint32_t asc = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ~asc;
+}
+__device__ __forceinline__ float key_to_float(uint32_t k) {
+  uint32_t asc = ~k;
+  uint32_t u = (asc & 0x80000000u) ? (asc & 0x7fffffffu) : ~asc;
+  return __uint_as_float(u);
+}
+
+// logits source: planar fp32 [B][nch][P]; nch==2 -> z = o1 - o0, nch==1 -> z = o0
+__device__ __forceinline__ float load_z(const float* out, int nch, int b, long P, long i) {
+  const float* base = out + (long)b * nch * P;
+  return nch == 2 ? base[P + i] - base[i] : base[i];
+}
+
+__global__ void lovasz_keygen_kernel(const float* out, int nch, const int64_t* tgt, int B, long P, uint32_t* keys,
+                                     uint32_t* vals) {
+  const long total = (long)B * P;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / P);
+    const long px = i - (long)b * P;
+    const float z = load_z(out, nch, b, P, px);
+    const uint32_t y = tgt[i] == 1 ? 1u : 0u;
+    const float e = 1.0f - z * (2.0f * (float)y - 1.0f);
+    keys[i] = desc_key(e);
+    vals[i] = (uint32_t)px | (y << 31);
+  }
+}
+
+__global__ void radix_hist_kernel(const uint32_t* keys, long P, int T, int shift, uint32_t* hist) {
+  __shared__ uint32_t h[256];
+  const int t = blockIdx.x, b = blockIdx.y;
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const long base = (long)b * P + (long)t * kTile;
+  const long n = min((long)kTile, P - (long)t * kTile);
+  for (long i = threadIdx.x; i < n; i += 256) atomicAdd(&h[(keys[base + i] >> shift) & 255u], 1u);
+  __syncthreads();
+  hist[((long)b * 256 + threadIdx.x) * T + t] = h[threadIdx.x];
+}
+
+// exclusive scan of hist[b][256*T] (digit-major) in place; one 1024-thread block per segment
+__global__ void radix_scan_kernel(uint32_t* hist, int T) {
+  __shared__ uint32_t part[1024];
+  const int b = blockIdx.x;
+  uint32_t* h = hist + (long)b * 256 * T;
+  const long n = 256L * T;
+  const long per = (n + 1023) / 1024;
+  const long lo = threadIdx.x * per, hi = min(n, lo + per);
+  uint32_t s = 0;
+  for (long i = lo; i < hi; ++i) s += h[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+  for (long i = lo; i < hi; ++i) {
+    const uint32_t c = h[i];
+    h[i] = run;
+    run += c;
+  }
+}
+
+// stable scatter: the tile is consumed in 16 rounds of 256 keys (original order = round-major)
+__global__ void radix_scatter_kernel(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
+                                     long P, int T, int shift, const uint32_t* hist) {
+  __shared__ uint32_t base[256];
+  __shared__ uint32_t wcnt[4][256];
+  const int t = blockIdx.x, b = blockIdx.y;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  base[threadIdx.x] = hist[((long)b * 256 + threadIdx.x) * T + t];
+  const long seg = (long)b * P;
+  const long tbase = (long)t * kTile;
+  const long n = min((long)kTile, P - tbase);
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  for (int round = 0; round < kTile / 256; ++round) {
+    const long i = round * 256L + threadIdx.x;
+    const bool ok = i < n;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) wcnt[w][threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t key = 0, val = 0, d = 0;
+    if (ok) {
+      key = kin[seg + tbase + i];
+      val = vin[seg + tbase + i];
+      d = (key >> shift) & 255u;
+    }
+    unsigned long long m = __ballot(ok);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const unsigned long long bal = __ballot(ok && ((d >> bit) & 1u));
+      m &= ((d >> bit) & 1u) ? bal : ~bal;
+    }
+    const int lrank = __popcll(m & lt_mask);
+    if (ok && lrank == 0) wcnt[wid][d] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (ok) {
+      uint32_t pos = base[d] + lrank;
+      for (int w = 0; w < wid; ++w) pos += wcnt[w][d];
+      kout[seg + pos] = key;
+      vout[seg + pos] = val;
+    }
+    __syncthreads();
+    base[threadIdx.x] += wcnt[0][threadIdx.x] + wcnt[1][threadIdx.x] + wcnt[2][threadIdx.x] + wcnt[3][threadIdx.x];
+  }
+}
+
+// per segment: Jaccard gradient over the sorted labels, loss = relu(e).g, dz[pixel] = g*[e>0]*(-(2y-1))
+__global__ void lovasz_scan_kernel(const uint32_t* keys, const uint32_t* vals, long P, float inv_b, float* gz,
+                                   float* seg_loss) {
+  __shared__ uint32_t part[1024];
+  __shared__ double sred[16];
+  const int b = blockIdx.x;
+  const uint32_t* k = keys + (long)b * P;
+  const uint32_t* v = vals + (long)b * P;
+  const long per = (P + 1023) / 1024;
+  const long lo = threadIdx.x * per, hi = min(P, lo + per);
+  uint32_t s = 0;
+  for (long i = lo; i < hi; ++i) s += v[i] >> 31;
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    uint32_t t = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+    __syncthreads();
+    part[threadIdx.x] += t;
+    __syncthreads();
+  }
+  const float G = (float)part[1023];
+  uint32_t cp = threadIdx.x ? part[threadIdx.x - 1] : 0;  // positives strictly before lo
+  float jprev;
+  if (lo == 0) {
+    jprev = 0.f;
+  } else {
+    const float cn = (float)(lo - cp);
+    jprev = 1.0f - (G - (float)cp) / (G + cn);
+  }
+  double loss = 0.0;
+  for (long i = lo; i < hi; ++i) {
+    const uint32_t val = v[i];
+    const uint32_t y = val >> 31;
+    cp += y;
+    const float cn = (float)(i + 1 - cp);
+    const float j = 1.0f - (G - (float)cp) / (G + cn);
+    const float g = j - jprev;
+    jprev = j;
+    const float e = key_to_float(k[i]);
+    if (e > 0.f) loss += (double)e * (double)g;
+    gz[(long)b * P + (val & 0x7fffffffu)] = e > 0.f ? g * (y ? -inv_b : inv_b) : 0.f;
+  }
+  loss = block_sum(loss, sred);
+  if (threadIdx.x == 0) seg_loss[b] = (float)loss;
+}
+
+__global__ void mean_kernel(const float* x, int n, float* out) {
+  __shared__ double sred[16];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += x[i];
+  s = block_sum(s, sred);
+  if (threadIdx.x == 0) out[0] = n > 0 ? (float)(s / n) : 0.f;
+}
+
+// d_out for a per-pixel dz: nch==2 -> d o1 = +g, d o0 = -g ; scale = upstream[0] * factor
+__global__ void dz_to_dout_kernel(const float* gz, int B, long P, int nch, const float* upstream, float factor,
+                                  float* dout) {
+  const float sc = (upstream ? upstream[0] : 1.f) * factor;
+  const long total = (long)B * P;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / P);
+    const long px = i - (long)b * P;
+    const float g = gz[i] * sc;
+    if (nch == 2) {
+      dout[((long)b * 2 + 1) * P + px] = g;
+      dout[((long)b * 2) * P + px] = -g;
+    } else {
+      dout[(long)b * P + px] = g;
+    }
+  }
+}
+
+// BCE with logits (PyTorch formulation), per-block partial sums; grad dz stored unscaled (1/count applied)
+__global__ void bce_kernel(const float* out, int nch, const int64_t* tgt, int B, long P, const float* pos_weight,
+                           float* gz, float* part) {
+  __shared__ double sred[16];
+  const long total = (long)B * P;
+  const float pw = pos_weight ? pos_weight[0] : 1.0f;
+  double s = 0.0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / P);
+    const long px = i - (long)b * P;
+    const float z = load_z(out, nch, b, P, px);
+    const float y = tgt[i] == 1 ? 1.f : 0.f;
+    const float lw = (pw - 1.f) * y + 1.f;
+    const float sp = log1pf(expf(-fabsf(z))) + fmaxf(-z, 0.f);
+    s += (double)((1.f - y) * z + lw * sp);
+    const float sig_neg = 1.f / (1.f + expf(z));  // sigmoid(-z)
+    if (gz) gz[i] = ((1.f - y) - lw * sig_neg) / (float)total;
+  }
+  s = block_sum(s, sred);
+  if (threadIdx.x == 0) part[blockIdx.x] = (float)(s / (double)total);
+}
+
+__global__ void sum_kernel(const float* x, int n, float* out) {
+  __shared__ double sred[16];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += x[i];
+  s = block_sum(s, sred);
+  if (threadIdx.x == 0) out[0] = (float)s;
+}
+
+// confusion counts: mode 2 -> pred = o1 > o0 (argmax, tie -> 0); mode 1 -> pred = sigmoid(o0) > 0.5
+__global__ void confusion_kernel(const float* out, int nch, const int64_t* tgt, int B, long P,
+                                 unsigned long long* conf) {
+  __shared__ unsigned long long sc[4][16];
+  const long total = (long)B * P;
+  unsigned long long c[4] = {0, 0, 0, 0};
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / P);
+    const long px = i - (long)b * P;
+    bool pred;
+    if (nch == 2) {
+      const float* base = out + (long)b * 2 * P;
+      pred = base[P + px] > base[px];
+    } else {
+      const float z = out[(long)b * P + px];
+      pred = 1.0f / (1.0f + expf(-z)) > 0.5f;
+    }
+    const bool t = tgt[i] == 1;
+    c[pred && t ? 0 : (pred ? 1 : (t ? 2 : 3))] += 1;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    unsigned long long v = c[k];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) sc[k][wid] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    unsigned long long v = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) v += sc[threadIdx.x][w];
+    atomicAdd(&conf[threadIdx.x], v);
+  }
+}
+
+// torch.optim.Adam single step on flat fp32 buffers (coupled L2 weight decay)
+__global__ void adam_kernel(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
+                            float eps, float wd, float bc1, float bc2_sqrt, const float* grad_scale) {
+  const float inv_scale = grad_scale ? 1.0f / grad_scale[0] : 1.0f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gr = g[i] * inv_scale;
+    const float pv = p[i];
+    if (wd != 0.f) gr = gr + wd * pv;
+    float mv = m[i];
+    mv = mv + (1.f - beta1) * (gr - mv);
+    float vv = v[i] * beta2 + (1.f - beta2) * gr * gr;
+    m[i] = mv;
+    v[i] = vv;
+    const float denom = sqrtf(vv) / bc2_sqrt + eps;
+    p[i] = pv - (lr / bc1) * (mv / denom);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// multitask classification head (model/unet_multitask.py:73-80)
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void gap_kernel(const T* x, int ldx, int B, int HW, int C, float* g) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i / C, c = i - b * C;
+  double s = 0.0;
+  for (int p = 0; p < HW; ++p) s += (float)x[((long)b * HW + p) * ldx + c];
+  g[i] = (float)(s / HW);
+}
+
+template <typename T>
+__global__ void gap_bwd_kernel(const float* dg, int B, int HW, int C, T* dx, int ldx, int accumulate) {
+  const long total = (long)B * HW * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long pix = i / C;
+    const int c = (int)(i - pix * C);
+    const int b = (int)(pix / HW);
+    T* o = dx + pix * ldx + c;
+    float v = dg[(long)b * C + c] / (float)HW;
+    if (accumulate) v += (float)(*o);
+    *o = (T)v;
+  }
+}
+
+__device__ __forceinline__ float hash_u01(unsigned long long seed, unsigned long long i) {
+  unsigned long long z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// y[b][o] = act(sum_i x[b][i] W[o][i] + bias[o]); act: 0 none, 1 relu, 2 relu + dropout(p)
+// one wave per output element
+__global__ void linear_fwd_kernel(const float* x, const float* W, const float* bias, int B, int I, int O, int act,
+                                  float p_drop, unsigned long long seed, const float* mask_in, float* mask_out,
+                                  float* pre, float* y) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (wave >= B * O) return;
+  const int b = wave / O, o = wave - b * O;
+  float s = 0.f;
+  for (int i = lane; i < I; i += 64) s += x[(long)b * I + i] * W[(long)o * I + i];
+  s = wave_sum(s);
+  if (lane == 0) {
+    s += bias ? bias[o] : 0.f;
+    if (pre) pre[wave] = s;
+    if (act >= 1) s = fmaxf(s, 0.f);
+    if (act == 2) {
+      float keep;
+      if (mask_in) keep = mask_in[wave];
+      else keep = hash_u01(seed, (unsigned long long)wave) >= p_drop ? 1.f : 0.f;
+      if (mask_out) mask_out[wave] = keep;
+      s = s * keep / (1.f - p_drop);
+    }
+    y[wave] = s;
+  }
+}
+
+// backward of linear (+ act): dyp = dy * act'(pre) ; dx[b][i] = sum_o dyp W[o][i] ; dW += ; db +=
+__global__ void linear_act_bwd_kernel(const float* dy, const float* pre, const float* mask, float p_drop, int act,
+                                      int B, int O, float* dyp) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * O) return;
+  float g = dy[i];
+  if (act >= 1 && pre[i] <= 0.f) g = 0.f;
+  if (act == 2) g = g * mask[i] / (1.f - p_drop);
+  dyp[i] = g;
+}
+
+__global__ void linear_bwd_x_kernel(const float* dyp, const float* W, int B, int I, int O, float* dx) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * I) return;
+  const int b = t / I, i = t - b * I;
+  float s = 0.f;
+  for (int o = 0; o < O; ++o) s += dyp[(long)b * O + o] * W[(long)o * I + i];
+  dx[t] = s;
+}
+
+__global__ void linear_bwd_w_kernel(const float* dyp, const float* x, int B, int I, int O, float* dW, float* db) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= O * I) return;
+  const int o = t / I, i = t - o * I;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += dyp[(long)b * O + o] * x[(long)b * I + i];
+  dW[t] += s;
+  if (i == 0 && db) {
+    float sb = 0.f;
+    for (int b = 0; b < B; ++b) sb += dyp[(long)b * O + o];
+    db[o] += sb;
+  }
+}
+
+// cross entropy (mean) over B rows of K logits; dlog = (softmax - onehot)/B (unscaled)
+__global__ void ce_kernel(const float* logits, const int64_t* tgt, int B, int K, float* loss, float* dlog) {
+  __shared__ double sred[16];
+  double s = 0.0;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const float* l = logits + (long)b * K;
+    float mx = l[0];
+    for (int k = 1; k < K; ++k) mx = fmaxf(mx, l[k]);
+    float se = 0.f;
+    for (int k = 0; k < K; ++k) se += expf(l[k] - mx);
+    const float lse = mx + logf(se);
+    const int t = (int)tgt[b];
+    s += (double)(lse - l[t]);
+    for (int k = 0; k < K; ++k) dlog[(long)b * K + k] = (expf(l[k] - lse) - (k == t ? 1.f : 0.f)) / (float)B;
+  }
+  s = block_sum(s, sred);
+  if (threadIdx.x == 0) loss[0] = (float)(s / B);
+}
+
+// multiply a per-element gradient buffer by a device scalar: out = g * (s1[0]*a1 + s2[0]*a2)
+__global__ void scale_grad_kernel(const float* g, long n, const float* s1, float a1, const float* s2, float a2,
+                                  float* out) {
+  const float sc = (s1 ? s1[0] * a1 : 0.f) + (s2 ? s2[0] * a2 : 0.f);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) out[i] = g[i] * sc;
+}
+
+inline int grid_for(long work, int cap = 8192) {
+  long b = (work + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (int)b;
+}
+
+}  // namespace
+
+// =========================================================================================
+// C ABI
+// =========================================================================================
+
+UNETSEG_API size_t unetseg_lovasz_workspace(int B, long P) {
+  const long T = (P + kTile - 1) / kTile;
+  return (size_t)B * P * 4 * sizeof(uint32_t) + (size_t)B * 256 * T * sizeof(uint32_t) + (size_t)B * sizeof(float) + 256;
+}
+
+// Lovasz hinge (per-image mean).  out: planar fp32 [B][nch][P] logits (nch 2 -> z = o1-o0);
+// tgt int64 [B][P] (==1 is foreground).  Writes loss[0] and gz [B][P] = dloss/dz (already /B).
+UNETSEG_API int unetseg_lovasz_fwd(const float* out, int nch, const int64_t* tgt, int B, long P, void* ws,
+                                   size_t ws_bytes, float* gz, float* loss, void* stream) {
+  US_CHECK_ARG(out && tgt && ws && gz && loss, "lovasz_fwd: null pointer");
+  US_CHECK_ARG(nch == 1 || nch == 2, "lovasz_fwd: nch must be 1 or 2");
+  US_CHECK_ARG(P < 0x80000000L, "lovasz_fwd: too many pixels per image");
+  US_CHECK_ARG(ws_bytes >= unetseg_lovasz_workspace(B, P), "lovasz_fwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  if (B == 0 || P == 0) {
+    (void)hipMemsetAsync(loss, 0, sizeof(float), st);
+    return 0;
+  }
+  const int T = (int)((P + kTile - 1) / kTile);
+  uint32_t* k0 = (uint32_t*)ws;
+  uint32_t* v0 = k0 + (long)B * P;
+  uint32_t* k1 = v0 + (long)B * P;
+  uint32_t* v1 = k1 + (long)B * P;
+  uint32_t* hist = v1 + (long)B * P;
+  float* seg = (float*)(hist + (long)B * 256 * T);
+  hipLaunchKernelGGL(lovasz_keygen_kernel, dim3(grid_for((long)B * P)), dim3(256), 0, st, out, nch, tgt, B, P, k0, v0);
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = pass * 8;
+    hipLaunchKernelGGL(radix_hist_kernel, dim3(T, B), dim3(256), 0, st, k0, P, T, shift, hist);
+    hipLaunchKernelGGL(radix_scan_kernel, dim3(B), dim3(1024), 0, st, hist, T);
+    hipLaunchKernelGGL(radix_scatter_kernel, dim3(T, B), dim3(256), 0, st, k0, v0, k1, v1, P, T, shift, hist);
+    uint32_t* t;
+    t = k0; k0 = k1; k1 = t;
+    t = v0; v0 = v1; v1 = t;
+  }
+  hipLaunchKernelGGL(lovasz_scan_kernel, dim3(B), dim3(1024), 0, st, k0, v0, P, 1.0f / (float)B, gz, seg);
+  hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(64), 0, st, seg, B, loss);
+  US_LAUNCH_CHECK("lovasz_fwd");
+  return 0;
+}
+
+UNETSEG_API size_t unetseg_bce_workspace(int B, long P) { return (size_t)grid_for((long)B * P) * sizeof(float) + 256; }
+
+// BCE-with-logits mean loss; gz (may be NULL) = dloss/dz (already /count); pos_weight fp32 scalar or NULL
+UNETSEG_API int unetseg_bce_fwd(const float* out, int nch, const int64_t* tgt, int B, long P, const float* pos_weight,
+                                void* ws, size_t ws_bytes, float* gz, float* loss, void* stream) {
+  US_CHECK_ARG(ws_bytes >= unetseg_bce_workspace(B, P), "bce_fwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int G = grid_for((long)B * P);
+  hipLaunchKernelGGL(bce_kernel, dim3(G), dim3(256), 0, st, out, nch, tgt, B, P, pos_weight, gz, (float*)ws);
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(256), 0, st, (const float*)ws, G, loss);
+  US_LAUNCH_CHECK("bce_fwd");
+  return 0;
+}
+
+// dout = gz * (s1[0]*a1 + s2[0]*a2) scattered to the planar logits (nch 2: +/-)
+UNETSEG_API int unetseg_dz_to_dout(const float* gz, int B, long P, int nch, const float* s1, float a1, const float* s2,
+                                   float a2, float* scratch, float* dout, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const long n = (long)B * P;
+  hipLaunchKernelGGL(scale_grad_kernel, dim3(grid_for(n)), dim3(256), 0, st, gz, n, s1, a1, s2, a2, scratch);
+  hipLaunchKernelGGL(dz_to_dout_kernel, dim3(grid_for(n)), dim3(256), 0, st, scratch, B, P, nch, (const float*)nullptr,
+                     1.f, dout);
+  US_LAUNCH_CHECK("dz_to_dout");
+  return 0;
+}
+
+// conf (uint64[4]) += (tp, fp, fn, tn)
+UNETSEG_API int unetseg_confusion(const float* out, int nch, const int64_t* tgt, int B, long P, unsigned long long* conf,
+                                  void* stream) {
+  hipLaunchKernelGGL(confusion_kernel, dim3(grid_for((long)B * P, 2048)), dim3(256), 0, (hipStream_t)stream, out, nch,
+                     tgt, B, P, conf);
+  US_LAUNCH_CHECK("confusion");
+  return 0;
+}
+
+UNETSEG_API int unetseg_adam(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
+                             float eps, float wd, int step, const float* grad_scale, void* stream) {
+  US_CHECK_ARG(step >= 1, "adam: step must be >= 1");
+  const double bc1 = 1.0 - pow((double)beta1, step);
+  const double bc2 = 1.0 - pow((double)beta2, step);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 16384)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, beta1,
+                     beta2, eps, wd, (float)bc1, (float)sqrt(bc2), grad_scale);
+  US_LAUNCH_CHECK("adam");
+  return 0;
+}
+
+UNETSEG_API int unetseg_gap_fwd(int dtype, const void* x, int ldx, int B, int HW, int C, float* g, void* stream) {
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(gap_kernel<bf16>, dim3(ceil_div(B * C, 256)), dim3(256), 0, (hipStream_t)stream, (const bf16*)x,
+                       ldx, B, HW, C, g);
+  else
+    hipLaunchKernelGGL(gap_kernel<float>, dim3(ceil_div(B * C, 256)), dim3(256), 0, (hipStream_t)stream, (const float*)x,
+                       ldx, B, HW, C, g);
+  US_LAUNCH_CHECK("gap_fwd");
+  return 0;
+}
+
+UNETSEG_API int unetseg_gap_bwd(int dtype, const float* dg, int B, int HW, int C, void* dx, int ldx, int accumulate,
+                                void* stream) {
+  const long n = (long)B * HW * C;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(gap_bwd_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dg, B, HW, C,
+                       (bf16*)dx, ldx, accumulate);
+  else
+    hipLaunchKernelGGL(gap_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dg, B, HW, C,
+                       (float*)dx, ldx, accumulate);
+  US_LAUNCH_CHECK("gap_bwd");
+  return 0;
+}
+
+UNETSEG_API int unetseg_linear_fwd(const float* x, const float* W, const float* bias, int B, int I, int O, int act,
+                                   float p_drop, unsigned long long seed, const float* mask_in, float* mask_out,
+                                   float* pre, float* y, void* stream) {
+  const long threads = (long)B * O * 64;
+  hipLaunchKernelGGL(linear_fwd_kernel, dim3(ceil_div(threads, 256)), dim3(256), 0, (hipStream_t)stream, x, W, bias, B,
+                     I, O, act, p_drop, seed, mask_in, mask_out, pre, y);
+  US_LAUNCH_CHECK("linear_fwd");
+  return 0;
+}
+
+// dx (may be NULL) = dyp . W ; dW += dyp^T x ; db += sum dyp ; scratch: B*O floats
+UNETSEG_API int unetseg_linear_bwd(const float* dy, const float* pre, const float* mask, float p_drop, int act,
+                                   const float* x, const float* W, int B, int I, int O, float* dx, float* dW, float* db,
+                                   float* scratch, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(linear_act_bwd_kernel, dim3(ceil_div(B * O, 256)), dim3(256), 0, st, dy, pre, mask, p_drop, act, B,
+                     O, scratch);
+  if (dx) hipLaunchKernelGGL(linear_bwd_x_kernel, dim3(ceil_div(B * I, 256)), dim3(256), 0, st, scratch, W, B, I, O, dx);
+  hipLaunchKernelGGL(linear_bwd_w_kernel, dim3(ceil_div(O * I, 256)), dim3(256), 0, st, scratch, x, B, I, O, dW, db);
+  US_LAUNCH_CHECK("linear_bwd");
+  return 0;
+}
+
+UNETSEG_API int unetseg_ce_fwd(const float* logits, const int64_t* tgt, int B, int K, float* loss, float* dlog,
+                               void* stream) {
+  hipLaunchKernelGGL(ce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, tgt, B, K, loss, dlog);
+  US_LAUNCH_CHECK("ce_fwd");
+  return 0;
+}
+
+// out = g * (s1[0]*a1 + s2[0]*a2)
+UNETSEG_API int unetseg_scale_grad(const float* g, long n, const float* s1, float a1, const float* s2, float a2,
+                                   float* out, void* stream) {
+  hipLaunchKernelGGL(scale_grad_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, g, n, s1, a1, s2, a2, out);
+  US_LAUNCH_CHECK("scale_grad");
+  return 0;
+}

@@ -1,0 +1,119 @@
+"""ctypes binding of libunetseg_hip.so (the C ABI declared in include/unetseg_hip.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc --offload-arch=gfx950).  There is
+no fallback: if the library or a HIP device is missing, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libunetseg_hip.so")
+
+DT_F32, DT_BF16 = 0, 1
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_long
+F = ctypes.c_float
+SZ = ctypes.c_size_t
+ULL = ctypes.c_ulonglong
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "unetseg_last_error": (ctypes.c_char_p, []),
+    "unetseg_abi_version": (I, []),
+    "unetseg_device_arch": (I, [ctypes.c_char_p, I]),
+    "unetseg_conv_tile_m": (I, []),
+    "unetseg_conv2d_fwd": (I, [I, P, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P, I, P, I, P, P]),
+    "unetseg_conv2d_dgrad": (I, [I, P, I, I, I, I, P, I, I, I, I, I, I, P, I, I, I, I, P]),
+    "unetseg_conv2d_wgrad_workspace": (SZ, [I, I, I, I, I, I, I, I]),
+    "unetseg_conv2d_wgrad": (I, [I, P, I, I, P, I, I, I, I, I, P, I, I, I, I, I, I, P, SZ, P, I, I, P]),
+    "unetseg_pack_conv_weight": (I, [I, P, I, I, I, I, I, P, P, P]),
+    "unetseg_bn_finalize": (I, [P, I, I, L, I, P, P, P, P, P, F, F, P, P, P, P, P]),
+    "unetseg_bn_eval_coeffs": (I, [I, P, P, P, P, F, P, P, P]),
+    "unetseg_bn_apply": (I, [I, P, I, P, P, P, I, P, P, I, I, P, I, L, I, P]),
+    "unetseg_reduce_tiles": (I, [I, L, I, P, P]),
+    "unetseg_bn_bwd_reduce": (I, [I, P, I, P, I, P, I, P, P, P, I, P, P, L, I, P, I, P]),
+    "unetseg_bn_bwd_finalize": (I, [P, I, I, L, I, P, P, P, P, P, P, P, P, P, P]),
+    "unetseg_bn_bwd_apply": (I, [I, P, I, P, I, P, I, P, P, P, I, P, I, P, P, P, I, P, P, I, I, L, I, P]),
+    "unetseg_relu_bwd_bias": (I, [I, P, I, P, I, P, I, L, I, P, I, P]),
+    "unetseg_colsum_finalize": (I, [P, I, I, P, I, P]),
+    "unetseg_maxpool_fwd": (I, [I, P, I, I, I, I, I, I, I, I, P, I, P, P, P, P]),
+    "unetseg_maxpool_bwd": (I, [I, P, I, P, I, I, I, I, I, I, I, I, P, I, I, P]),
+    "unetseg_upsample2x_fwd": (I, [I, P, I, I, I, I, I, I, P, I, P]),
+    "unetseg_upsample2x_bwd": (I, [I, P, I, I, I, I, I, I, P, I, I, P]),
+    "unetseg_pack_input": (I, [I, P, I, I, I, I, I, P, P]),
+    "unetseg_pw_small_tiles": (I, [L]),
+    "unetseg_pw_small_fwd": (I, [I, P, I, L, I, I, I, P, P, P, P, P]),
+    "unetseg_pw_small_bwd": (I, [I, P, P, I, L, I, I, I, P, P, I, I, P, P, P]),
+    "unetseg_attn_apply": (I, [I, P, I, P, P, P, P, P, I, L, I, P]),
+    "unetseg_attn_bwd1": (I, [I, P, I, P, I, P, P, P, P, P, I, I, P, L, I, P, P]),
+    "unetseg_attn_bwd2": (I, [I, P, P, P, P, P, P, I, P, P, I, L, I, P, P, P]),
+    "unetseg_add": (I, [I, P, I, P, I, L, I, P]),
+    "unetseg_lovasz_workspace": (SZ, [I, L]),
+    "unetseg_lovasz_fwd": (I, [P, I, P, I, L, P, SZ, P, P, P]),
+    "unetseg_bce_workspace": (SZ, [I, L]),
+    "unetseg_bce_fwd": (I, [P, I, P, I, L, P, P, SZ, P, P, P]),
+    "unetseg_dz_to_dout": (I, [P, I, L, I, P, F, P, F, P, P, P]),
+    "unetseg_confusion": (I, [P, I, P, I, L, P, P]),
+    "unetseg_adam": (I, [P, P, P, P, L, F, F, F, F, F, I, P, P]),
+    "unetseg_gap_fwd": (I, [I, P, I, I, I, I, P, P]),
+    "unetseg_gap_bwd": (I, [I, P, I, I, I, P, I, I, P]),
+    "unetseg_linear_fwd": (I, [P, P, P, I, I, I, I, F, ULL, P, P, P, P, P]),
+    "unetseg_linear_bwd": (I, [P, P, P, F, I, P, P, I, I, I, P, P, P, P, P]),
+    "unetseg_ce_fwd": (I, [P, P, I, I, P, P, P]),
+    "unetseg_scale_grad": (I, [P, L, P, F, P, F, P, P]),
+}
+
+_lib = None
+
+
+class HipUnavailable(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load the shared library and bind every C-ABI symbol (raises if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise HipUnavailable(
+            f"libunetseg_hip.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950).  There is no CPU fallback.")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def last_error() -> str:
+    return load().unetseg_last_error().decode("utf-8", "replace")
+
+
+class _Caller:
+    """lib.<name>(...) raises RuntimeError on a non-zero status."""
+
+    def __getattr__(self, item):
+        fn = getattr(load(), "unetseg_" + item)
+        if SIGNATURES["unetseg_" + item][0] is I and item not in ("reduce_tiles", "pw_small_tiles", "conv_tile_m",
+                                                                    "abi_version"):
+            def call(*args):
+                rc = fn(*args)
+                if rc != 0:
+                    raise RuntimeError(f"unetseg_{item} failed ({rc}): {last_error()}")
+                return rc
+            return call
+        return fn
+
+
+lib = _Caller()

@@ -1,0 +1,447 @@
+"""Host-side op layer: launches the HIP kernels and records the reverse-mode tape.
+
+Every activation is a ``Node`` holding an NHWC tensor view (``stride(-1) == 1``; the pixel stride
+``stride(-2)`` may exceed the channel count, so channel slices of a concat buffer are addressed in
+place).  Forward ops push a closure onto ``Ctx.tape``; ``Ctx.backward()`` runs them in reverse.
+Gradients of activations are accumulated in-kernel (``accumulate`` flags) and parameter gradients
+go straight into the model's flat fp32 gradient arena.  PyTorch supplies device memory and the
+stream only; all arithmetic is in libunetseg_hip.so.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .lib import DT_BF16, DT_F32, lib
+
+BN_TILE = 128  # == unetseg_conv_tile_m(): M tile of the conv kernel, hence of its BN partials
+PW_TILE = 2048  # pixel tile of the small-Cout 1x1 kernels
+
+
+def P(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def ldp(t):
+    """pixel stride (elements) of an NHWC view"""
+    return 0 if t is None else t.stride(-2)
+
+
+class Node:
+    __slots__ = ("data", "grad", "need_grad")
+
+    def __init__(self, data, need_grad=True):
+        self.data = data
+        self.grad = None
+        self.need_grad = need_grad
+
+    @property
+    def shape(self):
+        return self.data.shape
+
+
+_WORKSPACES = {}
+
+
+def workspace(nbytes, device):
+    """Stream-ordered scratch shared by consecutive launches (never shrunk: captured graphs keep
+    pointers into every buffer ever handed out)."""
+    key = (device.type, device.index)
+    lst = _WORKSPACES.setdefault(key, [])
+    if not lst or lst[-1].numel() < nbytes:
+        lst.append(torch.empty(max(int(nbytes), 1 << 20), dtype=torch.uint8, device=device))
+    return lst[-1]
+
+
+class Ctx:
+    def __init__(self, dt, training, record, device):
+        self.dt = dt
+        self.tdtype = torch.bfloat16 if dt == DT_BF16 else torch.float32
+        self.training = training
+        self.tape = [] if record else None
+        self.device = device
+        self.stream = torch.cuda.current_stream(device).cuda_stream
+        self.grad_hook = None  # called with a param after its gradient is final (DDP bucketing)
+
+    def push(self, fn):
+        if self.tape is not None:
+            self.tape.append(fn)
+
+    def empty(self, *shape, dtype=None):
+        return torch.empty(shape, dtype=dtype or self.tdtype, device=self.device)
+
+    def f32(self, *shape):
+        return torch.empty(shape, dtype=torch.float32, device=self.device)
+
+    def backward(self):
+        tape, self.tape = self.tape, None
+        for fn in reversed(tape):
+            fn()
+
+    def param_done(self, *params):
+        if self.grad_hook is not None:
+            for p in params:
+                if p is not None:
+                    self.grad_hook(p)
+
+
+def gbuf(ctx, node):
+    """gradient buffer of node: (tensor, accumulate flag)"""
+    if node.grad is None:
+        node.grad = ctx.empty(*node.data.shape)
+        return node.grad, 0
+    return node.grad, 1
+
+
+def give_grad(ctx, node, g):
+    """node.grad += g (g is an NHWC view); adopts g without a copy when node has no gradient yet"""
+    if not node.need_grad:
+        return
+    if node.grad is None:
+        node.grad = g
+        return
+    N, H, W, C = g.shape
+    lib.add(ctx.dt, P(g), ldp(g), P(node.grad), ldp(node.grad), N * H * W, C, ctx.stream)
+
+
+# ------------------------------------------------------------------------------------------------
+# weights
+# ------------------------------------------------------------------------------------------------
+class PackedConv:
+    """bf16/fp32 GEMM images of one conv weight: wk [K][R][S][Cpad] (fwd), wt [C][R][S][K] (dgrad)"""
+
+    def __init__(self, conv, cpad=None):
+        self.conv = conv
+        K, C, R, S = conv.weight.shape
+        self.K, self.C, self.R, self.S = K, C, R, S
+        self.cpad = cpad or C
+        self.wk = self.wt = None
+        self.dt = None
+
+    def pack(self, ctx, need_t):
+        K, C, R, S = self.K, self.C, self.R, self.S
+        if self.wk is None or self.dt != ctx.dt or self.wk.device != ctx.device:
+            self.wk = ctx.empty(K, R, S, self.cpad)
+            self.wt = ctx.empty(C, R, S, K) if need_t else None
+            self.dt = ctx.dt
+        if need_t and self.wt is None:
+            self.wt = ctx.empty(C, R, S, K)
+        lib.pack_conv_weight(ctx.dt, P(self.conv.weight), K, C, R, S, self.cpad, P(self.wk),
+                             P(self.wt) if need_t else 0, ctx.stream)
+
+
+# ------------------------------------------------------------------------------------------------
+# ops
+# ------------------------------------------------------------------------------------------------
+def pack_input(ctx, x, cpad=8):
+    """NCHW fp32 image batch -> NHWC node with channels zero-padded to cpad"""
+    x = x.contiguous()
+    if x.dtype != torch.float32:
+        x = x.float()
+    N, C, H, W = x.shape
+    y = ctx.empty(N, H, W, cpad)
+    lib.pack_input(ctx.dt, P(x), N, C, H, W, cpad, P(y), ctx.stream)
+    return Node(y, need_grad=False)
+
+
+def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
+    """y = conv(cat[x1, x2]) (+bias if the conv has one, ReLU).  Stride/padding come from the
+    Conv2d container.  Returns (Node y, BN partials or None)."""
+    stride, pad = pc.conv.stride, pc.conv.padding
+    X1 = x1.data
+    N, H, W, C1 = X1.shape
+    X2 = x2.data if x2 is not None else None
+    C2 = X2.shape[-1] if X2 is not None else 0
+    K, R, S = pc.K, pc.R, pc.S
+    Pq = (H + 2 * pad - R) // stride + 1
+    Qq = (W + 2 * pad - S) // stride + 1
+    M = N * Pq * Qq
+    y = ctx.empty(N, Pq, Qq, K)
+    G = math.ceil(M / BN_TILE)
+    st = ctx.f32(2, K, G) if stats else None
+    b = pc.conv.bias
+    lib.conv2d_fwd(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride, pad,
+                   P(b), int(relu), P(y), K, P(st), ctx.stream)
+    out = Node(y)
+
+    def bwd():
+        dA = out.grad
+        if dA is None:
+            return
+        dev = ctx.device
+        if relu:
+            Gr = lib.reduce_tiles(ctx.dt, M, K, None, None)
+            part = ctx.f32(K, Gr)
+            dY = ctx.empty(N, Pq, Qq, K)
+            lib.relu_bwd_bias(ctx.dt, P(dA), ldp(dA), P(y), K, P(dY), K, M, K, P(part), Gr, ctx.stream)
+            if b is not None:
+                lib.colsum_finalize(P(part), K, Gr, P(b.grad), 1, ctx.stream)
+        else:
+            assert b is None, "conv with bias and no ReLU is not on the hot path"
+            dY = dA
+        # weight gradient
+        cin = C1 + C2
+        ws_bytes = lib.conv2d_wgrad_workspace(ctx.dt, N, Pq, Qq, K, cin, R, S)
+        ws = workspace(ws_bytes, dev)
+        lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(dY), ldp(dY), K, R, S, stride,
+                         pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, ctx.stream)
+        ctx.param_done(pc.conv.weight, b)
+        # data gradient
+        if x2 is None:
+            if x1.need_grad:
+                g, acc = gbuf(ctx, x1)
+                lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, R, S, stride, pad, P(g),
+                                 ldp(g), H, W, acc, ctx.stream)
+        elif x1.need_grad or x2.need_grad:
+            g = ctx.empty(N, H, W, cin)
+            lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, cin, R, S, stride, pad, P(g), cin, H,
+                             W, 0, ctx.stream)
+            give_grad(ctx, x1, g[..., :C1])
+            give_grad(ctx, x2, g[..., C1:])
+
+    ctx.push(bwd)
+    return out, st
+
+
+class BNState:
+    """per-call BN coefficients"""
+
+    __slots__ = ("mean", "inv", "sc", "sh")
+
+
+def _bn_coeffs(ctx, bn, st, M, tile):
+    C = bn.weight.shape[0]
+    s = BNState()
+    s.sc, s.sh = ctx.f32(C), ctx.f32(C)
+    if ctx.training:
+        s.mean, s.inv = ctx.f32(C), ctx.f32(C)
+        G = st.shape[-1]
+        lib.bn_finalize(P(st), C, G, M, tile, P(bn.weight), P(bn.bias), P(bn.running_mean), P(bn.running_var),
+                        P(bn.num_batches_tracked), bn.momentum, bn.eps, P(s.mean), P(s.inv), P(s.sc), P(s.sh),
+                        ctx.stream)
+    else:
+        s.mean = s.inv = None
+        lib.bn_eval_coeffs(C, P(bn.weight), P(bn.bias), P(bn.running_mean), P(bn.running_var), bn.eps, P(s.sc),
+                           P(s.sh), ctx.stream)
+    return s
+
+
+def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None):
+    """a = act(BN(y) [+ res | + BN2(y2)]).  y: conv output Node with partial stats st.
+    res: raw residual Node; res_bn: (Node y2, stats2, bn module 2)."""
+    Y = y.data
+    N, H, W, C = Y.shape
+    M = N * H * W
+    s1 = _bn_coeffs(ctx, bnm, st, M, BN_TILE)
+    mode, R, s2 = 0, None, None
+    if res is not None:
+        mode, R = 1, res.data
+    elif res_bn is not None:
+        mode, R = 2, res_bn[0].data
+        s2 = _bn_coeffs(ctx, res_bn[2], res_bn[1], M, BN_TILE)
+    a = ctx.empty(N, H, W, C)
+    lib.bn_apply(ctx.dt, P(Y), ldp(Y), P(s1.sc), P(s1.sh), P(R), ldp(R), P(s2.sc if s2 else None),
+                 P(s2.sh if s2 else None), mode, int(relu), P(a), C, M, C, ctx.stream)
+    out = Node(a)
+
+    def bwd():
+        dA = out.grad
+        if dA is None:
+            return
+        if not ctx.training:
+            raise NotImplementedError("backward through eval-mode BatchNorm is not on the hot path")
+        Gr = lib.reduce_tiles(ctx.dt, M, C, None, None)
+        part = ctx.f32(3, C, Gr)
+        y2 = res_bn[0] if res_bn is not None else None
+        Y2 = y2.data if y2 is not None else None
+        lib.bn_bwd_reduce(ctx.dt, P(dA), ldp(dA), P(a) if relu else 0, C, P(Y), ldp(Y), P(s1.mean), P(s1.inv),
+                          P(Y2), ldp(Y2), P(s2.mean if s2 else None), P(s2.inv if s2 else None), M, C, P(part), Gr,
+                          ctx.stream)
+        coef = ctx.f32(6, C)
+        nb = 2 if y2 is not None else 1
+        b2 = res_bn[2] if res_bn is not None else None
+        lib.bn_bwd_finalize(P(part), C, Gr, M, nb, P(bnm.weight), P(s1.inv), P(bnm.weight.grad), P(bnm.bias.grad),
+                            P(b2.weight if b2 else None), P(s2.inv if s2 else None),
+                            P(b2.weight.grad if b2 else None), P(b2.bias.grad if b2 else None), P(coef), ctx.stream)
+        ctx.param_done(bnm.weight, bnm.bias)
+        if b2 is not None:
+            ctx.param_done(b2.weight, b2.bias)
+        dy1, acc1 = gbuf(ctx, y)
+        assert acc1 == 0
+        dy2 = None
+        if y2 is not None:
+            dy2, acc2 = gbuf(ctx, y2)
+            assert acc2 == 0
+        dz, dzacc = None, 0
+        if res is not None and res.need_grad:
+            dz, dzacc = gbuf(ctx, res)
+        lib.bn_bwd_apply(ctx.dt, P(dA), ldp(dA), P(a) if relu else 0, C, P(Y), ldp(Y), P(s1.mean), P(s1.inv),
+                         P(dy1), ldp(dy1), P(Y2), ldp(Y2), P(s2.mean if s2 else None), P(s2.inv if s2 else None),
+                         P(dy2), ldp(dy2), P(coef), P(dz), ldp(dz), dzacc, M, C, ctx.stream)
+
+    ctx.push(bwd)
+    return out
+
+
+def pool_out(h, k, s, ceil_mode):
+    """ATen pooling_output_shape (pad 0, dilation 1)"""
+    o = (h - k + (s - 1 if ceil_mode else 0)) // s + 1
+    if ceil_mode and (o - 1) * s >= h:
+        o -= 1
+    return o
+
+
+def maxpool(ctx, x, k, s, ceil_mode):
+    X = x.data
+    N, H, W, C = X.shape
+    Pq, Qq = pool_out(H, k, s, ceil_mode), pool_out(W, k, s, ceil_mode)
+    y = ctx.empty(N, Pq, Qq, C)
+    idx = torch.empty((N, Pq, Qq, C), dtype=torch.uint8, device=ctx.device)
+    lib.maxpool_fwd(ctx.dt, P(X), ldp(X), N, H, W, C, k, s, int(ceil_mode), P(y), C, P(idx), 0, 0, ctx.stream)
+    out = Node(y)
+
+    def bwd():
+        if out.grad is None or not x.need_grad:
+            return
+        g, acc = gbuf(ctx, x)
+        lib.maxpool_bwd(ctx.dt, P(out.grad), ldp(out.grad), P(idx), N, H, W, C, k, s, Pq, Qq, P(g), ldp(g), acc,
+                        ctx.stream)
+
+    ctx.push(bwd)
+    return out
+
+
+def upsample2x(ctx, x, align_corners):
+    X = x.data
+    N, H, W, C = X.shape
+    y = ctx.empty(N, 2 * H, 2 * W, C)
+    lib.upsample2x_fwd(ctx.dt, P(X), ldp(X), N, H, W, C, int(align_corners), P(y), C, ctx.stream)
+    out = Node(y)
+
+    def bwd():
+        if out.grad is None or not x.need_grad:
+            return
+        g, acc = gbuf(ctx, x)
+        lib.upsample2x_bwd(ctx.dt, P(out.grad), ldp(out.grad), N, H, W, C, int(align_corners), P(g), ldp(g), acc,
+                           ctx.stream)
+
+    ctx.push(bwd)
+    return out
+
+
+def pw_head(ctx, x, conv_mod):
+    """1x1 conv with Cout in {1,2} -> fp32 NCHW logits (the reference's output layout)"""
+    X = x.data
+    N, H, W, C = X.shape
+    K = conv_mod.weight.shape[0]
+    M = N * H * W
+    y = torch.empty((N, K, H, W), dtype=torch.float32, device=ctx.device)
+    lib.pw_small_fwd(ctx.dt, P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(conv_mod.bias), P(y), 0,
+                     ctx.stream)
+    holder = {}
+
+    def bwd():
+        dy = holder.get("grad")
+        if dy is None:
+            return
+        dy = dy.contiguous().float()
+        G = lib.pw_small_tiles(M)
+        pw, pb = ctx.f32(K, C, G), ctx.f32(K, G)
+        dx, acc = (gbuf(ctx, x) if x.need_grad else (None, 0))
+        lib.pw_small_bwd(ctx.dt, P(dy), P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(dx), ldp(dx), acc,
+                         P(pw), P(pb), ctx.stream)
+        lib.colsum_finalize(P(pw), K * C, G, P(conv_mod.weight.grad), 1, ctx.stream)
+        lib.colsum_finalize(P(pb), K, G, P(conv_mod.bias.grad), 1, ctx.stream)
+        ctx.param_done(conv_mod.weight, conv_mod.bias)
+
+    ctx.push(bwd)
+    return y, holder
+
+
+def attention_gate(ctx, skip, gate, gm, pth, pph):
+    """model/unet_attention.py:30-35.  gm: AttentionGate container; pth/pph: packed theta/phi convs.
+    Returns the gated skip Node (skip * alpha)."""
+    th, st_t = conv(ctx, skip, pth, stats=True)
+    ph, st_p = conv(ctx, gate, pph, stats=True)
+    f = bn(ctx, th, st_t, gm.theta[1], relu=True, res_bn=(ph, st_p, gm.phi[1]))
+    F_ = f.data
+    N, H, W, Ci = F_.shape
+    M = N * H * W
+    psi_conv, psi_bn = gm.psi[0], gm.psi[1]
+    psi = ctx.f32(M)
+    G = lib.pw_small_tiles(M)
+    pst = ctx.f32(2, 1, G)
+    lib.pw_small_fwd(ctx.dt, P(F_), ldp(F_), M, M, Ci, 1, P(psi_conv.weight), P(psi_conv.bias), P(psi),
+                     P(pst) if ctx.training else 0, ctx.stream)
+    s = _bn_coeffs(ctx, psi_bn, pst, M, PW_TILE)
+    S_ = skip.data
+    Cs = S_.shape[-1]
+    alpha = ctx.f32(M)
+    gated = ctx.empty(N, H, W, Cs)
+    lib.attn_apply(ctx.dt, P(S_), ldp(S_), P(psi), P(s.sc), P(s.sh), P(alpha), P(gated), Cs, M, Cs, ctx.stream)
+    out = Node(gated)
+
+    def bwd():
+        dg = out.grad
+        if dg is None:
+            return
+        dpsibn = ctx.f32(M)
+        part = ctx.f32(3, 1, G)
+        ds, dsacc = gbuf(ctx, skip)
+        lib.attn_bwd1(ctx.dt, P(dg), ldp(dg), P(S_), ldp(S_), P(alpha), P(psi), P(s.mean), P(s.inv), P(ds), ldp(ds),
+                      dsacc, P(dpsibn), M, Cs, P(part), ctx.stream)
+        coef = ctx.f32(6, 1)
+        lib.bn_bwd_finalize(P(part), 1, G, M, 1, P(psi_bn.weight), P(s.inv), P(psi_bn.weight.grad),
+                            P(psi_bn.bias.grad), 0, 0, 0, 0, P(coef), ctx.stream)
+        ctx.param_done(psi_bn.weight, psi_bn.bias)
+        dzf, acc = gbuf(ctx, f)
+        assert acc == 0
+        pw, pb = ctx.f32(Ci, G), ctx.f32(1, G)
+        lib.attn_bwd2(ctx.dt, P(dpsibn), P(psi), P(s.mean), P(s.inv), P(coef), P(F_), ldp(F_), P(psi_conv.weight),
+                      P(dzf), ldp(dzf), M, Ci, P(pw), P(pb), ctx.stream)
+        lib.colsum_finalize(P(pw), Ci, G, P(psi_conv.weight.grad), 1, ctx.stream)
+        lib.colsum_finalize(P(pb), 1, G, P(psi_conv.bias.grad), 1, ctx.stream)
+        ctx.param_done(psi_conv.weight, psi_conv.bias)
+
+    ctx.push(bwd)
+    return out
+
+
+def cls_head(ctx, feat, head, dropout_mask=None, seed=0):
+    """model/unet_multitask.py:73-80: GAP -> FC 2048->512 -> ReLU -> Dropout(0.5) -> FC 512->3"""
+    X = feat.data
+    N, H, W, C = X.shape
+    fc1, fc2 = head[2], head[5]
+    p_drop = head[4].p if ctx.training else 0.0
+    O1, O2 = fc1.weight.shape[0], fc2.weight.shape[0]
+    g = ctx.f32(N, C)
+    lib.gap_fwd(ctx.dt, P(X), ldp(X), N, H * W, C, P(g), ctx.stream)
+    pre, h, mask = ctx.f32(N, O1), ctx.f32(N, O1), ctx.f32(N, O1)
+    act = 2 if ctx.training else 1
+    if dropout_mask is not None:
+        dropout_mask = dropout_mask.to(device=ctx.device, dtype=torch.float32).contiguous()
+    lib.linear_fwd(P(g), P(fc1.weight), P(fc1.bias), N, C, O1, act, p_drop, seed, P(dropout_mask), P(mask), P(pre),
+                   P(h), ctx.stream)
+    y = torch.empty((N, O2), dtype=torch.float32, device=ctx.device)
+    lib.linear_fwd(P(h), P(fc2.weight), P(fc2.bias), N, O1, O2, 0, 0.0, 0, 0, 0, 0, P(y), ctx.stream)
+    holder = {}
+
+    def bwd():
+        dy = holder.get("grad")
+        if dy is None:
+            return
+        dy = dy.contiguous().float()
+        dh = ctx.f32(N, O1)
+        scratch = ctx.f32(N, max(O1, O2))
+        lib.linear_bwd(P(dy), 0, 0, 0.0, 0, P(h), P(fc2.weight), N, O1, O2, P(dh), P(fc2.weight.grad),
+                       P(fc2.bias.grad), P(scratch), ctx.stream)
+        dg = ctx.f32(N, C)
+        lib.linear_bwd(P(dh), P(pre), P(mask), p_drop, act, P(g), P(fc1.weight), N, C, O1, P(dg), P(fc1.weight.grad),
+                       P(fc1.bias.grad), P(scratch), ctx.stream)
+        ctx.param_done(fc2.weight, fc2.bias, fc1.weight, fc1.bias)
+        dx, acc = gbuf(ctx, feat)
+        lib.gap_bwd(ctx.dt, P(dg), N, H * W, C, P(dx), ldp(dx), acc, ctx.stream)
+
+    ctx.push(bwd)
+    return y, holder, mask

@@ -1,0 +1,126 @@
+"""Binary training / evaluation loops (reference: utils/train_and_eval.py:106-305).
+
+Same signatures, return values and metric definitions as the reference; the loss and the
+confusion counts run on fused HIP kernels and the per-iteration host syncs are reduced to one
+``loss.item()``.  The multiclass loops (train_one_epoch/evaluate) are outside the hot-path scope.
+"""
+import time
+
+import torch
+from torch.amp import autocast
+
+from unetseg_hip import losses
+from utils.utils import get_lr
+
+
+class LogColor:
+    GREEN = "\033[1;32m"
+    YELLOW = "\033[1;33m"
+    RED = "\033[1;31m"
+    RESET = "\033[0m"
+    BLUE = "\033[1;34m"
+
+
+def _binary_logits_from_two_class(output: torch.Tensor) -> torch.Tensor:
+    """train_and_eval.py:106-113"""
+    if output.dim() != 4 or output.size(1) != 2:
+        raise ValueError(f"Expected output shape (N,2,H,W), got {tuple(output.shape)}")
+    return output[:, 1, :, :] - output[:, 0, :, :]
+
+
+def _binary_confusion_from_pred(pred: torch.Tensor, target: torch.Tensor, ignore_index=None):
+    """train_and_eval.py:116-137 (pred already thresholded; helper kept for API parity)"""
+    if ignore_index is not None:
+        valid = target != ignore_index
+        pred, target = pred[valid], target[valid]
+    pf, tf = pred == 1, target == 1
+    tp = torch.logical_and(pf, tf).sum().item()
+    fp = torch.logical_and(pf, ~tf).sum().item()
+    fn = torch.logical_and(~pf, tf).sum().item()
+    tn = torch.logical_and(~pf, ~tf).sum().item()
+    return tp, fp, fn, tn
+
+
+def binary_segmentation_metrics(tp: float, fp: float, fn: float, tn: float, eps: float = 1e-7):
+    """train_and_eval.py:140-152"""
+    precision = tp / (tp + fp + eps)
+    recall = tp / (tp + fn + eps)
+    dice = (2.0 * tp) / (2.0 * tp + fp + fn + eps)
+    iou = tp / (tp + fp + fn + eps)
+    accuracy = (tp + tn) / (tp + tn + fp + fn + eps)
+    return {"Dice": float(dice), "IoU": float(iou), "Precision": float(precision), "Recall": float(recall),
+            "Accuracy": float(accuracy)}
+
+
+def binary_segmentation_loss(outputs, targets, loss_name: str, pos_weight=None, ignore_index=None):
+    """train_and_eval.py:155-182 -> fused HIP kernel (2-class difference fused)."""
+    return losses.binary_segmentation_loss(outputs, targets, loss_name, pos_weight, ignore_index)
+
+
+def train_one_epoch_binary(model, optimizer, train_loader, device, loss_name: str, pos_weight, gpu_used, scaler, epoch,
+                           train_epoch, ignore_index=None, max_batches=None):
+    """train_and_eval.py:185-263"""
+    epoch_loss = 0.0
+    seen_batches = 0
+    model_train = model.train().to(device)
+    n_batches = len(train_loader)
+    for iteration, batch in enumerate(train_loader):
+        imgs, pngs = batch[0], batch[1]
+        imgs = imgs.to(device, non_blocking=True)
+        pngs = pngs.to(device, non_blocking=True)
+        optimizer.zero_grad()
+        if scaler is None:
+            outputs = model_train(imgs)
+            loss = binary_segmentation_loss(outputs, pngs, loss_name, pos_weight, ignore_index)
+            loss.backward()
+            optimizer.step()
+        else:
+            with autocast(device_type=device.type, enabled=True):
+                outputs = model_train(imgs)
+                loss = binary_segmentation_loss(outputs, pngs, loss_name, pos_weight, ignore_index)
+            scaler.scale(loss).backward()
+            scaler.step(optimizer)
+            scaler.update()
+        lv = loss.item()
+        epoch_loss += lv
+        seen_batches += 1
+        if iteration == 0:
+            print(f"{LogColor.GREEN}Epoch{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}data_num{LogColor.RESET}{' ' * 12}"
+                  f"{LogColor.YELLOW}GPU Mem{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}Loss{LogColor.RESET}{' ' * 12}"
+                  f"{LogColor.YELLOW}LR{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}Image_size{LogColor.RESET}{' ' * 12}")
+        print(f"\r{epoch + 1}/{train_epoch}    {iteration + 1}/{n_batches}    {gpu_used:.2f} MB    {lv:.8f}    "
+              f"{get_lr(optimizer):.8f}    {imgs.shape[2]}", end="", flush=True)
+        if max_batches is not None and seen_batches >= max_batches:
+            break
+    print(f"{LogColor.GREEN}")
+    time.sleep(0.2)
+    return epoch_loss / max(seen_batches, 1)
+
+
+def evaluate_binary(model, val_loader, device, loss_name: str, pos_weight, ignore_index=None, max_batches=None):
+    """train_and_eval.py:266-305: eval-mode fp32 forward, global tp/fp/fn/tn, metrics with eps 1e-7."""
+    model_eval = model.eval().to(device)
+    total_loss = torch.zeros((), dtype=torch.float64, device=device)
+    conf = torch.zeros(4, dtype=torch.int64, device=device)
+    seen_batches = 0
+    with torch.no_grad():
+        for batch in val_loader:
+            imgs, pngs = batch[0].to(device), batch[1].to(device)
+            outputs = model_eval(imgs)
+            loss = binary_segmentation_loss(outputs, pngs, loss_name, pos_weight, ignore_index)
+            total_loss += loss
+            losses.binary_confusion(outputs, pngs, conf)
+            seen_batches += 1
+            if max_batches is not None and seen_batches >= max_batches:
+                break
+    tp, fp, fn, tn = (float(v) for v in conf.tolist())
+    metrics = binary_segmentation_metrics(tp, fp, fn, tn)
+    metrics["Loss"] = float(total_loss.item() / max(seen_batches, 1))
+    return metrics
+
+
+def _out_of_scope(*_a, **_k):
+    raise NotImplementedError("the multiclass task is outside the hot-path scope (SURVEY.md §2.1)")
+
+
+train_one_epoch = evaluate = pixel_accuracy = mean_accuracy = mean_iou = frequency_weighted_iou = _out_of_scope
