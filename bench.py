@@ -1,0 +1,185 @@
+"""Benchmark: unet_resnet50 binary segmentation training, 512x512, batch 16 per GPU, bf16 (HIP path).
+
+    python bench.py --gpus N --steps K --warmup W
+    (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+
+A step = zero_grad + forward + Lovasz-hinge loss + backward (+ RCCL gradient all-reduce when N>1) +
+fused Adam on one synthetic batch already resident in HBM.  Rank 0 prints ONE JSON line.
+`roofline` covers the dominant kernel (igemm_tn: conv fwd + dgrad), measured with HIP events around
+each of its launches in one probe step right after the timed region.  `cpu_baseline` times the CPU
+oracle (oracle/ref_cpu.py, fp32, the reference's op sequence) on the host on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "unet-embroidery-seg_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "images/sec training unet_resnet50 512×512 bf16 at 1/2/4/8 GPUs; mIoU parity"
+GFLOP_PER_IMG = {"unet_resnet50": 547.46, "multitask_unet": 547.36, "attention_unet": 1374.35, "unet_plain": 83.48}
+PEAK_BF16_TFLOPS = 2516.6  # gfx950 dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="unet_resnet50")
+    ap.add_argument("--batch", type=int, default=16, help="per-GPU batch")
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--loss", default="lovasz_hinge")
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (N=1)")
+    ap.add_argument("--cpu-batch", type=int, default=1)
+    ap.add_argument("--probe", type=int, default=1)
+    return ap.parse_args()
+
+
+def cpu_baseline(model_name, size, batch):
+    """The oracle's fp32 train step (fwd + loss + bwd + Adam) on host cores; bounded sample."""
+    from oracle import ref_cpu
+    from oracle.weights import make_torch_state
+    from utils.synthetic import make_batch
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    kw = dict(num_classes=1) if model_name == "multitask_unet" else dict(num_classes=2)
+    params, buffers = ref_cpu.split_state(make_torch_state(ref_cpu.model_spec(model_name, **kw)))
+    m1 = {k: torch.zeros_like(v) for k, v in params.items()}
+    m2 = {k: torch.zeros_like(v) for k, v in params.items()}
+    x, y = make_batch(batch, size, seed=99)
+    times = []
+    for i in range(3):  # 1 warmup + 2 timed
+        t0 = time.perf_counter()
+        _, _, grads = ref_cpu.train_step(model_name, params, buffers, x, y, "lovasz_hinge")
+        ref_cpu.adam_step(params, grads, m1, m2, i + 1, 1e-4)
+        times.append(time.perf_counter() - t0)
+    t = min(times[1:])
+    return {"value": round(batch / t, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle fp32 {model_name} {size}x{size} batch {batch}, 1 warmup + 2 timed train steps "
+                      f"(fwd+lovasz+bwd+Adam), best step {t:.2f} s, torch {torch.__version__} CPU"}
+
+
+def main():
+    args = parse()
+    from unetseg_hip.ddp import GradBuckets, init_from_env
+
+    rank, world, local = init_from_env("nccl")
+    if world != args.gpus:
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(11)
+
+    from model.model_factory import create_model
+    from unetseg_hip import ops
+    from unetseg_hip.arena import FusedAdam
+    from unetseg_hip.losses import binary_segmentation_loss
+    from utils.synthetic import make_batch
+
+    kw = dict(num_classes=1) if args.model == "multitask_unet" else dict(num_classes=2)
+    model = create_model(args.model, weights="", **kw).to(dev).train()
+    model.compute_dtype = "bf16"
+    buckets = GradBuckets(model) if world > 1 else None
+    opt = FusedAdam(model, lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4)
+    nbatches = 2
+    data = []
+    for i in range(nbatches):
+        x, y = make_batch(args.batch, args.size, seed=1234 + 100000 * rank + i)
+        data.append((x.to(dev), y.to(dev)))
+
+    def step(i):
+        x, y = data[i % nbatches]
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(x)
+            loss = binary_segmentation_loss(out, y, args.loss)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for i in range(args.steps):
+        loss = step(i)
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+    ms_per_step = 1000.0 * wall / args.steps
+    imgs_per_s = args.batch * world * args.steps / wall
+    final_loss = float(loss.item())
+
+    roof = None
+    if args.probe:
+        ops.PROBE = []
+        step(0)
+        torch.cuda.synchronize()
+        kinds = {}
+        for kind, flops, e0, e1 in ops.PROBE:
+            d = kinds.setdefault(kind, [0.0, 0.0, 0])
+            d[0] += flops
+            d[1] += e0.elapsed_time(e1) * 1e-3
+            d[2] += 1
+        ops.PROBE = None
+        dom = max(kinds, key=lambda k: kinds[k][1])
+        fl, sec, n = kinds[dom]
+        ach = fl / sec / 1e12
+        roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "launches_per_step": n, "avg_launch_us": round(1e6 * sec / n, 2),
+                "algorithmic_gflop_per_step": round(fl / 1e9, 1),
+                "kernels": {k: {"tflops": round(v[0] / v[1] / 1e12, 2), "ms_per_step": round(1e3 * v[1], 3),
+                                "launches": v[2]} for k, v in kinds.items()}}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        cpu = cpu_baseline(args.model, args.size, args.cpu_batch)
+
+    if rank == 0:
+        step_tflops = imgs_per_s / world * GFLOP_PER_IMG[args.model] / 1e3
+        line = {
+            "metric": METRIC, "value": round(imgs_per_s, 2), "unit": "images/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (seeded 512x512 RGB ellipse images + masks, resident in HBM)",
+            "config": {"workload": f"{args.model} binary seg {args.size}x{args.size}, per-GPU batch {args.batch}, "
+                                   f"{args.loss} + Adam", "global_batch": args.batch * world,
+                       "image_size": args.size, "parallelism": f"dp{world}"},
+            "roofline": roof, "cpu_baseline": cpu,
+            "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
+            "step_tflops_per_gpu": round(step_tflops, 2),
+            "gpu_event_ms_per_step": round(gpu_ms / args.steps, 3), "final_loss": round(final_loss, 5),
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,96 @@
+"""Data-parallel training over RCCL (torch.distributed "nccl" backend == RCCL on ROCm).
+
+The reference is single-process (train.py:98); this is the build's DP path:
+  * parameters (one flat fp32 arena) and BN buffers are broadcast from rank 0 at wrap time;
+  * gradient buckets are contiguous slices of the flat gradient arena.  The arena is laid out in
+    reverse forward order, so the tape's backward completes buckets front to back; the op layer
+    reports each finished parameter (``param_done``) and a bucket's all-reduce (AVG) is issued the
+    moment its last parameter is final, overlapping the rest of backward (RCCL runs on its own
+    stream, fenced against the compute stream by torch.distributed);
+  * BatchNorm uses per-GPU batch statistics and rank-local running stats (DDP without SyncBN).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class GradBuckets:
+    def __init__(self, model, bucket_mb: float = 25.0, group=None):
+        self.model = model
+        self.group = group
+        flat = model._flat
+        esz = flat.element_size()
+        cap = max(1, int(bucket_mb * 1024 * 1024 / esz))
+        # params in arena order
+        order = sorted(model._param_list, key=lambda p: model._slices[id(p)][0])
+        self.buckets = []  # [start, end, remaining]
+        self.owner = {}
+        start, count = None, 0
+        for p in order:
+            off, n = model._slices[id(p)]
+            if start is None:
+                start = off
+            self.owner[id(p)] = len(self.buckets)
+            count += 1
+            if off + n - start >= cap:
+                self.buckets.append([start, off + n, count])
+                start, count = None, 0
+        if start is not None:
+            self.buckets.append([start, flat.numel(), count])
+        self._pending = []
+        self._left = None
+        self._issued = None
+        model._grad_hook = self._on_grad
+        model._after_backward = self._finish
+        self.broadcast_state()
+
+    @torch.no_grad()
+    def broadcast_state(self):
+        dist.broadcast(self.model._flat, 0, group=self.group)
+        for b in self.model.buffers():
+            dist.broadcast(b, 0, group=self.group)
+
+    def _reset(self):
+        self._left = [b[2] for b in self.buckets]
+        self._issued = [False] * len(self.buckets)
+        self._pending = []
+
+    def _issue(self, i):
+        s, e, _ = self.buckets[i]
+        view = self.model._flat_grad[s:e]
+        self._pending.append(dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
+        self._issued[i] = True
+
+    def _on_grad(self, p):
+        if self._left is None:
+            self._reset()
+        i = self.owner[id(p)]
+        self._left[i] -= 1
+        if self._left[i] == 0 and not self._issued[i]:
+            self._issue(i)
+
+    def _finish(self):
+        if self._left is None:
+            self._reset()
+        for i in range(len(self.buckets)):
+            if not self._issued[i]:
+                self._issue(i)
+        for w in self._pending:
+            w.wait()
+        self._left = None
+        self._pending = []
+
+
+def init_from_env(backend: str = "nccl"):
+    """One process per GPU (torchrun env); returns (rank, world, local_rank)."""
+    import os
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    return rank, world, local

@@ -43,6 +43,26 @@ class Node:
 
 _WORKSPACES = {}
 
+#: when a list, conv launches append (kernel, algorithmic_flops, start_event, end_event) (bench.py probe)
+PROBE = None
+
+
+class _probe:
+    def __init__(self, kind, flops):
+        self.kind, self.flops = kind, flops
+
+    def __enter__(self):
+        if PROBE is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *a):
+        if PROBE is not None:
+            self.e1.record()
+            PROBE.append((self.kind, self.flops, self.e0, self.e1))
+
 
 def workspace(nbytes, device):
     """Stream-ordered scratch shared by consecutive launches (never shrunk: captured graphs keep
@@ -161,8 +181,10 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
     G = math.ceil(M / BN_TILE)
     st = ctx.f32(2, K, G) if stats else None
     b = pc.conv.bias
-    lib.conv2d_fwd(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride, pad,
-                   P(b), int(relu), P(y), K, P(st), ctx.stream)
+    flops = 2.0 * M * K * pc.C * R * S  # algorithmic (unpadded Cin)
+    with _probe("igemm_tn", flops):
+        lib.conv2d_fwd(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride, pad,
+                       P(b), int(relu), P(y), K, P(st), ctx.stream)
     out = Node(y)
 
     def bwd():
@@ -184,19 +206,22 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
         cin = C1 + C2
         ws_bytes = lib.conv2d_wgrad_workspace(ctx.dt, N, Pq, Qq, K, cin, R, S)
         ws = workspace(ws_bytes, dev)
-        lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(dY), ldp(dY), K, R, S, stride,
-                         pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, ctx.stream)
+        with _probe("wgrad", flops):
+            lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(dY), ldp(dY), K, R, S,
+                             stride, pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, ctx.stream)
         ctx.param_done(pc.conv.weight, b)
         # data gradient
         if x2 is None:
             if x1.need_grad:
                 g, acc = gbuf(ctx, x1)
-                lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, R, S, stride, pad, P(g),
-                                 ldp(g), H, W, acc, ctx.stream)
+                with _probe("igemm_tn", flops):
+                    lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, R, S, stride, pad, P(g),
+                                     ldp(g), H, W, acc, ctx.stream)
         elif x1.need_grad or x2.need_grad:
             g = ctx.empty(N, H, W, cin)
-            lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, cin, R, S, stride, pad, P(g), cin, H,
-                             W, 0, ctx.stream)
+            with _probe("igemm_tn", flops):
+                lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, cin, R, S, stride, pad, P(g), cin,
+                                 H, W, 0, ctx.stream)
             give_grad(ctx, x1, g[..., :C1])
             give_grad(ctx, x2, g[..., C1:])
 
