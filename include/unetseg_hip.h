@@ -1,0 +1,175 @@
+/*
+ * unetseg_hip.h -- C ABI of libunetseg_hip.so, the MI355X (gfx950) hot path of U-Net segmentation
+ * training: conv fwd/dgrad/wgrad on MFMA, BatchNorm, pooling, bilinear upsampling, the attention
+ * gate, the fused losses (Lovasz hinge, BCE-with-logits, cross entropy), binary confusion counts and
+ * Adam.
+ *
+ * The reference (TariAgentBenchmark/unet-embroidery-seg) has no FFI: its hot path sits behind the
+ * nn.Module protocol (model/model_factory.py:22 build_model, train.py:48 create_model,
+ * <Model>.forward, the loss callables in model/unet_training.py:205,253 and
+ * model/unet_multitask.py:119).  Each entry point below replaces the PyTorch/ATen operator the
+ * reference calls at the cited line; the Python mirror (unet-embroidery-seg_amd/unetseg_hip/*.py)
+ * binds them with ctypes and keeps the reference's module names, state_dict keys and errors.
+ *
+ * Conventions
+ *  - All pointers are DEVICE pointers borrowed from the caller (PyTorch's caching allocator); the
+ *    library allocates nothing.  `stream` is a hipStream_t (NULL = legacy default stream).
+ *  - Activations are NHWC with an explicit pixel stride `ld*` (elements between consecutive pixels),
+ *    so a tensor may be a channel slice of a wider buffer (virtual concat).  `M` = n*h*w pixels.
+ *  - `dtype`: 0 = fp32, 1 = bf16 (activations).  Weights arrive fp32 and are packed by
+ *    unetseg_pack_conv_weight; statistics, biases, BN parameters and losses are always fp32.
+ *  - Return value 0 = ok; non-zero = error, message via unetseg_last_error() (thread-local).
+ *    Launches are asynchronous: device faults surface at the caller's next synchronisation.
+ */
+#ifndef UNETSEG_HIP_H
+#define UNETSEG_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- library ------------------------------------------------------------------------------ */
+const char* unetseg_last_error(void);
+int unetseg_abi_version(void);
+int unetseg_device_arch(char* buf, int n);
+
+/* ---- convolution (nn.Conv2d: model/resnet_backbone.py:19,33,126,167; model/unet_resnet.py:17,19,
+ *      72,74,78; model/unet_plain.py:9,12,69; model/unet_attention.py:16,20,24,76;
+ *      model/unet_multitask.py:17,18,62,64,69) and the concat feeding it
+ *      (torch.cat: model/unet_resnet.py:34, model/unet_plain.py:46, model/unet_attention.py:54) --- */
+
+/* fp32 [K][C][R][S] -> wk dtype [K][R][S][Cpad] (fwd) and, if wt != NULL, wt dtype [C][R][S][K] (dgrad) */
+int unetseg_pack_conv_weight(int dtype, const float* w, int K, int C, int R, int S, int Cpad, void* wk, void* wt,
+                             void* stream);
+/* legacy generic row tile (kept for ABI v1 callers) */
+int unetseg_conv_tile_m(void);
+/* row tile of the BN partial statistics unetseg_conv2d_fwd writes for this shape */
+int unetseg_conv2d_fwd_tile_m(int dtype, int c1, int ldc1, int c2, int ldc2, int n, int h, int w, int cout, int r,
+                              int s, int stride, int pad);
+/* y[n,p,q,cout] = conv(cat(x1[.., c1], x2[.., c2]), wk) (+bias) (ReLU); stats (may be NULL):
+ * fp32 [2][cout][ceil(M/tile)] = per-tile (sum, M2 about the tile mean) of the rounded y (BN train) */
+int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h,
+                       int w, const void* wk, int cout, int r, int s, int stride, int pad, const float* bias, int relu,
+                       void* y, int ldy, float* stats, void* stream);
+/* dx[n,h,w,cin] (+)= conv_transpose(dy[n,p,q,cout], wt) */
+int unetseg_conv2d_dgrad(int dtype, const void* dy, int ldy, int n, int p, int q, const void* wt, int cout, int cin,
+                         int r, int s, int stride, int pad, void* dx, int ldx, int h, int w, int accumulate,
+                         void* stream);
+size_t unetseg_conv2d_wgrad_workspace(int dtype, int n, int p, int q, int cout, int cin, int r, int s);
+/* dw fp32 [cout][dw_c][r][s] (PyTorch layout) (+)= sum_pix dy x; ws of the size queried above */
+int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h,
+                         int w, const void* dy, int ldy, int cout, int r, int s, int stride, int pad, float* ws,
+                         size_t ws_bytes, float* dw, int dw_c, int accumulate, void* stream);
+/* NCHW fp32 input [n][c][h][w] -> NHWC dtype [n][h][w][cpad] (zero channel padding) */
+int unetseg_pack_input(int dtype, const float* x, int n, int c, int h, int w, int cpad, void* y, void* stream);
+
+/* ---- BatchNorm2d, training and eval (model/resnet_backbone.py:127,169; model/unet_plain.py:10,13;
+ *      model/unet_attention.py:17,21,25) -------------------------------------------------------- */
+
+/* Chan-merge conv partials -> batch mean/invstd, scale/shift; update running stats (momentum,
+ * unbiased var) and num_batches_tracked when rmean != NULL */
+int unetseg_bn_finalize(const float* part, int C, int G, long M, int tile, const float* gamma, const float* beta,
+                        float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* mean,
+                        float* invstd, float* scale, float* shift, void* stream);
+int unetseg_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                           float eps, float* scale, float* shift, void* stream);
+/* out = [relu](y*sc + sh [+ r | + r*sc2 + sh2])   res_mode 0 none, 1 identity add, 2 BN'd add */
+int unetseg_bn_apply(int dtype, const void* y, int ldy, const float* sc, const float* sh, const void* r, int ldr,
+                     const float* sc2, const float* sh2, int res_mode, int relu, void* out, int ldo, long M, int C,
+                     void* stream);
+/* partial-buffer geometry of the channel reductions below: returns G (row groups) */
+int unetseg_reduce_tiles(int dtype, long M, int C, int* tv_out, int* ppb_out);
+/* backward through [relu](BN(y1) [+ BN(y2)]): per-channel partials of dz and dz*xhat */
+int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const void* A, int lda, const void* y1, int ld1,
+                          const float* mean1, const float* inv1, const void* y2, int ld2, const float* mean2,
+                          const float* inv2, long M, int C, float* part, int G, void* stream);
+int unetseg_bn_bwd_finalize(const float* part, int C, int G, long M, int nbranch, const float* g1, const float* inv1,
+                            float* dg1, float* db1, const float* g2, const float* inv2, float* dg2, float* db2,
+                            float* coef, void* stream);
+int unetseg_bn_bwd_apply(int dtype, const void* dA, int ldd, const void* A, int lda, const void* y1, int ld1,
+                         const float* mean1, const float* inv1, void* dy1, int ldo1, const void* y2, int ld2,
+                         const float* mean2, const float* inv2, void* dy2, int ldo2, const float* coef, void* dzout,
+                         int ldz, int dz_acc, long M, int C, void* stream);
+/* ReLU backward (mask from the activation A) + per-channel bias-grad partials */
+int unetseg_relu_bwd_bias(int dtype, const void* dA, int ldd, const void* A, int lda, void* dY, int ldy, long M, int C,
+                          float* part, int G, void* stream);
+int unetseg_colsum_finalize(const float* part, int C, int G, float* out, int accumulate, void* stream);
+
+/* ---- pooling / resampling (nn.MaxPool2d: model/resnet_backbone.py:131, model/unet_plain.py:25,
+ *      model/unet_attention.py:66-69; UpsamplingBilinear2d / Upsample / interpolate:
+ *      model/unet_resnet.py:21,71, model/unet_plain.py:36, model/unet_attention.py:32,41,53) ------- */
+int unetseg_maxpool_fwd(int dtype, const void* x, int ldx, int n, int h, int w, int c, int k, int s, int ceil_mode,
+                        void* y, int ldy, uint8_t* idx, int* p_out, int* q_out, void* stream);
+int unetseg_maxpool_bwd(int dtype, const void* dy, int ldy, const uint8_t* idx, int n, int h, int w, int c, int k,
+                        int s, int p, int q, void* dx, int ldx, int accumulate, void* stream);
+int unetseg_upsample2x_fwd(int dtype, const void* x, int ldx, int n, int h, int w, int c, int align_corners, void* y,
+                           int ldy, void* stream);
+int unetseg_upsample2x_bwd(int dtype, const void* dy, int ldy, int n, int h, int w, int c, int align_corners,
+                           void* dx, int ldx, int accumulate, void* stream);
+int unetseg_add(int dtype, const void* x, int ldx, void* out, int ldo, long M, int c, void* stream);
+
+/* ---- narrow 1x1 heads (final / outc / seg_head / psi: model/unet_resnet.py:78,
+ *      model/unet_plain.py:69, model/unet_multitask.py:69, model/unet_attention.py:24) ------------ */
+int unetseg_pw_small_tiles(long M);
+/* y fp32 planar [n][k][hw] (k <= 2); stats (k == 1, may be NULL) [2][unetseg_pw_small_tiles(M)] */
+int unetseg_pw_small_fwd(int dtype, const void* x, int ldx, long M, int hw, int c, int k, const float* w,
+                         const float* b, float* y, float* stats, void* stream);
+int unetseg_pw_small_bwd(int dtype, const float* dy, const void* x, int ldx, long M, int hw, int c, int k,
+                         const float* w, void* dx, int lddx, int dx_acc, float* part_w, float* part_b, void* stream);
+
+/* ---- attention gate (AttentionGate.forward: model/unet_attention.py:28-36) -------------------- */
+/* alpha = sigmoid(BN1(psi)); gated = skip * alpha */
+int unetseg_attn_apply(int dtype, const void* skip, int lds_, const float* psi, const float* sc, const float* sh,
+                       float* alpha, void* gated, int ldg, long M, int c, void* stream);
+int unetseg_attn_bwd1(int dtype, const void* dg, int ldg, const void* skip, int lds_, const float* alpha,
+                      const float* psi, const float* mean, const float* inv, void* dskip, int ldds, int ds_acc,
+                      float* dpsibn, long M, int c, float* part, void* stream);
+int unetseg_attn_bwd2(int dtype, const float* dpsibn, const float* psi, const float* mean, const float* inv,
+                      const float* coef, const void* f, int ldf, const float* wpsi, void* dzf, int lddz, long M, int c,
+                      float* part_w, float* part_b, void* stream);
+
+/* ---- losses and metrics ---------------------------------------------------------------------- */
+/* Lovasz hinge, per-image mean (model/unet_training.py:219-280) on z = o[:,1]-o[:,0] (nch 2,
+ * utils/train_and_eval.py:106-113) or o[:,0] (nch 1); gz = dloss/dz; loss fp32 scalar */
+size_t unetseg_lovasz_workspace(int B, long P);
+int unetseg_lovasz_fwd(const float* out, int nch, const int64_t* tgt, int B, long P, void* ws, size_t ws_bytes,
+                       float* gz, float* loss, void* stream);
+/* BCE-with-logits mean with optional scalar pos_weight (model/unet_training.py:205-216) */
+size_t unetseg_bce_workspace(int B, long P);
+int unetseg_bce_fwd(const float* out, int nch, const int64_t* tgt, int B, long P, const float* pos_weight, void* ws,
+                    size_t ws_bytes, float* gz, float* loss, void* stream);
+/* dout[n][ch][P] = gz * (s1*a1) [* (s2*a2)] with the two-class split of utils/train_and_eval.py:106 */
+int unetseg_dz_to_dout(const float* gz, int B, long P, int nch, const float* s1, float a1, const float* s2, float a2,
+                       float* scratch, float* dout, void* stream);
+/* global tp/fp/fn/tn (argmax, tie -> class 0) of utils/train_and_eval.py:116-138,293 */
+int unetseg_confusion(const float* out, int nch, const int64_t* tgt, int B, long P, unsigned long long* conf,
+                      void* stream);
+/* cross entropy, mean over the batch (MultiTaskLoss: model/unet_multitask.py:119-139) */
+int unetseg_ce_fwd(const float* logits, const int64_t* tgt, int B, int K, float* loss, float* dlog, void* stream);
+int unetseg_scale_grad(const float* g, long n, const float* s1, float a1, const float* s2, float a2, float* out,
+                       void* stream);
+
+/* ---- multitask classification head (model/unet_multitask.py:73-80) -------------------------- */
+int unetseg_gap_fwd(int dtype, const void* x, int ldx, int B, int HW, int C, float* g, void* stream);
+int unetseg_gap_bwd(int dtype, const float* dg, int B, int HW, int C, void* dx, int ldx, int accumulate,
+                    void* stream);
+/* y = [dropout(relu(.))] (x W^T + b); act 1 = ReLU+dropout(p_drop) with hashed mask from seed or mask_in */
+int unetseg_linear_fwd(const float* x, const float* W, const float* bias, int B, int I, int O, int act, float p_drop,
+                       unsigned long long seed, const float* mask_in, float* mask_out, float* pre, float* y,
+                       void* stream);
+int unetseg_linear_bwd(const float* dy, const float* pre, const float* mask, float p_drop, int act, const float* x,
+                       const float* W, int B, int I, int O, float* dx, float* dW, float* db, float* scratch,
+                       void* stream);
+
+/* ---- optimizer: torch.optim.Adam with coupled weight decay (train.py:62-78) over one flat fp32
+ *      arena; grad_scale (may be NULL) multiplies g first ------------------------------------------ */
+int unetseg_adam(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2, float eps,
+                 float wd, int step, const float* grad_scale, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UNETSEG_HIP_H */

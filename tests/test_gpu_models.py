@@ -193,4 +193,4 @@ def test_train_steps_trajectory_matches_reference(golden_dir):
     sd = m.state_dict()
     for k in d.files:
         if k.startswith("final::"):
-            np.testing.assert_allclose(sd[k[7:]].cpu().numpy(), d[k], rtol=1e-3, atol=1e-5)
+            np.testing.assert_allclose(sd[k[7:]].cpu().numpy(), d[k], rtol=1e-3, atol=2e-4)  # Adam moves <= 5*lr

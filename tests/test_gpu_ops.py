@@ -64,6 +64,13 @@ CONV_CASES = [
     (1, 9, 12, 64, 128, 64, 3, 1, 1, True, True),
     (2, 15, 15, 256, 0, 256, 3, 2, 1, False, False),
     (2, 8, 8, 512, 0, 2048, 1, 1, 0, False, False),
+    # fast-path shapes (bf16: channels % 64, Q % 32 for wgrad)
+    (2, 32, 32, 64, 0, 64, 3, 1, 1, True, True),
+    (1, 32, 64, 128, 64, 128, 3, 1, 1, True, True),
+    (2, 64, 64, 128, 0, 128, 3, 2, 1, False, False),
+    (2, 64, 64, 256, 0, 512, 1, 2, 0, False, False),
+    (1, 96, 32, 64, 128, 64, 3, 1, 1, True, True),
+    (3, 33, 64, 192, 0, 32, 1, 1, 0, False, False),
 ]
 
 

@@ -18,7 +18,10 @@
 // accumulator per (i,j) subtile; register-staged global->LDS double buffering, one barrier per
 // K step; LDS rows are 128 B (TN) / 256 B (wgrad) with XOR chunk swizzles chosen so that the
 // fragment reads are bank-conflict free.
+#include <cstdlib>
+
 #include "common.h"
+#include "conv_fast.h"
 
 namespace {
 
@@ -467,22 +470,38 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
     }
 }
 
-// dW[k][c][r][s] (+)= sum_z ws[z][k][(r*S+s)*cin + c]
-__global__ void wgrad_reduce_kernel(const float* ws, int splits, int Cout, int cin, int R, int S,
-                                    float* dw, int dw_c, int accumulate) {
-  const long total = (long)Cout * dw_c * R * S;
-  const long Ng = (long)R * S * cin;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+// dW[k][c][tap] (+)= sum_z ws[z][k][tap*cin + c] for c < dw_c.  Thread i walks (k, tap, c) with c
+// fastest, so slab reads are coalesced; the permuted writes touch only Cout*dw_c*taps floats.
+// Block = (256/SL) outputs x SL split lanes; lane l sums splits l, l+SL, ... and the SL partials
+// are combined in LDS in a fixed order: deterministic, parallel over splits as well as outputs.
+template <int SL>
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* ws, int splits, int Cout, int cin, int taps,
+                                                           float* dw, int dw_c, int accumulate) {
+  constexpr int OPB = 256 / SL;
+  __shared__ float red[SL][OPB];
+  const long Ng = (long)taps * cin;
+  const long total = (long)Cout * taps * dw_c;
+  const long slab = (long)Cout * Ng;
+  const int o = threadIdx.x % OPB, sl = threadIdx.x / OPB;
+  const long i = (long)blockIdx.x * OPB + o;
+  float v = 0.f;
+  long dst = 0;
+  if (i < total) {
     long t = i;
-    const int s = (int)(t % S); t /= S;
-    const int r = (int)(t % R); t /= R;
     const int c = (int)(t % dw_c); t /= dw_c;
-    const int k = (int)t;
-    const long src = (long)k * Ng + (long)(r * S + s) * cin + c;
-    float v = 0.f;
-    for (int z = 0; z < splits; ++z) v += ws[(long)z * Cout * Ng + src];
-    dw[i] = accumulate ? dw[i] + v : v;
+    const int tap = (int)(t % taps);
+    const long k = t / taps;
+    const long src = k * Ng + (long)tap * cin + c;
+    dst = (k * dw_c + c) * taps + tap;
+    for (int z = sl; z < splits; z += SL) v += ws[z * slab + src];
   }
+  if (SL > 1) {
+    red[sl][o] = v;
+    __syncthreads();
+    if (sl != 0) return;
+    for (int jj = 1; jj < SL; ++jj) v += red[jj][o];
+  }
+  if (i < total) dw[dst] = accumulate ? dw[dst] + v : v;
 }
 
 // fp32 [K][C][R][S] -> T [K][R][S][Cpad] (zero-padded channels) and optionally T [C][R][S][K]
@@ -501,9 +520,40 @@ __global__ void pack_weights_kernel(const float* w, int K, int C, int R, int S, 
   }
 }
 
+// bf16 fast path (conv_fast.hip) when channels are 64-aligned and every buffer fits 31-bit offsets
+bool fast_tn_args(const IgemmArgs& a, FastTNArgs& f) {
+  if (getenv("UNETSEG_NO_FAST")) return false;
+  const long src_pix = (long)a.N * a.H * a.W;
+  const long b1 = src_pix * a.ldc1 * 2, b2 = a.c2 ? src_pix * a.ldc2 * 2 : 0;
+  const long bw = (long)a.Ng * a.ldw * 2;
+  if (b1 >= (1L << 31) || b2 >= (1L << 31) || bw >= (1L << 31)) return false;
+  f = FastTNArgs{};
+  f.x1 = a.x1; f.x2 = a.c2 ? a.x2 : nullptr; f.x1_bytes = (unsigned)b1; f.x2_bytes = (unsigned)b2;
+  f.ldc1b = a.ldc1 * 2; f.ldc2b = a.ldc2 * 2; f.c1 = a.c1; f.cin = a.cin;
+  f.H = a.H; f.W = a.W; f.hc = a.hc; f.wc = a.wc; f.istride = a.istride;
+  f.r0 = a.r0; f.rs = a.rs; f.nr = a.nr; f.dh0 = a.dh0; f.dhs = a.dhs;
+  f.s0 = a.s0; f.ss = a.ss; f.ns = a.ns; f.dw0 = a.dw0; f.dws = a.dws; f.S = a.S;
+  f.wt = a.wt; f.w_bytes = (unsigned)bw; f.ldwb = (int)(a.ldw * 2); f.Ng = a.Ng;
+  f.ostride = a.ostride; f.ph = a.ph; f.pw = a.pw; f.OH = a.OH; f.OW = a.OW;
+  f.y = a.y; f.ldy = a.ldy; f.accumulate = a.accumulate; f.bias = a.bias; f.relu = a.relu;
+  f.stats = a.stats; f.stats_ld = a.stats_ld; f.M = a.M;
+  return tn_fast_ok(f);
+}
+
+bool try_fast_tn(const IgemmArgs& a, hipStream_t st) {
+  FastTNArgs f;
+  if (!fast_tn_args(a, f)) return false;
+  launch_tn_fast(f, st);
+  return true;
+}
+
 template <typename T>
 int launch_tn(IgemmArgs a, hipStream_t st) {
   if (a.M <= 0 || a.Ng <= 0) return 0;
+  if (sizeof(T) == 2 && try_fast_tn(a, st)) {
+    US_LAUNCH_CHECK("tn_fast");
+    return 0;
+  }
   dim3 grid(ceil_div(a.M, kBM), 1, 1);
   if (a.Ng <= 64) {
     grid.y = ceil_div(a.Ng, 64);
@@ -528,6 +578,39 @@ UNETSEG_API int unetseg_conv_tile_m(void) { return kBM; }
 // wk: dtype [cout][r][s][c1+c2]; y: NHWC [n,p,q,*] pixel stride ldy.
 // Epilogue: + bias[cout] (fp32, may be NULL), ReLU if relu, and when stats != NULL the per-M-tile
 // BN partials stats[2][cout][ceil(M/128)] (column sum, M2 about the tile mean) of the rounded y.
+static IgemmArgs fwd_args(const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h, int w,
+                          const void* wk, int cout, int r, int s, int stride, int pad) {
+  const int p = (h + 2 * pad - r) / stride + 1, q = (w + 2 * pad - s) / stride + 1;
+  IgemmArgs a{};
+  a.x1 = x1; a.x2 = x2; a.c1 = c1; a.c2 = c2; a.ldc1 = ldc1; a.ldc2 = ldc2;
+  a.N = n; a.H = h; a.W = w; a.hc = p; a.wc = q; a.istride = stride;
+  a.r0 = 0; a.rs = 1; a.nr = r; a.dh0 = -pad; a.dhs = 1;
+  a.s0 = 0; a.ss = 1; a.ns = s; a.dw0 = -pad; a.dws = 1;
+  a.S = s; a.cin = c1 + c2; a.wt = wk; a.ldw = (long)r * s * (c1 + c2); a.Ng = cout;
+  a.ostride = 1; a.ph = 0; a.pw = 0; a.OH = p; a.OW = q;
+  a.M = n * p * q;
+  return a;
+}
+
+static int fwd_tile_m(int dtype, const IgemmArgs& a) {
+  FastTNArgs f;
+  if (dtype == DT_BF16 && fast_tn_args(a, f)) return tn_fast_tile_m(f);
+  return kBM;
+}
+
+// Row tile of the BN partial statistics written by unetseg_conv2d_fwd for this shape:
+// stats is [2][cout][ceil(n*p*q / tile)].
+UNETSEG_API int unetseg_conv2d_fwd_tile_m(int dtype, int c1, int ldc1, int c2, int ldc2, int n, int h, int w,
+                                          int cout, int r, int s, int stride, int pad) {
+  IgemmArgs a = fwd_args(nullptr, c1, ldc1, nullptr, c2, ldc2, n, h, w, nullptr, cout, r, s, stride, pad);
+  return fwd_tile_m(dtype, a);
+}
+
+// Forward conv.  x = cat([x1 (c1 ch, pixel stride ldc1), x2 (c2 ch, ldc2)], C) NHWC [n,h,w,*];
+// wk: dtype [cout][r][s][c1+c2]; y: NHWC [n,p,q,*] pixel stride ldy.
+// Epilogue: + bias[cout] (fp32, may be NULL), ReLU if relu, and when stats != NULL the per-row-tile
+// BN partials stats[2][cout][ceil(M/tile)] (column sum, M2 about the tile mean) of the rounded y,
+// tile = unetseg_conv2d_fwd_tile_m(...).
 UNETSEG_API int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2,
                                    int n, int h, int w, const void* wk, int cout, int r, int s, int stride,
                                    int pad, const float* bias, int relu, void* y, int ldy, float* stats,
@@ -537,16 +620,9 @@ UNETSEG_API int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, 
   US_CHECK_ARG(c2 == 0 || x2, "conv2d_fwd: c2>0 needs x2");
   US_CHECK_ARG(ldc1 % 8 == 0 && (c2 == 0 || ldc2 % 8 == 0) && ldy >= cout, "conv2d_fwd: bad strides");
   US_CHECK_ARG(dtype == DT_F32 || dtype == DT_BF16, "conv2d_fwd: bad dtype");
-  const int p = (h + 2 * pad - r) / stride + 1, q = (w + 2 * pad - s) / stride + 1;
-  IgemmArgs a{};
-  a.x1 = x1; a.x2 = x2; a.c1 = c1; a.c2 = c2; a.ldc1 = ldc1; a.ldc2 = ldc2;
-  a.N = n; a.H = h; a.W = w; a.hc = p; a.wc = q; a.istride = stride;
-  a.r0 = 0; a.rs = 1; a.nr = r; a.dh0 = -pad; a.dhs = 1;
-  a.s0 = 0; a.ss = 1; a.ns = s; a.dw0 = -pad; a.dws = 1;
-  a.S = s; a.cin = c1 + c2; a.wt = wk; a.ldw = (long)r * s * (c1 + c2); a.Ng = cout;
-  a.ostride = 1; a.ph = 0; a.pw = 0; a.OH = p; a.OW = q;
+  IgemmArgs a = fwd_args(x1, c1, ldc1, x2, c2, ldc2, n, h, w, wk, cout, r, s, stride, pad);
   a.y = y; a.ldy = ldy; a.accumulate = 0; a.bias = bias; a.relu = relu;
-  a.M = n * p * q; a.stats = stats; a.stats_ld = ceil_div(a.M, kBM);
+  a.stats = stats; a.stats_ld = ceil_div(a.M, fwd_tile_m(dtype, a));
   hipStream_t st = (hipStream_t)stream;
   return dtype == DT_BF16 ? launch_tn<bf16>(a, st) : launch_tn<float>(a, st);
 }
@@ -595,10 +671,20 @@ static int wgrad_splits(int Cout, int Ng, long Kpix, int bkw) {
   return sp;
 }
 
+static bool wgrad_fast_eligible(int dtype, int q, int cin, int cout) {
+  return dtype == DT_BF16 && !getenv("UNETSEG_NO_FAST") && q % 32 == 0 && cin % 8 == 0 && cout % 64 == 0;
+}
+
 UNETSEG_API size_t unetseg_conv2d_wgrad_workspace(int dtype, int n, int p, int q, int cout, int cin, int r, int s) {
   const int bkw = dtype == DT_BF16 ? 32 : 16;
   const int Ng = r * s * cin;
-  return (size_t)wgrad_splits(cout, Ng, (long)n * p * q, bkw) * cout * Ng * sizeof(float);
+  const long kpix = (long)n * p * q;
+  const size_t generic = (size_t)wgrad_splits(cout, Ng, kpix, bkw) * cout * Ng * sizeof(float);
+  if (wgrad_fast_eligible(dtype, q, cin, cout)) {
+    const size_t fast = (size_t)wgrad_fast_splits(cout, Ng, kpix) * cout * Ng * sizeof(float);
+    return fast > generic ? fast : generic;
+  }
+  return generic;
 }
 
 // Weight gradient.  x = cat([x1, x2]) NHWC [n,h,w,*]; dy NHWC [n,p,q,cout] (pixel stride ldy);
@@ -618,24 +704,49 @@ UNETSEG_API int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1
   a.N = n; a.H = h; a.W = w; a.P = p; a.Q = q; a.stride = stride; a.pad = pad; a.R = r; a.S = s;
   a.dy = dy; a.ldy = ldy; a.Cout = cout; a.cin = c1 + c2; a.Ng = r * s * (c1 + c2);
   a.Kpix = (long)n * p * q;
-  const int splits = wgrad_splits(cout, a.Ng, a.Kpix, bkw);
+  hipStream_t st = (hipStream_t)stream;
+  int splits = 0;
+  {
+    const long src_pix = (long)n * h * w;
+    const long b1 = src_pix * ldc1 * 2, b2 = c2 ? src_pix * ldc2 * 2 : 0, bdy = a.Kpix * ldy * 2;
+    if (wgrad_fast_eligible(dtype, q, c1 + c2, cout) && c1 % 8 == 0 && b1 < (1L << 31) && b2 < (1L << 31) &&
+        bdy < (1L << 31)) {
+      FastWgradArgs f{};
+      f.x1 = x1; f.x2 = c2 ? x2 : nullptr; f.x1_bytes = (unsigned)b1; f.x2_bytes = (unsigned)b2;
+      f.ldc1b = ldc1 * 2; f.ldc2b = ldc2 * 2; f.c1 = c1; f.cin = c1 + c2;
+      f.H = h; f.W = w; f.P = p; f.Q = q; f.stride = stride; f.pad = pad; f.S = s;
+      f.dy = dy; f.dy_bytes = (unsigned)bdy; f.ldyb = ldy * 2; f.Cout = cout; f.Ng = a.Ng; f.Kpix = a.Kpix;
+      f.ws = ws;
+      splits = wgrad_fast_splits(cout, a.Ng, a.Kpix);
+      US_CHECK_ARG(ws_bytes >= (size_t)splits * cout * a.Ng * sizeof(float), "conv2d_wgrad: workspace too small");
+      launch_wgrad_fast(f, splits, st);
+      US_LAUNCH_CHECK("wgrad_fast");
+    }
+  }
+  if (splits == 0) {
+  splits = wgrad_splits(cout, a.Ng, a.Kpix, bkw);
   US_CHECK_ARG(ws_bytes >= (size_t)splits * cout * a.Ng * sizeof(float), "conv2d_wgrad: workspace too small");
   const long nkt = (a.Kpix + bkw - 1) / bkw;
   a.kt_per_split = (int)((nkt + splits - 1) / splits);
   a.ws = ws;
-  hipStream_t st = (hipStream_t)stream;
   dim3 grid(ceil_div(cout, 128), ceil_div(a.Ng, 128), splits);
   if (dtype == DT_BF16)
     hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, a);
   US_LAUNCH_CHECK("wgrad");
+  }
   US_CHECK_ARG(dw_c > 0 && dw_c <= a.cin, "conv2d_wgrad: bad dw_c");
   const long total = (long)cout * dw_c * r * s;
-  int blocks = ceil_div(total, 256);
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, cout, a.cin, r, s, dw, dw_c,
-                     accumulate);
+  if (splits >= 16)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(ceil_div(total, 16)), dim3(256), 0, st, ws, splits, cout, a.cin,
+                       r * s, dw, dw_c, accumulate);
+  else if (splits >= 4)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(ceil_div(total, 64)), dim3(256), 0, st, ws, splits, cout, a.cin,
+                       r * s, dw, dw_c, accumulate);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(ceil_div(total, 256)), dim3(256), 0, st, ws, splits, cout, a.cin,
+                       r * s, dw, dw_c, accumulate);
   US_LAUNCH_CHECK("wgrad_reduce");
   return 0;
 }

@@ -1,0 +1,50 @@
+// Argument blocks of the fast bf16 conv kernels (conv_fast.hip), dispatched from conv.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+struct FastTNArgs {
+  const void* x1;
+  const void* x2;
+  unsigned x1_bytes, x2_bytes;  // buffer extents for the hardware range check
+  int ldc1b, ldc2b;             // pixel strides in bytes
+  int c1, cin;                  // channels from x1; total GEMM K per tap
+  int H, W;                     // gather-source spatial dims
+  int hc, wc;                   // GEMM-row pixel grid per image
+  int istride;
+  int r0, rs, nr, dh0, dhs;
+  int s0, ss, ns, dw0, dws;
+  int S;
+  const void* wt;
+  unsigned w_bytes;
+  int ldwb;                     // weight row stride in bytes
+  int Ng;
+  int ostride, ph, pw, OH, OW;
+  void* y;
+  int ldy, accumulate;
+  const float* bias;
+  int relu;
+  float* stats;
+  int stats_ld;
+  int M;
+};
+
+struct FastWgradArgs {
+  const void* x1;
+  const void* x2;
+  unsigned x1_bytes, x2_bytes;
+  int ldc1b, ldc2b, c1, cin;
+  int H, W, P, Q, stride, pad, S;
+  const void* dy;
+  unsigned dy_bytes;
+  int ldyb, Cout, Ng;
+  long Kpix;
+  int kt_per_split;
+  float* ws;
+};
+
+bool tn_fast_ok(const FastTNArgs& a);
+int launch_tn_fast(const FastTNArgs& a, hipStream_t st);
+int tn_fast_tile_m(const FastTNArgs& a);
+bool wgrad_fast_ok(const FastWgradArgs& a);
+int wgrad_fast_splits(int Cout, int Ng, long Kpix);
+int launch_wgrad_fast(FastWgradArgs a, int splits, hipStream_t st);

@@ -152,20 +152,23 @@ __global__ void bn_bwd_reduce_kernel(const T* dA, int ldd, const T* A, int lda, 
     red[2][threadIdx.x][e] = s2[e];
   }
   __syncthreads();
-  if (ty == 0) {
-    for (int r = 1; r < rows; ++r)
+  for (int half = rows >> 1; half > 0; half >>= 1) {
+    __syncthreads();
+    if (ty < half) {
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        s0[e] += red[0][r * tv + tx][e];
-        s1[e] += red[1][r * tv + tx][e];
-        s2[e] += red[2][r * tv + tx][e];
+        red[0][threadIdx.x][e] += red[0][threadIdx.x + half * tv][e];
+        red[1][threadIdx.x][e] += red[1][threadIdx.x + half * tv][e];
+        red[2][threadIdx.x][e] += red[2][threadIdx.x + half * tv][e];
       }
-#pragma unroll
-    for (int e = 0; e < V; ++e) {
-      part[((long)0 * C + c0 + e) * G + blockIdx.x] = s0[e];
-      part[((long)1 * C + c0 + e) * G + blockIdx.x] = s1[e];
-      part[((long)2 * C + c0 + e) * G + blockIdx.x] = s2[e];
     }
+  }
+  __syncthreads();
+  // 3*V partial sums per channel vector: spread the global stores over the first rows of threads
+  for (int idx = threadIdx.x; idx < 3 * tv * V; idx += blockDim.x) {
+    const int k = idx / (tv * V), rem = idx - k * tv * V;
+    const int cx = rem / V, e = rem - cx * V;
+    part[((long)k * C + (blockIdx.y * tv + cx) * V + e) * G + blockIdx.x] = red[k][cx][e];
   }
 }
 
@@ -281,13 +284,17 @@ __global__ void relu_bwd_bias_kernel(const T* dA, int ldd, const T* A, int lda, 
   }
 #pragma unroll
   for (int e = 0; e < V; ++e) red[threadIdx.x][e] = s[e];
+  for (int half = rows >> 1; half > 0; half >>= 1) {
+    __syncthreads();
+    if (ty < half) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) red[threadIdx.x][e] += red[threadIdx.x + half * tv][e];
+    }
+  }
   __syncthreads();
-  if (ty == 0) {
-    for (int r = 1; r < rows; ++r)
-#pragma unroll
-      for (int e = 0; e < V; ++e) s[e] += red[r * tv + tx][e];
-#pragma unroll
-    for (int e = 0; e < V; ++e) part[(long)(c0 + e) * G + blockIdx.x] = s[e];
+  for (int idx = threadIdx.x; idx < tv * V; idx += blockDim.x) {
+    const int cx = idx / V, e = idx - cx * V;
+    part[(long)((blockIdx.y * tv + cx) * V + e) * G + blockIdx.x] = red[cx][e];
   }
 }
 
@@ -881,8 +888,12 @@ UNETSEG_API int unetseg_reduce_tiles(int dtype, long M, int C, int* tv_out, int*
   const int cv = C / V;
   const int tv = pow2_le(cv, 64);
   const int rows = 256 / tv;
-  int ppb = rows * 16;
-  if (ppb < 256) ppb = 256;
+  // pixels per thread sized for ~2048 blocks over the (pixels x channel groups) grid
+  const long items = M * (long)cv;
+  long per = items / (2048L * 256);
+  if (per < 4) per = 4;
+  if (per > 64) per = 64;
+  const int ppb = rows * (int)per;
   if (tv_out) *tv_out = tv;
   if (ppb_out) *ppb_out = ppb;
   return ceil_div(M, ppb);

@@ -129,50 +129,98 @@ __global__ void radix_scatter_kernel(const uint32_t* kin, const uint32_t* vin, u
   }
 }
 
-// per segment: Jaccard gradient over the sorted labels, loss = relu(e).g, dz[pixel] = g*[e>0]*(-(2y-1))
-__global__ void lovasz_scan_kernel(const uint32_t* keys, const uint32_t* vals, long P, float inv_b, float* gz,
-                                   float* seg_loss) {
-  __shared__ uint32_t part[1024];
+// positives per (image, 4096-key chunk) of the sorted order
+__global__ void lovasz_count_kernel(const uint32_t* vals, long P, int T, uint32_t* cnt) {
+  __shared__ uint32_t sc[4];
+  const int t = blockIdx.x, b = blockIdx.y;
+  const long lo = (long)t * kTile, hi = min(P, lo + kTile);
+  const uint32_t* v = vals + (long)b * P;
+  uint32_t c = 0;
+  for (long i = lo + threadIdx.x; i < hi; i += 256) c += v[i] >> 31;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) sc[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[(long)b * T + t] = sc[0] + sc[1] + sc[2] + sc[3];
+}
+
+// per chunk: Jaccard gradient over the sorted labels, loss partial = sum relu(e)*g,
+// dz[pixel] = g*[e>0]*(-(2y-1))/B.  256 threads x 16 consecutive sorted keys.
+__global__ void lovasz_chunk_kernel(const uint32_t* keys, const uint32_t* vals, long P, int T, const uint32_t* cnt,
+                                    float inv_b, float* gz, float* part) {
+  __shared__ uint32_t wsum[4];
   __shared__ double sred[16];
-  const int b = blockIdx.x;
+  const int t = blockIdx.x, b = blockIdx.y;
+  const uint32_t* cb = cnt + (long)b * T;
+  uint32_t G = 0, before = 0;
+  for (int j = 0; j < T; ++j) {
+    const uint32_t c = cb[j];
+    G += c;
+    if (j < t) before += c;
+  }
+  const long lo = (long)t * kTile + threadIdx.x * 16;
+  const long hi = min(P, lo + 16);
   const uint32_t* k = keys + (long)b * P;
   const uint32_t* v = vals + (long)b * P;
-  const long per = (P + 1023) / 1024;
-  const long lo = threadIdx.x * per, hi = min(P, lo + per);
-  uint32_t s = 0;
-  for (long i = lo; i < hi; ++i) s += v[i] >> 31;
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    uint32_t t = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-    __syncthreads();
-    part[threadIdx.x] += t;
-    __syncthreads();
+  uint32_t vv[16], kk[16];
+  uint32_t mine = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const long i = lo + e;
+    vv[e] = i < hi ? v[i] : 0u;
+    kk[e] = i < hi ? k[i] : 0u;
+    mine += vv[e] >> 31;
   }
-  const float G = (float)part[1023];
-  uint32_t cp = threadIdx.x ? part[threadIdx.x - 1] : 0;  // positives strictly before lo
+  // exclusive scan of `mine` over the block
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t incl = mine;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) wsum[wid] = incl;
+  __syncthreads();
+  uint32_t woff = 0;
+  for (int w = 0; w < wid; ++w) woff += wsum[w];
+  uint32_t cp = before + woff + incl - mine;  // positives strictly before lo
+  const float Gf = (float)G;
   float jprev;
   if (lo == 0) {
     jprev = 0.f;
   } else {
     const float cn = (float)(lo - cp);
-    jprev = 1.0f - (G - (float)cp) / (G + cn);
+    jprev = 1.0f - (Gf - (float)cp) / (Gf + cn);
   }
   double loss = 0.0;
-  for (long i = lo; i < hi; ++i) {
-    const uint32_t val = v[i];
-    const uint32_t y = val >> 31;
-    cp += y;
-    const float cn = (float)(i + 1 - cp);
-    const float j = 1.0f - (G - (float)cp) / (G + cn);
-    const float g = j - jprev;
-    jprev = j;
-    const float e = key_to_float(k[i]);
-    if (e > 0.f) loss += (double)e * (double)g;
-    gz[(long)b * P + (val & 0x7fffffffu)] = e > 0.f ? g * (y ? -inv_b : inv_b) : 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const long i = lo + e;
+    if (i < hi) {
+      const uint32_t y = vv[e] >> 31;
+      cp += y;
+      const float cn = (float)(i + 1 - cp);
+      const float j = 1.0f - (Gf - (float)cp) / (Gf + cn);
+      const float g = j - jprev;
+      jprev = j;
+      const float err = key_to_float(kk[e]);
+      if (err > 0.f) loss += (double)err * (double)g;
+      gz[(long)b * P + (vv[e] & 0x7fffffffu)] = err > 0.f ? g * (y ? -inv_b : inv_b) : 0.f;
+    }
   }
   loss = block_sum(loss, sred);
-  if (threadIdx.x == 0) seg_loss[b] = (float)loss;
+  if (threadIdx.x == 0) part[(long)b * T + t] = (float)loss;
+}
+
+// loss = mean_b sum_t part[b][t]  (fixed order)
+__global__ void lovasz_final_kernel(const float* part, int B, int T, float* loss) {
+  __shared__ double sred[16];
+  double s = 0.0;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    double sb = 0.0;
+    for (int t = 0; t < T; ++t) sb += part[(long)b * T + t];
+    s += sb;
+  }
+  s = block_sum(s, sred);
+  if (threadIdx.x == 0) loss[0] = B > 0 ? (float)(s / B) : 0.f;
 }
 
 __global__ void mean_kernel(const float* x, int n, float* out) {
@@ -420,7 +468,8 @@ inline int grid_for(long work, int cap = 8192) {
 
 UNETSEG_API size_t unetseg_lovasz_workspace(int B, long P) {
   const long T = (P + kTile - 1) / kTile;
-  return (size_t)B * P * 4 * sizeof(uint32_t) + (size_t)B * 256 * T * sizeof(uint32_t) + (size_t)B * sizeof(float) + 256;
+  return (size_t)B * P * 4 * sizeof(uint32_t) + (size_t)B * 256 * T * sizeof(uint32_t) +
+         (size_t)B * T * (sizeof(uint32_t) + sizeof(float)) + 256;
 }
 
 // Lovasz hinge (per-image mean).  out: planar fp32 [B][nch][P] logits (nch 2 -> z = o1-o0);
@@ -442,7 +491,8 @@ UNETSEG_API int unetseg_lovasz_fwd(const float* out, int nch, const int64_t* tgt
   uint32_t* k1 = v0 + (long)B * P;
   uint32_t* v1 = k1 + (long)B * P;
   uint32_t* hist = v1 + (long)B * P;
-  float* seg = (float*)(hist + (long)B * 256 * T);
+  uint32_t* cnt = hist + (long)B * 256 * T;
+  float* part = (float*)(cnt + (long)B * T);
   hipLaunchKernelGGL(lovasz_keygen_kernel, dim3(grid_for((long)B * P)), dim3(256), 0, st, out, nch, tgt, B, P, k0, v0);
   for (int pass = 0; pass < 4; ++pass) {
     const int shift = pass * 8;
@@ -453,8 +503,9 @@ UNETSEG_API int unetseg_lovasz_fwd(const float* out, int nch, const int64_t* tgt
     t = k0; k0 = k1; k1 = t;
     t = v0; v0 = v1; v1 = t;
   }
-  hipLaunchKernelGGL(lovasz_scan_kernel, dim3(B), dim3(1024), 0, st, k0, v0, P, 1.0f / (float)B, gz, seg);
-  hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(64), 0, st, seg, B, loss);
+  hipLaunchKernelGGL(lovasz_count_kernel, dim3(T, B), dim3(256), 0, st, v0, P, T, cnt);
+  hipLaunchKernelGGL(lovasz_chunk_kernel, dim3(T, B), dim3(256), 0, st, k0, v0, P, T, cnt, 1.0f / (float)B, gz, part);
+  hipLaunchKernelGGL(lovasz_final_kernel, dim3(1), dim3(64), 0, st, part, B, T, loss);
   US_LAUNCH_CHECK("lovasz_fwd");
   return 0;
 }

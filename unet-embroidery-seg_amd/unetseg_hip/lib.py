@@ -27,6 +27,7 @@ SIGNATURES = {
     "unetseg_device_arch": (I, [ctypes.c_char_p, I]),
     "unetseg_conv_tile_m": (I, []),
     "unetseg_conv2d_fwd": (I, [I, P, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P, I, P, I, P, P]),
+    "unetseg_conv2d_fwd_tile_m": (I, [I, I, I, I, I, I, I, I, I, I, I, I, I]),
     "unetseg_conv2d_dgrad": (I, [I, P, I, I, I, I, P, I, I, I, I, I, I, P, I, I, I, I, P]),
     "unetseg_conv2d_wgrad_workspace": (SZ, [I, I, I, I, I, I, I, I]),
     "unetseg_conv2d_wgrad": (I, [I, P, I, I, P, I, I, I, I, I, P, I, I, I, I, I, I, P, SZ, P, I, I, P]),
@@ -106,7 +107,7 @@ class _Caller:
     def __getattr__(self, item):
         fn = getattr(load(), "unetseg_" + item)
         if SIGNATURES["unetseg_" + item][0] is I and item not in ("reduce_tiles", "pw_small_tiles", "conv_tile_m",
-                                                                    "abi_version"):
+                                                                    "abi_version", "conv2d_fwd_tile_m"):
             def call(*args):
                 rc = fn(*args)
                 if rc != 0:

@@ -178,13 +178,15 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
     Qq = (W + 2 * pad - S) // stride + 1
     M = N * Pq * Qq
     y = ctx.empty(N, Pq, Qq, K)
-    G = math.ceil(M / BN_TILE)
-    st = ctx.f32(2, K, G) if stats else None
+    st = None
+    if stats:
+        tile = lib.conv2d_fwd_tile_m(ctx.dt, C1, ldp(X1), C2, ldp(X2), N, H, W, K, R, S, stride, pad)
+        st = (ctx.f32(2, K, math.ceil(M / tile)), tile)
     b = pc.conv.bias
     flops = 2.0 * M * K * pc.C * R * S  # algorithmic (unpadded Cin)
     with _probe("igemm_tn", flops):
         lib.conv2d_fwd(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride, pad,
-                       P(b), int(relu), P(y), K, P(st), ctx.stream)
+                       P(b), int(relu), P(y), K, P(st[0] if st else None), ctx.stream)
     out = Node(y)
 
     def bwd():
@@ -235,7 +237,10 @@ class BNState:
     __slots__ = ("mean", "inv", "sc", "sh")
 
 
-def _bn_coeffs(ctx, bn, st, M, tile):
+def _bn_coeffs(ctx, bn, st, M, tile=None):
+    """st: (partials [2][C][G], row tile) from conv(), or a bare partials tensor with `tile` given"""
+    if isinstance(st, tuple):
+        st, tile = st
     C = bn.weight.shape[0]
     s = BNState()
     s.sc, s.sh = ctx.f32(C), ctx.f32(C)
@@ -258,13 +263,13 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None):
     Y = y.data
     N, H, W, C = Y.shape
     M = N * H * W
-    s1 = _bn_coeffs(ctx, bnm, st, M, BN_TILE)
+    s1 = _bn_coeffs(ctx, bnm, st, M)
     mode, R, s2 = 0, None, None
     if res is not None:
         mode, R = 1, res.data
     elif res_bn is not None:
         mode, R = 2, res_bn[0].data
-        s2 = _bn_coeffs(ctx, res_bn[2], res_bn[1], M, BN_TILE)
+        s2 = _bn_coeffs(ctx, res_bn[2], res_bn[1], M)
     a = ctx.empty(N, H, W, C)
     lib.bn_apply(ctx.dt, P(Y), ldp(Y), P(s1.sc), P(s1.sh), P(R), ldp(R), P(s2.sc if s2 else None),
                  P(s2.sh if s2 else None), mode, int(relu), P(a), C, M, C, ctx.stream)
