@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--loss", default="lovasz_hinge")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (N=1)")
-    ap.add_argument("--cpu-batch", type=int, default=1)
+    ap.add_argument("--cpu-batch", type=int, default=4, help="images in the bounded CPU sample")
     ap.add_argument("--probe", type=int, default=1)
     return ap.parse_args()
 
@@ -68,6 +68,23 @@ def cpu_baseline(model_name, size, batch):
     return {"value": round(batch / t, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"oracle fp32 {model_name} {size}x{size} batch {batch}, 1 warmup + 2 timed train steps "
                       f"(fwd+lovasz+bwd+Adam), best step {t:.2f} s, torch {torch.__version__} CPU"}
+
+
+def pmc_traffic(workload, kind):
+    """HBM bytes per launch of `kind` from the committed PMC summary (tools/pmc_traffic.py), if one was
+    measured for this exact workload; bench.py cannot profile itself, so the counters come from two
+    separate rocprofv3 --pmc passes of this same command (profiles/README.md)."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload and kind in d.get("groups", {}):
+            best = (round(d["groups"][kind]["traffic_bytes_per_launch"]), os.path.relpath(f, REPO))
+    return best
 
 
 def main():
@@ -135,23 +152,26 @@ def main():
     imgs_per_s = args.batch * world * args.steps / wall
     final_loss = float(loss.item())
 
+    workload = f"{args.model} binary seg {args.size}x{args.size}, per-GPU batch {args.batch}, {args.loss} + Adam"
     roof = None
     if args.probe:
         ops.PROBE = []
         step(0)
         torch.cuda.synchronize()
         kinds = {}
-        for kind, flops, e0, e1 in ops.PROBE:
+        for kind, flops, nl, e0, e1 in ops.PROBE:
             d = kinds.setdefault(kind, [0.0, 0.0, 0])
             d[0] += flops
             d[1] += e0.elapsed_time(e1) * 1e-3
-            d[2] += 1
+            d[2] += nl
         ops.PROBE = None
         dom = max(kinds, key=lambda k: kinds[k][1])
         fl, sec, n = kinds[dom]
         ach = fl / sec / 1e12
+        tr = pmc_traffic(workload, dom)
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": tr[0] if tr else None,
+                "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": tr[1] if tr else None,
                 "launches_per_step": n, "avg_launch_us": round(1e6 * sec / n, 2),
                 "algorithmic_gflop_per_step": round(fl / 1e9, 1),
                 "kernels": {k: {"tflops": round(v[0] / v[1] / 1e12, 2), "ms_per_step": round(1e3 * v[1], 3),
@@ -168,8 +188,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (seeded 512x512 RGB ellipse images + masks, resident in HBM)",
-            "config": {"workload": f"{args.model} binary seg {args.size}x{args.size}, per-GPU batch {args.batch}, "
-                                   f"{args.loss} + Adam", "global_batch": args.batch * world,
+            "config": {"workload": workload, "global_batch": args.batch * world,
                        "image_size": args.size, "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu,
             "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),

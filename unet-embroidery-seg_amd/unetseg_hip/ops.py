@@ -43,13 +43,14 @@ class Node:
 
 _WORKSPACES = {}
 
-#: when a list, conv launches append (kernel, algorithmic_flops, start_event, end_event) (bench.py probe)
+#: when a list, conv calls append (kernel, algorithmic_flops, kernel_launches, start_event, end_event)
+#: (bench.py probe; a stride-2 dgrad call launches one GEMM per output parity class)
 PROBE = None
 
 
 class _probe:
-    def __init__(self, kind, flops):
-        self.kind, self.flops = kind, flops
+    def __init__(self, kind, flops, launches=1):
+        self.kind, self.flops, self.launches = kind, flops, launches
 
     def __enter__(self):
         if PROBE is not None:
@@ -61,7 +62,7 @@ class _probe:
     def __exit__(self, *a):
         if PROBE is not None:
             self.e1.record()
-            PROBE.append((self.kind, self.flops, self.e0, self.e1))
+            PROBE.append((self.kind, self.flops, self.launches, self.e0, self.e1))
 
 
 def workspace(nbytes, device):
@@ -216,12 +217,12 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
         if x2 is None:
             if x1.need_grad:
                 g, acc = gbuf(ctx, x1)
-                with _probe("igemm_tn", flops):
+                with _probe("igemm_tn", flops, stride * stride):
                     lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, R, S, stride, pad, P(g),
                                      ldp(g), H, W, acc, ctx.stream)
         elif x1.need_grad or x2.need_grad:
             g = ctx.empty(N, H, W, cin)
-            with _probe("igemm_tn", flops):
+            with _probe("igemm_tn", flops, stride * stride):
                 lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, cin, R, S, stride, pad, P(g), cin,
                                  H, W, 0, ctx.stream)
             give_grad(ctx, x1, g[..., :C1])

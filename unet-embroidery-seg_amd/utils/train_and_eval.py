@@ -119,6 +119,69 @@ def evaluate_binary(model, val_loader, device, loss_name: str, pos_weight, ignor
     return metrics
 
 
+def train_one_epoch_multitask(model, optimizer, train_loader, device, criterion, scaler, amp=True, max_batches=None,
+                              hook=None):
+    """train.py:225-250 (the reference keeps this loop inline): autocast fwd, fused BCE/Lovasz + CE,
+    scaled backward, step.  Loss sums and the cls-accuracy counters stay on the device; one host read
+    at the end of the epoch.  Returns (loss, seg_loss, cls_loss, cls_acc%) averaged like the reference
+    (sums / len(train_loader))."""
+    model.train()
+    sums = torch.zeros(3, dtype=torch.float64, device=device)
+    correct = torch.zeros((), dtype=torch.int64, device=device)
+    total = 0
+    for batch_idx, batch in enumerate(train_loader):
+        if max_batches and batch_idx >= max_batches:
+            break
+        images, seg_targets, _, cls_targets = batch
+        images, seg_targets, cls_targets = images.to(device), seg_targets.to(device), cls_targets.to(device)
+        with autocast(device_type=device.type, enabled=amp and device.type == "cuda"):
+            seg_logits, cls_logits = model(images)
+            loss, seg_loss, cls_loss = criterion(seg_logits, cls_logits, seg_targets, cls_targets)
+        optimizer.zero_grad()
+        if scaler is not None:
+            scaler.scale(loss).backward()
+            scaler.step(optimizer)
+            scaler.update()
+        else:
+            loss.backward()
+            optimizer.step()
+        sums += torch.stack([loss.detach(), seg_loss.detach(), cls_loss.detach()]).double()
+        correct += cls_logits.detach().argmax(1).eq(cls_targets).sum()
+        total += cls_targets.size(0)
+        if hook is not None:
+            hook(batch_idx)
+    n = max(len(train_loader), 1)
+    l, sl, cl = (float(v) / n for v in sums.tolist())
+    return l, sl, cl, 100.0 * float(correct.item()) / max(total, 1)
+
+
+def evaluate_multitask(model, loader, device, criterion, max_batches=None):
+    """train.py:294-355 / val.py:73-110: eval-mode forward; seg IoU = I/(U+1e-6), Dice = 2I/(|P|+|T|+1e-6)
+    with P = sigmoid(seg) > 0.5 (fused confusion kernel, u64 counts on the device); cls accuracy %."""
+    model.eval()
+    sums = torch.zeros(3, dtype=torch.float64, device=device)
+    conf = torch.zeros(4, dtype=torch.int64, device=device)
+    correct = torch.zeros((), dtype=torch.int64, device=device)
+    total = 0
+    with torch.no_grad():
+        for batch_idx, batch in enumerate(loader):
+            if max_batches and batch_idx >= max_batches:
+                break
+            images, seg_targets, _, cls_targets = batch
+            images, seg_targets, cls_targets = images.to(device), seg_targets.to(device), cls_targets.to(device)
+            seg_logits, cls_logits = model(images)
+            loss, seg_loss, cls_loss = criterion(seg_logits, cls_logits, seg_targets, cls_targets)
+            sums += torch.stack([loss, seg_loss, cls_loss]).double()
+            losses.binary_confusion(seg_logits, seg_targets, conf)
+            correct += cls_logits.argmax(1).eq(cls_targets).sum()
+            total += cls_targets.size(0)
+    tp, fp, fn, _tn = (float(v) for v in conf.tolist())
+    n = max(len(loader), 1)
+    l, sl, cl = (float(v) / n for v in sums.tolist())
+    return {"Loss": l, "Seg Loss": sl, "Cls Loss": cl, "IoU": tp / (tp + fp + fn + 1e-6),
+            "Dice": 2 * tp / ((tp + fp) + (tp + fn) + 1e-6), "Cls Acc": 100.0 * float(correct.item()) / max(total, 1)}
+
+
 def _out_of_scope(*_a, **_k):
     raise NotImplementedError("the multiclass task is outside the hot-path scope (SURVEY.md §2.1)")
 
