@@ -159,7 +159,7 @@ def main():
         step(0)
         torch.cuda.synchronize()
         kinds = {}
-        for kind, flops, nl, e0, e1 in ops.PROBE:
+        for kind, flops, nl, e0, e1, _ in ops.PROBE:
             d = kinds.setdefault(kind, [0.0, 0.0, 0])
             d[0] += flops
             d[1] += e0.elapsed_time(e1) * 1e-3

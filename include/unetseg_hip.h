@@ -44,6 +44,16 @@ int unetseg_device_arch(char* buf, int n);
 /* fp32 [K][C][R][S] -> wk dtype [K][R][S][Cpad] (fwd) and, if wt != NULL, wt dtype [C][R][S][K] (dgrad) */
 int unetseg_pack_conv_weight(int dtype, const float* w, int K, int C, int R, int S, int Cpad, void* wk, void* wt,
                              void* stream);
+/* one conv of a batched pack; `desc` arrays of these live in DEVICE memory */
+typedef struct UnetsegPackDesc {
+  const float* w;  /* fp32 [K][C][R][S] */
+  void* wk;        /* dtype [K][R][S][Cpad] */
+  void* wt;        /* dtype [C][R][S][K] or NULL */
+  long long start; /* first packed element of this conv in the batch (ascending, desc[0].start == 0) */
+  int K, C, R, S, Cpad, pad_;
+} UnetsegPackDesc;
+/* every conv weight of a model in one launch (total = sum of K*R*S*Cpad) */
+int unetseg_pack_conv_weights(int dtype, const void* desc, int n, long total, void* stream);
 /* legacy generic row tile (kept for ABI v1 callers) */
 int unetseg_conv_tile_m(void);
 /* row tile of the BN partial statistics unetseg_conv2d_fwd writes for this shape */

@@ -91,3 +91,13 @@ __device__ __forceinline__ F block_sum(F v, F* scratch /* >= 16 entries */) {
 }
 
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+// one conv weight of a batched pack (unetseg_pack_conv_weights); layout shared with the host
+struct UnetsegPackDesc {
+  const float* w;   // fp32 [K][C][R][S]
+  void* wk;         // dtype [K][R][S][Cpad]
+  void* wt;         // dtype [C][R][S][K] or NULL
+  long long start;  // first packed element of this conv in the batch
+  int K, C, R, S, Cpad, pad_;
+};
+

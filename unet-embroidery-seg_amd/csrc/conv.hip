@@ -520,6 +520,28 @@ __global__ void pack_weights_kernel(const float* w, int K, int C, int R, int S, 
   }
 }
 
+// Every conv of a model in one launch: desc[i] covers packed elements [start_i, start_{i+1}).
+template <typename T>
+__global__ void pack_weights_batched_kernel(const UnetsegPackDesc* desc, int n, long total) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {  // last desc with start <= i
+      const int mid = (lo + hi + 1) >> 1;
+      if (desc[mid].start <= i) lo = mid; else hi = mid - 1;
+    }
+    const UnetsegPackDesc d = desc[lo];
+    long t = i - d.start;
+    const long li = t;
+    const int c = (int)(t % d.Cpad); t /= d.Cpad;
+    const int s = (int)(t % d.S); t /= d.S;
+    const int r = (int)(t % d.R); t /= d.R;
+    const int k = (int)t;
+    const float v = c < d.C ? d.w[(((long)k * d.C + c) * d.R + r) * d.S + s] : 0.f;
+    reinterpret_cast<T*>(d.wk)[li] = (T)v;
+    if (d.wt && c < d.C) reinterpret_cast<T*>(d.wt)[(((long)c * d.R + r) * d.S + s) * d.K + k] = (T)v;
+  }
+}
+
 // bf16 fast path (conv_fast.hip) when channels are 64-aligned and every buffer fits 31-bit offsets
 bool fast_tn_args(const IgemmArgs& a, FastTNArgs& f) {
   if (getenv("UNETSEG_NO_FAST")) return false;
@@ -675,16 +697,30 @@ static bool wgrad_fast_eligible(int dtype, int q, int cin, int cout) {
   return dtype == DT_BF16 && !getenv("UNETSEG_NO_FAST") && q % 32 == 0 && cin % 8 == 0 && cout % 64 == 0;
 }
 
+// shape test of the halo wgrad path (3x3, stride 1, pad 1, output grid == input grid)
+static bool halo_wgrad_args(int dtype, int c1, int cin, int n, int h, int w, int cout, int r, int s, int p, int q,
+                            HaloWgradArgs& hw) {
+  if (dtype != DT_BF16 || getenv("UNETSEG_NO_FAST") || r != 3 || s != 3 || p != h || q != w) return false;
+  hw.c1 = c1; hw.cin = cin; hw.N = n; hw.H = h; hw.W = w; hw.Cout = cout;
+  return halo3_wgrad_ok(hw);
+}
+
 UNETSEG_API size_t unetseg_conv2d_wgrad_workspace(int dtype, int n, int p, int q, int cout, int cin, int r, int s) {
   const int bkw = dtype == DT_BF16 ? 32 : 16;
   const int Ng = r * s * cin;
   const long kpix = (long)n * p * q;
   const size_t generic = (size_t)wgrad_splits(cout, Ng, kpix, bkw) * cout * Ng * sizeof(float);
+  size_t best = generic;
   if (wgrad_fast_eligible(dtype, q, cin, cout)) {
     const size_t fast = (size_t)wgrad_fast_splits(cout, Ng, kpix) * cout * Ng * sizeof(float);
-    return fast > generic ? fast : generic;
+    if (fast > best) best = fast;
   }
-  return generic;
+  HaloWgradArgs hw{};
+  if (halo_wgrad_args(dtype, cin, cin, n, p, q, cout, r, s, p, q, hw)) {
+    const size_t halo = (size_t)halo3_wgrad_splits(hw) * cout * Ng * sizeof(float);
+    if (halo > best) best = halo;
+  }
+  return best;
 }
 
 // Weight gradient.  x = cat([x1, x2]) NHWC [n,h,w,*]; dy NHWC [n,p,q,cout] (pixel stride ldy);
@@ -706,7 +742,21 @@ UNETSEG_API int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1
   a.Kpix = (long)n * p * q;
   hipStream_t st = (hipStream_t)stream;
   int splits = 0;
-  {
+  HaloWgradArgs hw{};
+  if (stride == 1 && pad == 1 && halo_wgrad_args(dtype, c1, c1 + c2, n, h, w, cout, r, s, p, q, hw)) {
+    const long src_pix = (long)n * h * w;
+    const long b1 = src_pix * ldc1 * 2, b2 = c2 ? src_pix * ldc2 * 2 : 0, bdy = a.Kpix * ldy * 2;
+    if (b1 < (1L << 31) && b2 < (1L << 31) && bdy < (1L << 31)) {
+      hw.x1 = x1; hw.x2 = c2 ? x2 : nullptr; hw.x1_bytes = (unsigned)b1; hw.x2_bytes = (unsigned)b2;
+      hw.ldc1b = ldc1 * 2; hw.ldc2b = ldc2 * 2; hw.dy = dy; hw.dy_bytes = (unsigned)bdy; hw.ldyb = ldy * 2;
+      hw.ws = ws;
+      splits = halo3_wgrad_splits(hw);
+      US_CHECK_ARG(ws_bytes >= (size_t)splits * cout * a.Ng * sizeof(float), "conv2d_wgrad: workspace too small");
+      launch_halo3_wgrad(hw, splits, st);
+      US_LAUNCH_CHECK("halo3_wgrad");
+    }
+  }
+  if (splits == 0) {
     const long src_pix = (long)n * h * w;
     const long b1 = src_pix * ldc1 * 2, b2 = c2 ? src_pix * ldc2 * 2 : 0, bdy = a.Kpix * ldy * 2;
     if (wgrad_fast_eligible(dtype, q, c1 + c2, cout) && c1 % 8 == 0 && b1 < (1L << 31) && b2 < (1L << 31) &&
@@ -748,6 +798,22 @@ UNETSEG_API int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1
     hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(ceil_div(total, 256)), dim3(256), 0, st, ws, splits, cout, a.cin,
                        r * s, dw, dw_c, accumulate);
   US_LAUNCH_CHECK("wgrad_reduce");
+  return 0;
+}
+
+// All of a model's conv weights in one launch.  desc: DEVICE array of n UnetsegPackDesc with
+// ascending `start` (desc[0].start == 0); total = sum of K*R*S*Cpad.
+UNETSEG_API int unetseg_pack_conv_weights(int dtype, const void* desc, int n, long total, void* stream) {
+  US_CHECK_ARG(desc && n > 0 && total > 0, "pack_conv_weights: bad args");
+  int blocks = ceil_div(total, 256);
+  if (blocks > 16384) blocks = 16384;
+  hipStream_t st = (hipStream_t)stream;
+  const UnetsegPackDesc* d = (const UnetsegPackDesc*)desc;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(pack_weights_batched_kernel<bf16>, dim3(blocks), dim3(256), 0, st, d, n, total);
+  else
+    hipLaunchKernelGGL(pack_weights_batched_kernel<float>, dim3(blocks), dim3(256), 0, st, d, n, total);
+  US_LAUNCH_CHECK("pack_weights_batched");
   return 0;
 }
 

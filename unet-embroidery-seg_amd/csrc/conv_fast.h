@@ -42,9 +42,28 @@ struct FastWgradArgs {
   float* ws;
 };
 
+// 3x3 / stride 1 / pad 1 weight gradient on the halo path (conv_halo.hip)
+struct HaloWgradArgs {
+  const void* x1;
+  const void* x2;
+  unsigned x1_bytes, x2_bytes;
+  int ldc1b, ldc2b, c1, cin;
+  int N, H, W;
+  const void* dy;
+  unsigned dy_bytes;
+  int ldyb, Cout;
+  float* ws;
+};
+
 bool tn_fast_ok(const FastTNArgs& a);
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st);
 int tn_fast_tile_m(const FastTNArgs& a);
+bool halo3_ok(const FastTNArgs& a);
+int launch_halo3(const FastTNArgs& a, hipStream_t st);
+int halo_tile_m();
+bool halo3_wgrad_ok(const HaloWgradArgs& a);
+int halo3_wgrad_splits(const HaloWgradArgs& a);
+int launch_halo3_wgrad(const HaloWgradArgs& a, int G_per, hipStream_t st);
 bool wgrad_fast_ok(const FastWgradArgs& a);
 int wgrad_fast_splits(int Cout, int Ng, long Kpix);
 int launch_wgrad_fast(FastWgradArgs a, int splits, hipStream_t st);

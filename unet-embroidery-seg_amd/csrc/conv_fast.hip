@@ -16,41 +16,10 @@
 
 #include "common.h"
 #include "conv_fast.h"
+#include "fast_util.h"
 
 namespace {
 
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-constexpr unsigned kOOB = 0x80000000u;  // beyond any num_records we build (< 2^31)
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t srd(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
-}
-__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-  return *reinterpret_cast<uint4*>(&v);
-}
-__device__ __forceinline__ int swz8(int row, int ch) { return ch ^ ((row >> 1) & 7); }
-
-// LDS-DMA of 16 B per lane (64 lanes -> 1 KiB contiguous at lds_byte): issued in inline asm so
-// hipcc neither tracks it (no conservative vmcnt(0) before every ds_read) nor reuses M0 (saved and
-// restored inside the statement).  Completion is counted by the caller's explicit vmcnt.
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned lds_byte, unsigned voff) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(lds_byte), "v"(voff), "s"(r)
-      : "memory");
-}
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-  return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
-}
-__device__ __forceinline__ int swz_tr16(int row) { return ((row & 3) | ((row >> 1) & 4)) << 1; }
-__device__ __forceinline__ int swz_tr8(int row) { return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1; }
 
 // ------------------------------------------------------------------------------------------
 // TN (fwd / dgrad).  Tile: BM pixels x BN output channels, K step 64 channels of one tap.
@@ -816,6 +785,7 @@ static bool use_v3() {
 }
 
 int tn_fast_tile_m(const FastTNArgs& a) {
+  if (halo3_ok(a)) return halo_tile_m();
   if (a.Ng <= 64) return 256;
   const long tiles_big = (long)ceil_div(a.M, 256) * ceil_div(a.Ng, 128);
   if (use_v3()) return tiles_big >= 128 ? 256 : 128;
@@ -824,6 +794,7 @@ int tn_fast_tile_m(const FastTNArgs& a) {
 
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
   if (a.M <= 0 || a.Ng <= 0) return 0;
+  if (halo3_ok(a)) return launch_halo3(a, st);
   // zero-tap dgrad parity classes (nr*ns == 0) only write zeros: the register-staged kernel's
   // empty K loop does that, the persistent kernel would skip the tile entirely
   if (use_v3() && a.Ng <= 64 * 2048 && a.nr * a.ns > 0) {  // bias staged in LDS

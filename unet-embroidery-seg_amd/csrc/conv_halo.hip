@@ -1,0 +1,458 @@
+// 3x3 stride-1 "same" convolutions with 64 input channels (fwd and stride-1 dgrad), bf16, gfx950.
+//
+// These are the high-resolution, narrow layers of the U-Net decoder (up_conv at 512^2, up_concat1 at
+// 256^2) and of ResNet layer1 at 128^2.  The generic implicit GEMM re-reads every input pixel once
+// per tap (9x) through L2 and restages the weights per 256-pixel tile; here:
+//  * weights stay resident: one block owns one 64-channel output tile for its whole life and keeps
+//    all 9 taps x 64 x 64 bf16 (72 KiB) in LDS;
+//  * the input arrives as a 2D halo tile: (TH+2) x 34 pixels x 64 channels (42.5 KiB) serve a
+//    TH x 32 output tile for all 9 taps (1.33 reads per pixel instead of 9);
+//  * persistent blocks (one per CU) walk spatial tiles; the next tile's halo streams in by
+//    LDS-DMA (buffer_load ... lds) while the current one is computed -- two halo stages;
+//  * within a tile there is no barrier: 9 taps x 2 K-halves of MFMA straight from LDS;
+//  * output stores are explicit buffer stores so the per-wave count of memory operations after the
+//    next tile's DMA is a compile-time constant: the wait for that DMA is `vmcnt(FP*FC)` and never
+//    waits on this tile's stores.
+// Operand roles as in the TN kernels: weights = A (16 output channels per MFMA row block),
+// pixels = B, so each lane's accumulator holds 4 consecutive output channels of one pixel.
+#include <cstdlib>
+
+#include "common.h"
+#include "conv_fast.h"
+#include "fast_util.h"
+
+namespace {
+
+constexpr int HW_TW = 32;  // output tile width (pixels)
+
+__device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, unsigned off, uint2 v) {
+  asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
+}
+
+template <int TH>
+__global__ __launch_bounds__(256) void halo3_kernel(FastTNArgs a, int tiles_w, int tiles_h, int n_sp, int G_per,
+                                                    unsigned y_bytes) {
+  constexpr int NW = 4;                      // waves; wave w owns output rows [w*TH/4, (w+1)*TH/4)
+  constexpr int RPW = TH / NW;               // rows per wave
+  constexpr int FP = RPW * (HW_TW / 16);     // 16-pixel groups per wave
+  constexpr int FC = 4;                      // 16-channel output groups (64 output channels)
+  constexpr int HP = (TH + 2) * (HW_TW + 2); // halo pixels
+  constexpr int HCH = HP * 8;                // 16-B chunks per halo stage
+  constexpr int HI = (HCH + 64 * NW - 1) / (64 * NW);  // halo DMA instructions per wave
+  constexpr int WCH = 9 * 64 * 8;            // 16-B chunks of resident weights
+  constexpr int WI = WCH / (64 * NW);        // weight DMA instructions per wave
+  static_assert(TH % NW == 0 && WCH % (64 * NW) == 0, "tile shape");
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];
+  uint4* wl = lds;                           // [9*64 rows][8 chunks]
+  uint4* hl = lds + WCH;                     // [2][HP][8]
+  float* red = reinterpret_cast<float*>(hl + 2 * HCH);  // [2][NW][64]
+  float* sbias = red + 2 * NW * 64;          // [64]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntn = a.Ng >> 6;
+  // block -> (output-channel tile, first spatial tile); spatial tiles dealt round-robin
+  const int tn = blockIdx.x / G_per, slot = blockIdx.x % G_per;
+  const int n0 = tn * 64;
+  const int my_tiles = slot < n_sp ? (n_sp - slot + G_per - 1) / G_per : 0;
+  const __amdgpu_buffer_rsrc_t rx = srd(a.x1, a.x1_bytes);
+  const __amdgpu_buffer_rsrc_t rw = srd(a.wt, a.w_bytes);
+  const __amdgpu_buffer_rsrc_t ry = srd(a.y, y_bytes);
+  (void)ntn;
+
+  if (a.bias && tid < 64) sbias[tid] = a.bias[n0 + tid];
+
+  // ---- resident weights: LDS row (jt, k) = weights of output channel n0+k at halo tap jt ----
+  {
+    const unsigned base = lds_addr(wl);
+#pragma unroll 2
+    for (int i = 0; i < WI; ++i) {
+      const int inst = i * NW + wid;
+      const int idx = inst * 64 + lane;
+      const int row = idx >> 3, pc = idx & 7;
+      const int jt = row >> 6, k = row & 63;
+      const int jr = jt / 3, js = jt - jr * 3;
+      const int wtap = (a.r0 + a.rs * jr) * a.S + (a.s0 + a.ss * js);
+      const unsigned off = (unsigned)(n0 + k) * (unsigned)a.ldwb + (unsigned)(wtap * 128 + swz8(row, pc) * 16);
+      dma16(rw, base + (unsigned)inst * 1024u, off);
+    }
+  }
+
+  // ---- halo geometry of this lane's DMA slots (identical for every tile) ----
+  int hrc[HI];  // (hr << 8) | hc, or -1 for lanes past the halo
+#pragma unroll
+  for (int i = 0; i < HI; ++i) {
+    const int idx = (i * NW + wid) * 64 + lane;
+    const int hp = idx >> 3;
+    hrc[i] = idx < HCH ? (((hp / (HW_TW + 2)) << 8) | (hp % (HW_TW + 2))) : -1;
+  }
+  auto issue_halo = [&](int t, int stage) {
+    const int sp = slot + t * G_per;
+    const int tw = sp % tiles_w, rest = sp / tiles_w;
+    const int th = rest % tiles_h, nb = rest / tiles_h;
+    const int gh0 = th * TH - 1, gw0 = tw * HW_TW - 1;
+    const unsigned base = lds_addr(hl + stage * HCH);
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const int v = hrc[i];
+      const int hr = v >> 8, hc = v & 255;
+      const int gh = gh0 + hr, gw = gw0 + hc;
+      const int hp = hr * (HW_TW + 2) + hc;
+      const int pc = lane & 7;
+      const bool ok = v >= 0 && gh >= 0 && gh < a.H && gw >= 0 && gw < a.W;
+      const unsigned off = ok ? (unsigned)((nb * a.H + gh) * a.W + gw) * (unsigned)a.ldc1b + swz8(hp, pc) * 16u : kOOB;
+      if (v >= 0 || HCH % (64 * NW) == 0) dma16(rx, base + (unsigned)((i * NW + wid) * 1024), off);
+    }
+  };
+
+  f32x4 acc[FC][FP];
+  if (my_tiles > 0) issue_halo(0, 0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  // halo tap offsets (uniform): jt -> (dh, dw)
+  const int dh0 = a.dh0, dhs = a.dhs, dw0 = a.dw0, dws = a.dws;
+  const int j16 = lane & 15, kg = lane >> 4;
+
+  for (int t = 0; t < my_tiles; ++t) {
+    const int stage = t & 1;
+    if (t + 1 < my_tiles) issue_halo(t + 1, stage ^ 1);
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int p = 0; p < FP; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint4* hs = hl + stage * HCH;
+#pragma unroll
+    for (int jt = 0; jt < 9; ++jt) {
+      const int jr = jt / 3, js = jt - jr * 3;
+      const int dh = dh0 + dhs * jr, dw = dw0 + dws * js;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ch = kk * 4 + kg;
+        bf16x8 wf[FC], pf[FP];
+#pragma unroll
+        for (int c = 0; c < FC; ++c) {
+          const int row = jt * 64 + c * 16 + j16;
+          uint4 v = wl[row * 8 + swz8(row, ch)];
+          wf[c] = *reinterpret_cast<bf16x8*>(&v);
+        }
+#pragma unroll
+        for (int p = 0; p < FP; ++p) {
+          const int r = wid * RPW + p / (HW_TW / 16);
+          const int col = (p % (HW_TW / 16)) * 16 + j16;
+          const int hp = (r + 1 + dh) * (HW_TW + 2) + col + 1 + dw;
+          uint4 v = hs[hp * 8 + swz8(hp, ch)];
+          pf[p] = *reinterpret_cast<bf16x8*>(&v);
+        }
+#pragma unroll
+        for (int c = 0; c < FC; ++c)
+#pragma unroll
+          for (int p = 0; p < FP; ++p)
+            acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], pf[p], acc[c][p], 0, 0, 0);
+      }
+    }
+
+    // ================= epilogue =================
+    const int sp = slot + t * G_per;
+    const int tw = sp % tiles_w, rest = sp / tiles_w;
+    const int th = rest % tiles_h, nb = rest / tiles_h;
+    float csum[FC][4];
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) csum[c][e] = 0.f;
+    uint2 outv[FC][FP];
+    unsigned outo[FP];
+#pragma unroll
+    for (int p = 0; p < FP; ++p) {
+      const int r = wid * RPW + p / (HW_TW / 16);
+      const int col = (p % (HW_TW / 16)) * 16 + j16;
+      const long opix = ((long)nb * a.OH + th * TH + r) * a.OW + tw * HW_TW + col;
+      outo[p] = (unsigned)(opix * a.ldy + n0) * 2u;
+#pragma unroll
+      for (int c = 0; c < FC; ++c) {
+        const int cb = c * 16 + kg * 4;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[c][p][e] + (a.bias ? sbias[cb + e] : 0.f);
+          if (a.relu) v[e] = fmaxf(v[e], 0.f);
+        }
+        if (a.accumulate) {
+          const bf16* ob = reinterpret_cast<const bf16*>((const char*)a.y + outo[p] + cb * 2);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)ob[e];
+        }
+        bf16 o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = (bf16)v[e];
+          v[e] = (float)o[e];
+          csum[c][e] += v[e];
+          acc[c][p][e] = v[e];
+        }
+        outv[c][p] = *reinterpret_cast<uint2*>(o);
+      }
+    }
+    if (a.stats) {
+      // per-tile BN partials over the TH*32 pixels: column sums, then M2 about the tile mean
+#pragma unroll
+      for (int c = 0; c < FC; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float s = csum[c][e];
+          s += __shfl_xor(s, 1, 64);
+          s += __shfl_xor(s, 2, 64);
+          s += __shfl_xor(s, 4, 64);
+          s += __shfl_xor(s, 8, 64);
+          if (j16 == 0) red[wid * 64 + c * 16 + kg * 4 + e] = s;
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+      for (int c = 0; c < FC; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int col = c * 16 + kg * 4 + e;
+          const float mean = (red[col] + red[64 + col] + red[128 + col] + red[192 + col]) * (1.0f / (TH * HW_TW));
+          float q = 0.f;
+#pragma unroll
+          for (int p = 0; p < FP; ++p) {
+            const float d = acc[c][p][e] - mean;
+            q += d * d;
+          }
+          q += __shfl_xor(q, 1, 64);
+          q += __shfl_xor(q, 2, 64);
+          q += __shfl_xor(q, 4, 64);
+          q += __shfl_xor(q, 8, 64);
+          if (j16 == 0) red[NW * 64 + wid * 64 + col] = q;
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (tid < 64) {
+        const float s = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
+        const float q = red[256 + tid] + red[320 + tid] + red[384 + tid] + red[448 + tid];
+        a.stats[(long)(n0 + tid) * a.stats_ld + sp] = s;
+        a.stats[((long)a.Ng + n0 + tid) * a.stats_ld + sp] = q;
+      }
+    }
+    // output stores last: exactly FP*FC buffer stores per wave after the next tile's DMA
+#pragma unroll
+    for (int p = 0; p < FP; ++p)
+#pragma unroll
+      for (int c = 0; c < FC; ++c) bstore64(ry, outo[p] + (c * 16 + kg * 4) * 2, outv[c][p]);
+    // next halo landed (all but this tile's FP*FC stores retired) and every wave is done with
+    // both the current stage (WAR for the DMA after next) and `red`
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(FP * FC) : "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+
+// ------------------------------------------------------------------------------------------
+// wgrad of the same convolutions: dW[k][tap][c] = sum_pix dY[pix][k] * X[pix + off(tap)][c].
+// Block group = (64 output channels, 64 input channels); persistent over TH x 32 spatial tiles,
+// each tile = dY tile (256 px x 64 ch) + X halo (340 px x 64 ch) by LDS-DMA, double buffered.
+// Wave w owns 9 of the 36 (tap, 16-channel) column blocks: 4 x 9 accumulators of 16x16.
+// Fragments come from pixel-major LDS with ds_read_b64_tr_b16 (K = 32 pixels of one output row);
+// the halo rows of a tap are the output row's pixels shifted by (dh, dw), so the same transposed
+// read serves all 9 taps.  Partials go to slab[slot] in the natural [cout][tap*cin + c] layout of
+// the split-K reduce.
+// ------------------------------------------------------------------------------------------
+template <int TH>
+__global__ __launch_bounds__(256) void halo3_wgrad_kernel(HaloWgradArgs a, int tiles_w, int tiles_h, int n_sp,
+                                                          int G_per) {
+  constexpr int NW = 4;
+  constexpr int TP = TH * HW_TW;              // output pixels per tile
+  constexpr int HP = (TH + 2) * (HW_TW + 2);  // halo pixels
+  constexpr int DCH = TP * 8, HCH = HP * 8;   // 16-B chunks per stage part
+  constexpr int DI = DCH / (64 * NW);         // dY DMA instructions per wave
+  constexpr int HI = (HCH + 64 * NW - 1) / (64 * NW);
+  constexpr int STG = DCH + HCH;              // uint4 per stage
+  constexpr int FM = 4, FN = 9;
+  static_assert(DCH % (64 * NW) == 0, "tile shape");
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mtiles = a.Cout >> 6;
+  const int grp = blockIdx.x / G_per, slot = blockIdx.x % G_per;
+  const int mt = grp % mtiles, ct = grp / mtiles;
+  const int my_tiles = slot < n_sp ? (n_sp - slot + G_per - 1) / G_per : 0;
+  const bool first = ct * 64 < a.c1;
+  const __amdgpu_buffer_rsrc_t rx = first ? srd(a.x1, a.x1_bytes) : srd(a.x2, a.x2_bytes);
+  const unsigned ldxb = first ? (unsigned)a.ldc1b : (unsigned)a.ldc2b;
+  const unsigned xcb = (unsigned)(first ? ct * 64 : ct * 64 - a.c1) * 2u;
+  const __amdgpu_buffer_rsrc_t rdy = srd(a.dy, a.dy_bytes);
+  const unsigned dycb = (unsigned)mt * 128u;
+
+  int hrc[HI];
+#pragma unroll
+  for (int i = 0; i < HI; ++i) {
+    const int idx = (i * NW + wid) * 64 + lane;
+    const int hp = idx >> 3;
+    hrc[i] = idx < HCH ? (((hp / (HW_TW + 2)) << 8) | (hp % (HW_TW + 2))) : -1;
+  }
+  auto issue = [&](int t, int stage) {
+    const int sp = slot + t * G_per;
+    const int tw = sp % tiles_w, rest = sp / tiles_w;
+    const int th = rest % tiles_h, nb = rest / tiles_h;
+    const int h0 = th * TH, w0 = tw * HW_TW;
+    const unsigned base = lds_addr(lds + stage * STG);
+    const int pc = lane & 7;
+#pragma unroll
+    for (int i = 0; i < DI; ++i) {
+      const int inst = i * NW + wid;
+      const int px = (inst * 64 + lane) >> 3;
+      const unsigned pix = (unsigned)((nb * a.H + h0 + px / HW_TW) * a.W + w0 + px % HW_TW);
+      dma16(rdy, base + (unsigned)inst * 1024u, pix * (unsigned)a.ldyb + dycb + (unsigned)((pc ^ swz_tr8(px)) * 16));
+    }
+    const unsigned hbase = base + DCH * 16;
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const int v = hrc[i];
+      const int hr = v >> 8, hc = v & 255;
+      const int gh = h0 - 1 + hr, gw = w0 - 1 + hc;
+      const int hp = hr * (HW_TW + 2) + hc;
+      const bool ok = v >= 0 && gh >= 0 && gh < a.H && gw >= 0 && gw < a.W;
+      const unsigned off =
+          ok ? (unsigned)((nb * a.H + gh) * a.W + gw) * ldxb + xcb + (unsigned)((pc ^ swz_tr8(hp)) * 16) : kOOB;
+      if (v >= 0 || HCH % (64 * NW) == 0) dma16(rx, hbase + (unsigned)((i * NW + wid) * 1024), off);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (my_tiles > 0) issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  auto tr = [&](const char* rowbase_a, int row_a, int chunk) -> bf16x8 {
+    // rows row_a (+0..3 via qq) and row_a + 4 of a 128-B-row image starting at rowbase_a
+    const int ra = row_a + qq, rb = row_a + qq + 4;
+    const char* pa = rowbase_a + ra * 128 + ((chunk ^ swz_tr8(ra)) * 16) + (pp & 1) * 8;
+    const char* pb = rowbase_a + rb * 128 + ((chunk ^ swz_tr8(rb)) * 16) + (pp & 1) * 8;
+    s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(pa));
+    s16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(pb));
+    s16x8 v = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
+    return *reinterpret_cast<bf16x8*>(&v);
+  };
+
+  for (int t = 0; t < my_tiles; ++t) {
+    const int stage = t & 1;
+    if (t + 1 < my_tiles) issue(t + 1, stage ^ 1);
+    const char* dbase = reinterpret_cast<const char*>(lds + stage * STG);
+    const char* hbase = dbase + DCH * 16;
+#pragma unroll 2
+    for (int rr = 0; rr < TH; ++rr) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = tr(dbase, rr * HW_TW + 8 * g, i * 2 + (pp >> 1));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int f = wid * FN + j;
+        const int jt = f >> 2, cg = f & 3;
+        const int dh = jt / 3 - 1, dw = jt % 3 - 1;
+        bfr[j] = tr(hbase, (rr + 1 + dh) * (HW_TW + 2) + 1 + dw + 8 * g, cg * 2 + (pp >> 1));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  // slab[slot][cout][tap*cin + c]
+  const long Ng = 9L * a.cin;
+  float* ws = a.ws + (long)slot * a.Cout * Ng;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = mt * 64 + i * 16 + g * 4 + e;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int f = wid * FN + j;
+        const int jt = f >> 2, cg = f & 3;
+        ws[(long)m * Ng + (long)jt * a.cin + ct * 64 + cg * 16 + i16] = acc[i][j][e];
+      }
+    }
+}
+
+template <int TH>
+size_t halo_lds_bytes() {
+  return (size_t)9 * 64 * 128 + 2 * (size_t)(TH + 2) * (HW_TW + 2) * 128 + 2 * 4 * 64 * 4 + 64 * 4;
+}
+
+}  // namespace
+
+int halo_tile_m() { return 8 * HW_TW; }
+
+bool halo3_ok(const FastTNArgs& a) {
+  static const bool off = getenv("UNETSEG_NO_HALO") != nullptr;
+  if (off) return false;
+  if (a.x2 || a.c1 != 64 || a.cin != 64 || a.nr != 3 || a.ns != 3 || a.istride != 1) return false;
+  if (a.dhs * a.dhs != 1 || a.dws * a.dws != 1) return false;
+  const int dh_lo = a.dhs > 0 ? a.dh0 : a.dh0 - 2, dw_lo = a.dws > 0 ? a.dw0 : a.dw0 - 2;
+  if (dh_lo != -1 || dw_lo != -1) return false;  // halo of one pixel on every side
+  if (a.ostride != 1 || a.ph || a.pw || a.OH != a.hc || a.OW != a.wc || a.H != a.hc || a.W != a.wc) return false;
+  if (a.Ng % 64 || a.hc % 8 || a.wc % HW_TW) return false;
+  if ((long)a.M * a.ldy * 2 >= (1L << 31)) return false;
+  return true;
+}
+
+int launch_halo3(const FastTNArgs& a, hipStream_t st) {
+  constexpr int TH = 8;
+  const int tiles_w = a.wc / HW_TW, tiles_h = a.hc / TH;
+  const int n_img = a.M / (a.hc * a.wc);
+  const int n_sp = n_img * tiles_h * tiles_w;
+  const int ntn = a.Ng / 64;
+  int G_per = 256 / ntn;
+  if (G_per < 1) G_per = 1;
+  if (G_per > n_sp) G_per = n_sp;
+  const size_t lds = halo_lds_bytes<TH>();
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_kernel<TH>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const unsigned y_bytes = (unsigned)((long)a.M * a.ldy * 2);
+  hipLaunchKernelGGL((halo3_kernel<TH>), dim3(ntn * G_per), dim3(256), lds, st, a, tiles_w, tiles_h, n_sp, G_per,
+                     y_bytes);
+  return 0;
+}
+
+bool halo3_wgrad_ok(const HaloWgradArgs& a) {
+  static const bool off = getenv("UNETSEG_NO_HALO") != nullptr;
+  if (off) return false;
+  return a.cin % 64 == 0 && a.c1 % 64 == 0 && a.Cout % 64 == 0 && a.H % 8 == 0 && a.W % HW_TW == 0;
+}
+
+int halo3_wgrad_splits(const HaloWgradArgs& a) {
+  const int groups = (a.Cout / 64) * (a.cin / 64);
+  const int n_sp = a.N * (a.H / 8) * (a.W / HW_TW);
+  int g = 256 / groups;
+  if (g < 1) g = 1;
+  if (g > n_sp) g = n_sp;
+  return g;
+}
+
+int launch_halo3_wgrad(const HaloWgradArgs& a, int G_per, hipStream_t st) {
+  constexpr int TH = 8;
+  const int tiles_w = a.W / HW_TW, tiles_h = a.H / TH;
+  const int n_sp = a.N * tiles_h * tiles_w;
+  const int groups = (a.Cout / 64) * (a.cin / 64);
+  const size_t lds = 2 * ((size_t)TH * HW_TW + (size_t)(TH + 2) * (HW_TW + 2)) * 128;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_wgrad_kernel<TH>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((halo3_wgrad_kernel<TH>), dim3(groups * G_per), dim3(256), lds, st, a, tiles_w, tiles_h, n_sp,
+                     G_per);
+  return 0;
+}

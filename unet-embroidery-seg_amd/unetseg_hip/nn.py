@@ -240,8 +240,11 @@ class HipModel(nn.Module):
         return DT_BF16 if _is_autocast() else DT_F32
 
     def _pack_weights(self, ctx, need_t):
-        for pc in self._packed:
-            pc.pack(ctx, need_t and pc.conv.in_channels >= 8)
+        if not self._packed:
+            return
+        if getattr(self, "_pack_table", None) is None:
+            self._pack_table = ops.PackTable()
+        self._pack_table.run(ctx, self._packed, [need_t and pc.conv.in_channels >= 8 for pc in self._packed])
 
     def forward(self, x):
         if not x.is_cuda:

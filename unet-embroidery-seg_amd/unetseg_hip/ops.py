@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import torch
 
 from .lib import DT_BF16, DT_F32, lib
@@ -49,8 +50,8 @@ PROBE = None
 
 
 class _probe:
-    def __init__(self, kind, flops, launches=1):
-        self.kind, self.flops, self.launches = kind, flops, launches
+    def __init__(self, kind, flops, launches=1, desc=None):
+        self.kind, self.flops, self.launches, self.desc = kind, flops, launches, desc
 
     def __enter__(self):
         if PROBE is not None:
@@ -62,7 +63,7 @@ class _probe:
     def __exit__(self, *a):
         if PROBE is not None:
             self.e1.record()
-            PROBE.append((self.kind, self.flops, self.launches, self.e0, self.e1))
+            PROBE.append((self.kind, self.flops, self.launches, self.e0, self.e1, self.desc))
 
 
 def workspace(nbytes, device):
@@ -140,7 +141,8 @@ class PackedConv:
         self.wk = self.wt = None
         self.dt = None
 
-    def pack(self, ctx, need_t):
+    def ensure(self, ctx, need_t):
+        """allocate the packed images for ctx's dtype/device (no launch)"""
         K, C, R, S = self.K, self.C, self.R, self.S
         if self.wk is None or self.dt != ctx.dt or self.wk.device != ctx.device:
             self.wk = ctx.empty(K, R, S, self.cpad)
@@ -148,8 +150,44 @@ class PackedConv:
             self.dt = ctx.dt
         if need_t and self.wt is None:
             self.wt = ctx.empty(C, R, S, K)
+
+    def pack(self, ctx, need_t):
+        K, C, R, S = self.K, self.C, self.R, self.S
+        self.ensure(ctx, need_t)
         lib.pack_conv_weight(ctx.dt, P(self.conv.weight), K, C, R, S, self.cpad, P(self.wk),
                              P(self.wt) if need_t else 0, ctx.stream)
+
+
+_PACK_DESC = np.dtype([("w", "<u8"), ("wk", "<u8"), ("wt", "<u8"), ("start", "<i8"), ("K", "<i4"), ("C", "<i4"),
+                       ("R", "<i4"), ("S", "<i4"), ("Cpad", "<i4"), ("pad_", "<i4")])  # UnetsegPackDesc
+
+
+class PackTable:
+    """Device descriptor table for packing every conv weight of a model in ONE launch
+    (unetseg_pack_conv_weights); rebuilt only when a buffer address changes."""
+
+    def __init__(self):
+        self.key = None
+        self.desc = None
+        self.total = 0
+
+    def run(self, ctx, pcs, need_t):
+        for pc, nt in zip(pcs, need_t):
+            pc.ensure(ctx, nt)
+        key = (ctx.dt, str(ctx.device)) + tuple(
+            (pc.conv.weight.data_ptr(), pc.wk.data_ptr(), pc.wt.data_ptr() if (nt and pc.wt is not None) else 0)
+            for pc, nt in zip(pcs, need_t))
+        if key != self.key:
+            d = np.zeros(len(pcs), dtype=_PACK_DESC)
+            start = 0
+            for i, (pc, nt) in enumerate(zip(pcs, need_t)):
+                d[i] = (pc.conv.weight.data_ptr(), pc.wk.data_ptr(), pc.wt.data_ptr() if nt else 0, start,
+                        pc.K, pc.C, pc.R, pc.S, pc.cpad, 0)
+                start += pc.K * pc.R * pc.S * pc.cpad
+            self.desc = torch.from_numpy(d.view(np.uint8).copy()).to(ctx.device)
+            self.total = start
+            self.key = key
+        lib.pack_conv_weights(ctx.dt, P(self.desc), len(pcs), self.total, ctx.stream)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -185,7 +223,8 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
         st = (ctx.f32(2, K, math.ceil(M / tile)), tile)
     b = pc.conv.bias
     flops = 2.0 * M * K * pc.C * R * S  # algorithmic (unpadded Cin)
-    with _probe("igemm_tn", flops):
+    desc = (N, H, W, C1, C2, K, R, S, stride)
+    with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
         lib.conv2d_fwd(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride, pad,
                        P(b), int(relu), P(y), K, P(st[0] if st else None), ctx.stream)
     out = Node(y)
@@ -209,7 +248,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
         cin = C1 + C2
         ws_bytes = lib.conv2d_wgrad_workspace(ctx.dt, N, Pq, Qq, K, cin, R, S)
         ws = workspace(ws_bytes, dev)
-        with _probe("wgrad", flops):
+        with _probe("wgrad", flops, 1, ("wgrad",) + desc):
             lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(dY), ldp(dY), K, R, S,
                              stride, pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, ctx.stream)
         ctx.param_done(pc.conv.weight, b)
@@ -217,12 +256,12 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
         if x2 is None:
             if x1.need_grad:
                 g, acc = gbuf(ctx, x1)
-                with _probe("igemm_tn", flops, stride * stride):
+                with _probe("igemm_tn", flops, stride * stride, ("dgrad",) + desc):
                     lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, R, S, stride, pad, P(g),
                                      ldp(g), H, W, acc, ctx.stream)
         elif x1.need_grad or x2.need_grad:
             g = ctx.empty(N, H, W, cin)
-            with _probe("igemm_tn", flops, stride * stride):
+            with _probe("igemm_tn", flops, stride * stride, ("dgrad",) + desc):
                 lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, cin, R, S, stride, pad, P(g), cin,
                                  H, W, 0, ctx.stream)
             give_grad(ctx, x1, g[..., :C1])
