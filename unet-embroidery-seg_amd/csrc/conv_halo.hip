@@ -29,10 +29,10 @@ __device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, unsigned off,
   asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
 }
 
-template <int TH>
-__global__ __launch_bounds__(256) void halo3_kernel(FastTNArgs a, int tiles_w, int tiles_h, int n_sp, int G_per,
-                                                    unsigned y_bytes) {
-  constexpr int NW = 4;                      // waves; wave w owns output rows [w*TH/4, (w+1)*TH/4)
+template <int TH, int NW>
+__global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_w, int tiles_h, int n_sp, int G_per,
+                                                        unsigned y_bytes) {
+  // wave w owns output rows [w*TH/NW, (w+1)*TH/NW)
   constexpr int RPW = TH / NW;               // rows per wave
   constexpr int FP = RPW * (HW_TW / 16);     // 16-pixel groups per wave
   constexpr int FC = 4;                      // 16-channel output groups (64 output channels)
@@ -45,8 +45,8 @@ __global__ __launch_bounds__(256) void halo3_kernel(FastTNArgs a, int tiles_w, i
   extern __shared__ __attribute__((aligned(16))) uint4 lds[];
   uint4* wl = lds;                           // [9*64 rows][8 chunks]
   uint4* hl = lds + WCH;                     // [2][HP][8]
-  float* red = reinterpret_cast<float*>(hl + 2 * HCH);  // [2][NW][64]
-  float* sbias = red + 2 * NW * 64;          // [64]
+  float* red = reinterpret_cast<float*>(hl + 2 * HCH);  // [NW][64]
+  float* sbias = red + NW * 64;              // [64]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -207,12 +207,16 @@ __global__ __launch_bounds__(256) void halo3_kernel(FastTNArgs a, int tiles_w, i
           if (j16 == 0) red[wid * 64 + c * 16 + kg * 4 + e] = s;
         }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      float qv[FC][4];
 #pragma unroll
       for (int c = 0; c < FC; ++c)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int col = c * 16 + kg * 4 + e;
-          const float mean = (red[col] + red[64 + col] + red[128 + col] + red[192 + col]) * (1.0f / (TH * HW_TW));
+          float tot = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) tot += red[w * 64 + col];
+          const float mean = tot * (1.0f / (TH * HW_TW));
           float q = 0.f;
 #pragma unroll
           for (int p = 0; p < FP; ++p) {
@@ -223,13 +227,24 @@ __global__ __launch_bounds__(256) void halo3_kernel(FastTNArgs a, int tiles_w, i
           q += __shfl_xor(q, 2, 64);
           q += __shfl_xor(q, 4, 64);
           q += __shfl_xor(q, 8, 64);
-          if (j16 == 0) red[NW * 64 + wid * 64 + col] = q;
+          qv[c][e] = q;
         }
+      float stot = 0.f;
+      if (tid < 64)
+#pragma unroll
+        for (int w = 0; w < NW; ++w) stot += red[w * 64 + tid];
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // sums consumed: reuse red for M2
+#pragma unroll
+      for (int c = 0; c < FC; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (j16 == 0) red[wid * 64 + c * 16 + kg * 4 + e] = qv[c][e];
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (tid < 64) {
-        const float s = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
-        const float q = red[256 + tid] + red[320 + tid] + red[384 + tid] + red[448 + tid];
-        a.stats[(long)(n0 + tid) * a.stats_ld + sp] = s;
+        float q = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) q += red[w * 64 + tid];
+        a.stats[(long)(n0 + tid) * a.stats_ld + sp] = stot;
         a.stats[((long)a.Ng + n0 + tid) * a.stats_ld + sp] = q;
       }
     }
@@ -381,9 +396,9 @@ __global__ __launch_bounds__(256) void halo3_wgrad_kernel(HaloWgradArgs a, int t
     }
 }
 
-template <int TH>
+template <int TH, int NW>
 size_t halo_lds_bytes() {
-  return (size_t)9 * 64 * 128 + 2 * (size_t)(TH + 2) * (HW_TW + 2) * 128 + 2 * 4 * 64 * 4 + 64 * 4;
+  return (size_t)9 * 64 * 128 + 2 * (size_t)(TH + 2) * (HW_TW + 2) * 128 + NW * 64 * 4 + 64 * 4;
 }
 
 }  // namespace
@@ -403,8 +418,8 @@ bool halo3_ok(const FastTNArgs& a) {
   return true;
 }
 
-int launch_halo3(const FastTNArgs& a, hipStream_t st) {
-  constexpr int TH = 8;
+template <int TH, int NW>
+static int launch_halo3_cfg(const FastTNArgs& a, hipStream_t st) {
   const int tiles_w = a.wc / HW_TW, tiles_h = a.hc / TH;
   const int n_img = a.M / (a.hc * a.wc);
   const int n_sp = n_img * tiles_h * tiles_w;
@@ -412,17 +427,22 @@ int launch_halo3(const FastTNArgs& a, hipStream_t st) {
   int G_per = 256 / ntn;
   if (G_per < 1) G_per = 1;
   if (G_per > n_sp) G_per = n_sp;
-  const size_t lds = halo_lds_bytes<TH>();
+  const size_t lds = halo_lds_bytes<TH, NW>();
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_kernel<TH>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_kernel<TH, NW>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const unsigned y_bytes = (unsigned)((long)a.M * a.ldy * 2);
-  hipLaunchKernelGGL((halo3_kernel<TH>), dim3(ntn * G_per), dim3(256), lds, st, a, tiles_w, tiles_h, n_sp, G_per,
-                     y_bytes);
+  hipLaunchKernelGGL((halo3_kernel<TH, NW>), dim3(ntn * G_per), dim3(64 * NW), lds, st, a, tiles_w, tiles_h, n_sp,
+                     G_per, y_bytes);
   return 0;
+}
+
+int launch_halo3(const FastTNArgs& a, hipStream_t st) {
+  static const int nw = getenv("UNETSEG_HALO_W4") ? 4 : 8;
+  return nw == 4 ? launch_halo3_cfg<8, 4>(a, st) : launch_halo3_cfg<8, 8>(a, st);
 }
 
 bool halo3_wgrad_ok(const HaloWgradArgs& a) {
