@@ -49,10 +49,10 @@ typedef struct UnetsegPackDesc {
   const float* w;  /* fp32 [K][C][R][S] */
   void* wk;        /* dtype [K][R][S][Cpad] */
   void* wt;        /* dtype [C][R][S][K] or NULL */
-  long long start; /* first packed element of this conv in the batch (ascending, desc[0].start == 0) */
+  long long start; /* first tile of this conv (ascending, desc[0].start == 0; ceil(K/32)*ceil(Cpad/64) tiles) */
   int K, C, R, S, Cpad, pad_;
 } UnetsegPackDesc;
-/* every conv weight of a model in one launch (total = sum of K*R*S*Cpad) */
+/* every conv weight of a model in one launch (total = number of tiles) */
 int unetseg_pack_conv_weights(int dtype, const void* desc, int n, long total, void* stream);
 /* legacy generic row tile (kept for ABI v1 callers) */
 int unetseg_conv_tile_m(void);

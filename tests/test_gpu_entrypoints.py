@@ -71,7 +71,9 @@ def test_miou_parity_unet_resnet50_512():
             ro = ref_cpu.forward("unet_resnet50", params, buffers, x, train=False)
         rconf = [a + b for a, b in zip(rconf, ref_cpu.binary_confusion(ro, y))]
         nflip += int(((ro[:, 1] - ro[:, 0]).abs() < 1e-4).sum())
-        assert (o.cpu() - ro).abs().max() < 1e-3
+        # 1e-3 per pixel, relative once |logit| > 1 (these hash-weight logits reach ~13 at 512^2)
+        err = ((o.cpu() - ro).abs() / ro.abs().clamp(min=1.0)).max()
+        assert err < 1e-3, err
     hip = binary_segmentation_metrics(*[float(v) for v in conf.tolist()])
     ref = binary_segmentation_metrics(*[float(v) for v in rconf])
     assert abs(hip["IoU"] - ref["IoU"]) < 1e-4, (hip, ref, nflip)

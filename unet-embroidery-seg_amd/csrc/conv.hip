@@ -520,25 +520,47 @@ __global__ void pack_weights_kernel(const float* w, int K, int C, int R, int S, 
   }
 }
 
-// Every conv of a model in one launch: desc[i] covers packed elements [start_i, start_{i+1}).
+// Every conv of a model in one launch.  A block packs a tile of 32 output x 64 input channels of
+// one conv for all taps: fp32 reads are shared across the tap loop through L1/L2, the wk image
+// ([K][R][S][Cpad], channel-contiguous) is written straight from the loads and the transposed wt
+// image ([C][R][S][K], K-contiguous) through an LDS transpose, so every store is coalesced.
+// desc[i].start = first tile of conv i (tiles of a conv: ceil(K/32) * ceil(Cpad/64)).
 template <typename T>
-__global__ void pack_weights_batched_kernel(const UnetsegPackDesc* desc, int n, long total) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {  // last desc with start <= i
-      const int mid = (lo + hi + 1) >> 1;
-      if (desc[mid].start <= i) lo = mid; else hi = mid - 1;
+__global__ __launch_bounds__(256) void pack_weights_batched_kernel(const UnetsegPackDesc* desc, int n) {
+  __shared__ float tile[32][65];
+  const long b = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {  // last desc with start <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (desc[mid].start <= b) lo = mid; else hi = mid - 1;
+  }
+  const UnetsegPackDesc d = desc[lo];
+  const int lt = (int)(b - d.start);
+  const int ctiles = (d.Cpad + 63) / 64;
+  const int kt = lt / ctiles, ct = lt - kt * ctiles;
+  const int taps = d.R * d.S;
+  const int t = threadIdx.x;
+  const int cl = t & 63, kl0 = t >> 6;
+  const int c = ct * 64 + cl;
+  for (int tap = 0; tap < taps; ++tap) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int kl = kl0 + 4 * i, k = kt * 32 + kl;
+      float v = 0.f;
+      if (k < d.K && c < d.C) v = d.w[((long)k * d.C + c) * taps + tap];
+      tile[kl][cl] = v;
+      if (k < d.K && c < d.Cpad) reinterpret_cast<T*>(d.wk)[((long)k * taps + tap) * d.Cpad + c] = (T)v;
     }
-    const UnetsegPackDesc d = desc[lo];
-    long t = i - d.start;
-    const long li = t;
-    const int c = (int)(t % d.Cpad); t /= d.Cpad;
-    const int s = (int)(t % d.S); t /= d.S;
-    const int r = (int)(t % d.R); t /= d.R;
-    const int k = (int)t;
-    const float v = c < d.C ? d.w[(((long)k * d.C + c) * d.R + r) * d.S + s] : 0.f;
-    reinterpret_cast<T*>(d.wk)[li] = (T)v;
-    if (d.wt && c < d.C) reinterpret_cast<T*>(d.wt)[(((long)c * d.R + r) * d.S + s) * d.K + k] = (T)v;
+    if (d.wt) {
+      __syncthreads();
+      const int kl = t & 31, k = kt * 32 + kl;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int cl2 = (t >> 5) + 8 * i, c2 = ct * 64 + cl2;
+        if (k < d.K && c2 < d.C) reinterpret_cast<T*>(d.wt)[((long)c2 * taps + tap) * d.K + k] = (T)tile[kl][cl2];
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -802,17 +824,16 @@ UNETSEG_API int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1
 }
 
 // All of a model's conv weights in one launch.  desc: DEVICE array of n UnetsegPackDesc with
-// ascending `start` (desc[0].start == 0); total = sum of K*R*S*Cpad.
+// ascending `start` = first tile (desc[0].start == 0; a conv has ceil(K/32)*ceil(Cpad/64) tiles);
+// total = number of tiles.
 UNETSEG_API int unetseg_pack_conv_weights(int dtype, const void* desc, int n, long total, void* stream) {
-  US_CHECK_ARG(desc && n > 0 && total > 0, "pack_conv_weights: bad args");
-  int blocks = ceil_div(total, 256);
-  if (blocks > 16384) blocks = 16384;
+  US_CHECK_ARG(desc && n > 0 && total > 0 && total < (1L << 31), "pack_conv_weights: bad args");
   hipStream_t st = (hipStream_t)stream;
   const UnetsegPackDesc* d = (const UnetsegPackDesc*)desc;
   if (dtype == DT_BF16)
-    hipLaunchKernelGGL(pack_weights_batched_kernel<bf16>, dim3(blocks), dim3(256), 0, st, d, n, total);
+    hipLaunchKernelGGL(pack_weights_batched_kernel<bf16>, dim3(total), dim3(256), 0, st, d, n);
   else
-    hipLaunchKernelGGL(pack_weights_batched_kernel<float>, dim3(blocks), dim3(256), 0, st, d, n, total);
+    hipLaunchKernelGGL(pack_weights_batched_kernel<float>, dim3(total), dim3(256), 0, st, d, n);
   US_LAUNCH_CHECK("pack_weights_batched");
   return 0;
 }

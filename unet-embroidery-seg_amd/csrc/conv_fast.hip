@@ -168,7 +168,16 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
   }
 
   // ---- epilogue: lane holds D[cout = (lane>>4)*4 + e][pixel = lane&15] per (c, p) subtile ----
-  bf16* y = (bf16*)a.y;
+  // bias + ReLU + bf16 rounding in registers; per-wave BN partials over the wave's WTM rows (no
+  // barrier: the stats row tile is WTM = 64); then each wave transposes its WTM x WTN tile through
+  // LDS (the operand stages are free after the K loop's last barrier) and writes whole 16-B chunks
+  // of each pixel's channel run: coalesced stores instead of 8-B pieces.
+  static_assert(WTM == 64, "stats row tile == 64 rows per wave");
+  const int kg = lane >> 4, j16 = lane & 15;
+  const int row0 = m0 + wm * WTM;
+  const int cnt = min(WTM, a.M - row0);
+  constexpr int LROW = WTN * 2 + 16;  // bytes per LDS row (padded: conflict-free 8-B writes)
+  char* tl = reinterpret_cast<char*>(lds) + wid * (WTM * LROW);
   float csum[FC][4];
 #pragma unroll
   for (int c = 0; c < FC; ++c)
@@ -177,115 +186,101 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
   float bias[FC][4];
 #pragma unroll
   for (int c = 0; c < FC; ++c) {
-    const int nb = n0 + wn * WTN + c * 16 + (lane >> 4) * 4;
+    const int nb = n0 + wn * WTN + c * 16 + kg * 4;
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias[c][e] = (a.bias && nb + e < a.Ng) ? a.bias[nb + e] : 0.f;
   }
+  auto out_pix = [&](int m) -> long {
+    if (a.ostride == 1 && a.ph == 0 && a.pw == 0 && a.OW == a.wc && a.OH == a.hc) return m;
+    const int nb = m / hw, rem = m - nb * hw;
+    const int hh = rem / a.wc, ww = rem - hh * a.wc;
+    return ((long)nb * a.OH + hh * a.ostride + a.ph) * a.OW + ww * a.ostride + a.pw;
+  };
+  if (a.accumulate) {
+    // dx += dgrad: read-add-round per 8-B piece (rare: gradients meeting at a fork)
 #pragma unroll
-  for (int p = 0; p < FP; ++p) {
-    const int m = m0 + wm * WTM + p * 16 + (lane & 15);
-    const bool mok = m < a.M;
-    long opix = 0;
-    if (mok) {
-      if (a.ostride == 1 && a.ph == 0 && a.pw == 0 && a.OW == a.wc && a.OH == a.hc) {
-        opix = m;
-      } else {
-        const int nb = m / hw, rem = m - nb * hw;
-        const int hh = rem / a.wc, ww = rem - hh * a.wc;
-        opix = ((long)nb * a.OH + hh * a.ostride + a.ph) * a.OW + ww * a.ostride + a.pw;
-      }
-    }
+    for (int p = 0; p < FP; ++p) {
+      if (p * 16 + j16 >= cnt) continue;
+      const long opix = out_pix(row0 + p * 16 + j16);
 #pragma unroll
-    for (int c = 0; c < FC; ++c) {
-      const int nb = n0 + wn * WTN + c * 16 + (lane >> 4) * 4;
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = acc[c][p][e] + bias[c][e];
-        if (a.relu) v[e] = fmaxf(v[e], 0.f);
-      }
-      if (mok && nb < a.Ng) {
-        bf16* ptr = y + opix * a.ldy + nb;
-        if (a.accumulate) {
-          uint2 old = *reinterpret_cast<const uint2*>(ptr);
-          const bf16* ob = reinterpret_cast<const bf16*>(&old);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += (float)ob[e];
-        }
-        bf16 ob[4];
+      for (int c = 0; c < FC; ++c) {
+        const int nb = n0 + wn * WTN + c * 16 + kg * 4;
+        if (nb >= a.Ng) continue;
+        bf16* ptr = (bf16*)a.y + opix * a.ldy + nb;
+        uint2 old = *reinterpret_cast<const uint2*>(ptr);
+        const bf16* ob = reinterpret_cast<const bf16*>(&old);
+        bf16 o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          ob[e] = (bf16)v[e];
-          v[e] = (float)ob[e];
-          csum[c][e] += v[e];
+          float v = acc[c][p][e] + bias[c][e];
+          if (a.relu) v = fmaxf(v, 0.f);
+          o[e] = (bf16)(v + (float)ob[e]);
         }
-        *reinterpret_cast<uint2*>(ptr) = *reinterpret_cast<uint2*>(ob);
+        *reinterpret_cast<uint2*>(ptr) = *reinterpret_cast<uint2*>(o);
       }
-      // keep the rounded value for the M2 pass
+    }
+    return;
+  }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[c][p][e] = (mok && nb < a.Ng) ? v[e] : 0.f;
+  for (int p = 0; p < FP; ++p) {
+    const bool mok = p * 16 + j16 < cnt;
+#pragma unroll
+    for (int c = 0; c < FC; ++c) {
+      bf16 ob[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = acc[c][p][e] + bias[c][e];
+        if (a.relu) v = fmaxf(v, 0.f);
+        ob[e] = (bf16)v;
+        acc[c][p][e] = mok ? (float)ob[e] : 0.f;  // BN statistics are of the stored (rounded) values
+        csum[c][e] += acc[c][p][e];
+      }
+      *reinterpret_cast<uint2*>(tl + (p * 16 + j16) * LROW + (c * 16 + kg * 4) * 2) = *reinterpret_cast<uint2*>(ob);
     }
   }
-  if (!a.stats) return;
-  // per-tile BN partials: column sums over the tile's pixels, then M2 about the tile mean
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(lds);  // [NWM][BN] sums, then [NWM][BN] M2
-  const int cnt = min(BM, a.M - m0);
+  if (a.stats) {
 #pragma unroll
-  for (int c = 0; c < FC; ++c)
+    for (int c = 0; c < FC; ++c)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float s = csum[c][e];
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      s += __shfl_xor(s, 4, 64);
-      s += __shfl_xor(s, 8, 64);
-      if ((lane & 15) == 0) red[wm * BN + wn * WTN + c * 16 + (lane >> 4) * 4 + e] = s;
-    }
-  __syncthreads();
-  float m2[FC][4];
+      for (int e = 0; e < 4; ++e) {
+        float sm = csum[c][e];
+        sm += __shfl_xor(sm, 1, 64);
+        sm += __shfl_xor(sm, 2, 64);
+        sm += __shfl_xor(sm, 4, 64);
+        sm += __shfl_xor(sm, 8, 64);
+        const float mean = sm / (float)max(cnt, 1);
+        float q = 0.f;
 #pragma unroll
-  for (int c = 0; c < FC; ++c)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int col = wn * WTN + c * 16 + (lane >> 4) * 4 + e;
-      float tot = 0.f;
-#pragma unroll
-      for (int w = 0; w < NWM; ++w) tot += red[w * BN + col];
-      const float mean = tot / (float)cnt;
-      float q = 0.f;
-#pragma unroll
-      for (int p = 0; p < FP; ++p) {
-        const int m = m0 + wm * WTM + p * 16 + (lane & 15);
-        if (m < a.M) {
-          const float d = acc[c][p][e] - mean;
-          q += d * d;
+        for (int p = 0; p < FP; ++p)
+          if (p * 16 + j16 < cnt) {
+            const float d = acc[c][p][e] - mean;
+            q += d * d;
+          }
+        q += __shfl_xor(q, 1, 64);
+        q += __shfl_xor(q, 2, 64);
+        q += __shfl_xor(q, 4, 64);
+        q += __shfl_xor(q, 8, 64);
+        const int n = n0 + wn * WTN + c * 16 + kg * 4 + e;
+        if (j16 == 0 && n < a.Ng && cnt > 0) {
+          const long col = (long)blockIdx.x * NWM + wm;
+          a.stats[(long)n * a.stats_ld + col] = sm;
+          a.stats[((long)a.Ng + n) * a.stats_ld + col] = q;
         }
       }
-      q += __shfl_xor(q, 1, 64);
-      q += __shfl_xor(q, 2, 64);
-      q += __shfl_xor(q, 4, 64);
-      q += __shfl_xor(q, 8, 64);
-      m2[c][e] = q;
-    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS tile is written
+  __builtin_amdgcn_wave_barrier();
+  // coalesced write-out: lane -> (pixel row r = i*(64/CPR) + lane/CPR, 16-B chunk lane%CPR)
+  constexpr int CPR = WTN / 8;          // 16-B chunks per pixel row of the wave tile
+  constexpr int RPI = 64 / CPR;         // rows per store instruction
+  const int ck = lane % CPR, rsub = lane / CPR;
+  const int nc = n0 + wn * WTN + ck * 8;
 #pragma unroll
-  for (int c = 0; c < FC; ++c)
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if ((lane & 15) == 0) red[NWM * BN + wm * BN + wn * WTN + c * 16 + (lane >> 4) * 4 + e] = m2[c][e];
-  __syncthreads();
-  for (int col = tid; col < BN; col += NT) {
-    const int n = n0 + col;
-    if (n < a.Ng) {
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int w = 0; w < NWM; ++w) {
-        s += red[w * BN + col];
-        q += red[NWM * BN + w * BN + col];
-      }
-      a.stats[(long)n * a.stats_ld + blockIdx.x] = s;
-      a.stats[((long)a.Ng + n) * a.stats_ld + blockIdx.x] = q;
-    }
+  for (int i = 0; i < WTM / RPI; ++i) {
+    const int r = i * RPI + rsub;
+    if (r >= cnt || nc >= a.Ng) continue;
+    bf16* ptr = (bf16*)a.y + out_pix(row0 + r) * a.ldy + nc;
+    *reinterpret_cast<uint4*>(ptr) = *reinterpret_cast<const uint4*>(tl + r * LROW + ck * 16);
   }
 }
 
@@ -450,313 +445,6 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// TN v3: persistent, 3-stage LDS-DMA pipeline.
-//  * operands go HBM/L2 -> LDS by buffer_load_dwordx4 ... lds (no VGPR staging); the XOR
-//    swizzle of the LDS image is applied to the per-lane SOURCE offset (the DMA destination is
-//    lane-linear), padding taps / out-of-range rows read past num_records -> zeros;
-//  * counted `s_waitcnt vmcnt(N)` + raw s_barrier: two stages stay in flight while one is
-//    consumed (never vmcnt(0) in the steady state);
-//  * persistent blocks (one per CU) walk tiles; the loads of the next tile's first steps overlap
-//    the current tile's epilogue.  Tiles are dealt so that the 8 XCDs each get contiguous runs
-//    (neighbouring pixel rows share halos in one L2); speed-only, never correctness.
-// ------------------------------------------------------------------------------------------
-template <int BM, int BN, int NWM, int NWN>
-__global__ __launch_bounds__(64 * NWM * NWN) void tn_dma_kernel(FastTNArgs a, int mtiles, int ntiles) {
-  constexpr int NW = NWM * NWN;
-  constexpr int WTM = BM / NWM, WTN = BN / NWN;
-  constexpr int FP = WTM / 16, FC = WTN / 16;
-  constexpr int AI = BM / 8 / NW, BI = BN / 8 / NW;
-  constexpr int INS = AI + BI;
-  constexpr int STAGES = 3;
-  constexpr int STAGE = (BM + BN) * 8;  // uint4 per stage
-  static_assert(AI >= 1 && BI >= 1, "each wave must issue A and B DMA");
-  extern __shared__ __attribute__((aligned(16))) uint4 lds[];
-  float* red = reinterpret_cast<float*>(lds + STAGES * STAGE);  // [2][NWM][BN] stats scratch
-  float* sbias = red + 2 * NWM * BN;                             // [Ng] bias
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / NWN, wn = wid % NWN;
-  const int hw = a.hc * a.wc;
-  const __amdgpu_buffer_rsrc_t r1 = srd(a.x1, a.x1_bytes);
-  const __amdgpu_buffer_rsrc_t r2 = srd(a.x2 ? a.x2 : a.x1, a.x2 ? a.x2_bytes : 0u);
-  const __amdgpu_buffer_rsrc_t rw = srd(a.wt, a.w_bytes);
-  if (a.bias)
-    for (int i = tid; i < a.Ng; i += 64 * NW) sbias[i] = a.bias[i];
-
-  // tiles of this block: XCD-grouped deal of the persistent grid
-  const int G = gridDim.x;
-  const int total = mtiles * ntiles;
-  const int nx = G / 8;
-  const int slot = (G % 8 == 0) ? ((int)blockIdx.x % 8) * nx + (int)blockIdx.x / 8 : (int)blockIdx.x;
-  const int my_tiles = slot < total ? (total - slot + G - 1) / G : 0;
-  const int nch = a.cin >> 6;
-  const int nsteps = a.nr * a.ns * nch;
-  const int total_steps = my_tiles * nsteps;
-
-  // ---- issue-side state (scalar) and per-lane row info of the tile being issued ----
-  int is_tile = 0, is_jr = 0, is_js = 0, is_c = 0;
-  int pix[AI];
-  unsigned vmask[AI], boff[BI];
-  const int pc = lane & 7, rsub = lane >> 3;
-  auto setup_rows = [&](int t) {
-    const int tile = slot + t * G;
-    const int tm = tile % mtiles, tn = tile / mtiles;
-    const int m0 = tm * BM, n0 = tn * BN;
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      const int row = (wid * AI + i) * 8 + rsub;
-      const int m = m0 + row;
-      pix[i] = 0;
-      vmask[i] = 0u;
-      if (m < a.M) {
-        const int nb = m / hw, rem = m - nb * hw;
-        const int hh = rem / a.wc, ww = rem - hh * a.wc;
-        const int ih0 = hh * a.istride, iw0 = ww * a.istride;
-        pix[i] = (nb * a.H + ih0) * a.W + iw0;
-        unsigned msk = 0u;
-        for (int jr = 0; jr < a.nr; ++jr) {
-          const int ih = ih0 + a.dh0 + a.dhs * jr;
-          if (ih < 0 || ih >= a.H) continue;
-          for (int js = 0; js < a.ns; ++js) {
-            const int iw = iw0 + a.dw0 + a.dws * js;
-            if (iw >= 0 && iw < a.W) msk |= 1u << (jr * a.ns + js);
-          }
-        }
-        vmask[i] = msk;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < BI; ++i) {
-      const int row = (wid * BI + i) * 8 + rsub;
-      const int n = n0 + row;
-      const int lc = swz8(row, pc);  // logical chunk held by physical chunk pc (XOR involution)
-      boff[i] = n < a.Ng ? (unsigned)n * (unsigned)a.ldwb + lc * 16 : kOOB;
-    }
-  };
-  auto issue = [&](int buf) {
-    const int dh = a.dh0 + a.dhs * is_jr, dw = a.dw0 + a.dws * is_js;
-    const int tapbit = is_jr * a.ns + is_js;
-    const int tapdelta = dh * a.W + dw;
-    const unsigned wofs = (unsigned)(((a.r0 + a.rs * is_jr) * a.S + (a.s0 + a.ss * is_js)) * a.cin + is_c) * 2u;
-    const unsigned base = lds_addr(lds) + (unsigned)buf * (STAGE * 16);
-    const bool first = is_c < a.c1;
-    const unsigned ldcb = first ? (unsigned)a.ldc1b : (unsigned)a.ldc2b;
-    const unsigned cb = (unsigned)(first ? is_c : is_c - a.c1) * 2u;
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      const int row = (wid * AI + i) * 8 + rsub;
-      const int lc = swz8(row, pc);  // logical chunk held by physical chunk pc (XOR involution)
-      const bool ok = (vmask[i] >> tapbit) & 1u;
-      const unsigned off = ok ? (unsigned)(pix[i] + tapdelta) * ldcb + cb + lc * 16 : kOOB;
-      const unsigned dst = base + (unsigned)(wid * AI + i) * 1024u;
-      if (first)
-        dma16(r1, dst, off);
-      else
-        dma16(r2, dst, off);
-    }
-#pragma unroll
-    for (int i = 0; i < BI; ++i) {
-      const unsigned dst = base + (unsigned)(BM * 128 + (wid * BI + i) * 1024);
-      dma16(rw, dst, boff[i] == kOOB ? kOOB : boff[i] + wofs);
-    }
-    is_c += 64;
-    if (is_c >= a.cin) {
-      is_c = 0;
-      if (++is_js == a.ns) {
-        is_js = 0;
-        if (++is_jr == a.nr) {
-          is_jr = 0;
-          if (++is_tile < my_tiles) setup_rows(is_tile);
-        }
-      }
-    }
-  };
-
-  f32x4 acc[FC][FP];
-#pragma unroll
-  for (int c = 0; c < FC; ++c)
-#pragma unroll
-    for (int p = 0; p < FP; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // sbias visible
-  if (total_steps > 0) setup_rows(0);
-  if (total_steps > 0) issue(0);
-  if (total_steps > 1) issue(1);
-
-  int ct = 0, cstep = 0, bc = 0, bi = 2;
-  for (int g = 0; g < total_steps; ++g) {
-    if (g + 1 < total_steps)
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(INS) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    if (g + 2 < total_steps) {
-      issue(bi);
-      bi = bi == STAGES - 1 ? 0 : bi + 1;
-    }
-    const uint4* As = lds + bc * STAGE;
-    bc = bc == STAGES - 1 ? 0 : bc + 1;
-    const uint4* Bs = As + BM * 8;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int ch = kk * 4 + (lane >> 4);
-      bf16x8 pf[FP], wf[FC];
-#pragma unroll
-      for (int p = 0; p < FP; ++p) {
-        const int row = wm * WTM + p * 16 + (lane & 15);
-        uint4 v = As[row * 8 + swz8(row, ch)];
-        pf[p] = *reinterpret_cast<bf16x8*>(&v);
-      }
-#pragma unroll
-      for (int c = 0; c < FC; ++c) {
-        const int row = wn * WTN + c * 16 + (lane & 15);
-        uint4 v = Bs[row * 8 + swz8(row, ch)];
-        wf[c] = *reinterpret_cast<bf16x8*>(&v);
-      }
-#pragma unroll
-      for (int c = 0; c < FC; ++c)
-#pragma unroll
-        for (int p = 0; p < FP; ++p)
-          acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], pf[p], acc[c][p], 0, 0, 0);
-    }
-    if (++cstep < nsteps) continue;
-    // ================= epilogue of tile ct =================
-    cstep = 0;
-    const int tile = slot + ct * G;
-    ++ct;
-    const int tm = tile % mtiles, tn = tile / mtiles;
-    const int m0 = tm * BM, n0 = tn * BN;
-    bf16* y = (bf16*)a.y;
-    float csum[FC][4];
-#pragma unroll
-    for (int c = 0; c < FC; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) csum[c][e] = 0.f;
-#pragma unroll
-    for (int p = 0; p < FP; ++p) {
-      const int m = m0 + wm * WTM + p * 16 + (lane & 15);
-      const bool mok = m < a.M;
-      long opix = 0;
-      if (mok) {
-        if (a.ostride == 1 && a.ph == 0 && a.pw == 0 && a.OW == a.wc && a.OH == a.hc) {
-          opix = m;
-        } else {
-          const int nb = m / hw, rem = m - nb * hw;
-          const int hh = rem / a.wc, ww = rem - hh * a.wc;
-          opix = ((long)nb * a.OH + hh * a.ostride + a.ph) * a.OW + ww * a.ostride + a.pw;
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < FC; ++c) {
-        const int nb = n0 + wn * WTN + c * 16 + (lane >> 4) * 4;
-        const bool ok = mok && nb < a.Ng;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = acc[c][p][e] + ((a.bias && ok) ? sbias[nb + e] : 0.f);
-          if (a.relu) v[e] = fmaxf(v[e], 0.f);
-        }
-        if (ok) {
-          bf16* ptr = y + opix * a.ldy + nb;
-          if (a.accumulate) {
-            uint2 old = *reinterpret_cast<const uint2*>(ptr);
-            const bf16* ob = reinterpret_cast<const bf16*>(&old);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += (float)ob[e];
-          }
-          bf16 ob[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            ob[e] = (bf16)v[e];
-            v[e] = (float)ob[e];
-            csum[c][e] += v[e];
-          }
-          *reinterpret_cast<uint2*>(ptr) = *reinterpret_cast<uint2*>(ob);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[c][p][e] = ok ? v[e] : 0.f;
-      }
-    }
-    if (a.stats) {
-      const int cnt = min(BM, a.M - m0);
-#pragma unroll
-      for (int c = 0; c < FC; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float sm = csum[c][e];
-          sm += __shfl_xor(sm, 1, 64);
-          sm += __shfl_xor(sm, 2, 64);
-          sm += __shfl_xor(sm, 4, 64);
-          sm += __shfl_xor(sm, 8, 64);
-          if ((lane & 15) == 0) red[wm * BN + wn * WTN + c * 16 + (lane >> 4) * 4 + e] = sm;
-        }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#pragma unroll
-      for (int c = 0; c < FC; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int col = wn * WTN + c * 16 + (lane >> 4) * 4 + e;
-          float tot = 0.f;
-#pragma unroll
-          for (int w = 0; w < NWM; ++w) tot += red[w * BN + col];
-          const float mean = tot / (float)cnt;
-          float q = 0.f;
-#pragma unroll
-          for (int p = 0; p < FP; ++p) {
-            const int m = m0 + wm * WTM + p * 16 + (lane & 15);
-            if (m < a.M) {
-              const float d = acc[c][p][e] - mean;
-              q += d * d;
-            }
-          }
-          q += __shfl_xor(q, 1, 64);
-          q += __shfl_xor(q, 2, 64);
-          q += __shfl_xor(q, 4, 64);
-          q += __shfl_xor(q, 8, 64);
-          if ((lane & 15) == 0) red[NWM * BN + wm * BN + col] = q;
-        }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      for (int col = tid; col < BN; col += 64 * NW) {
-        const int n = n0 + col;
-        if (n < a.Ng) {
-          float sm = 0.f, q = 0.f;
-#pragma unroll
-          for (int w = 0; w < NWM; ++w) {
-            sm += red[w * BN + col];
-            q += red[NWM * BN + w * BN + col];
-          }
-          a.stats[(long)n * a.stats_ld + tm] = sm;
-          a.stats[((long)a.Ng + n) * a.stats_ld + tm] = q;
-        }
-      }
-      // protect `red` against the next tile's epilogue
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-#pragma unroll
-    for (int c = 0; c < FC; ++c)
-#pragma unroll
-      for (int p = 0; p < FP; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-}
-
-template <int BM, int BN, int NWM, int NWN>
-int launch_tn_dma(const FastTNArgs& a, hipStream_t st) {
-  constexpr int NW = NWM * NWN;
-  const size_t lds = 3 * (size_t)(BM + BN) * 128 + (size_t)(2 * NWM * BN) * 4 + (size_t)a.Ng * 4;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_dma_kernel<BM, BN, NWM, NWN>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-    attr = true;
-  }
-  const int mtiles = ceil_div(a.M, BM), ntiles = ceil_div(a.Ng, BN);
-  int grid = 256;  // one block per CU
-  if (mtiles * ntiles < grid) grid = mtiles * ntiles;
-  hipLaunchKernelGGL((tn_dma_kernel<BM, BN, NWM, NWN>), dim3(grid), dim3(64 * NW), lds, st, a, mtiles, ntiles);
-  return 0;
-}
-
 template <int BM, int BN, int NWM, int NWN>
 int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   constexpr int NT = 64 * NWM * NWN;
@@ -778,32 +466,24 @@ bool tn_fast_ok(const FastTNArgs& a) {
   return a.cin % 64 == 0 && a.c1 % 64 == 0 && a.nr * a.ns <= 32 && a.Ng % 8 == 0;
 }
 
-// The persistent LDS-DMA kernel is opt-in until it beats the register-staged one.
-static bool use_v3() {
-  static const bool on = getenv("UNETSEG_TN_V3") != nullptr;
-  return on;
+// 256-row tiles when they still fill the chip, else 128
+static bool tn_big_tiles(const FastTNArgs& a) {
+  const long tiles_big = (long)ceil_div(a.M, 256) * ceil_div(a.Ng, 128);
+  return tiles_big >= 256;
 }
 
+// Row tile of the BN partial statistics: per wave (64 rows) on the TN kernels, per 8x32 spatial
+// tile on the halo kernel.
 int tn_fast_tile_m(const FastTNArgs& a) {
   if (halo3_ok(a)) return halo_tile_m();
-  if (a.Ng <= 64) return 256;
-  const long tiles_big = (long)ceil_div(a.M, 256) * ceil_div(a.Ng, 128);
-  if (use_v3()) return tiles_big >= 128 ? 256 : 128;
-  return tiles_big >= 256 ? 256 : 128;
+  return 64;
 }
 
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
   if (a.M <= 0 || a.Ng <= 0) return 0;
   if (halo3_ok(a)) return launch_halo3(a, st);
-  // zero-tap dgrad parity classes (nr*ns == 0) only write zeros: the register-staged kernel's
-  // empty K loop does that, the persistent kernel would skip the tile entirely
-  if (use_v3() && a.Ng <= 64 * 2048 && a.nr * a.ns > 0) {  // bias staged in LDS
-    if (a.Ng <= 64) return launch_tn_dma<256, 64, 8, 1>(a, st);
-    if (tn_fast_tile_m(a) == 256) return launch_tn_dma<256, 128, 4, 2>(a, st);
-    return launch_tn_dma<128, 128, 2, 4>(a, st);
-  }
   if (a.Ng <= 64) return launch_tn_cfg<256, 64, 4, 1>(a, st);
-  if (tn_fast_tile_m(a) == 256) return launch_tn_cfg<256, 128, 4, 2>(a, st);
+  if (tn_big_tiles(a)) return launch_tn_cfg<256, 128, 4, 2>(a, st);
   return launch_tn_cfg<128, 128, 2, 2>(a, st);
 }
 

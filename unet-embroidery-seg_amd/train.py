@@ -100,6 +100,8 @@ def train(args):
     device = torch.device("cuda", local) if world > 1 else torch.device(args.device)
     if device.type != "cuda" or not torch.cuda.is_available():
         raise RuntimeError("the HIP training path needs a GPU (no CPU fallback)")
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
     torch.cuda.set_device(device)
     exp_folder = os.path.join(args.out_dir, datetime.datetime.now().strftime("exp_%Y%m%d_%H%M%S"))
     weights_folder = os.path.join(exp_folder, "weights")
