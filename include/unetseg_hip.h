@@ -60,7 +60,7 @@ int unetseg_conv_tile_m(void);
 int unetseg_conv2d_fwd_tile_m(int dtype, int c1, int ldc1, int c2, int ldc2, int n, int h, int w, int cout, int r,
                               int s, int stride, int pad);
 /* y[n,p,q,cout] = conv(cat(x1[.., c1], x2[.., c2]), wk) (+bias) (ReLU); stats (may be NULL):
- * fp32 [2][cout][ceil(M/tile)] = per-tile (sum, M2 about the tile mean) of the rounded y (BN train) */
+ * fp32 [ceil(M/tile)][2][cout] = per-tile (sum, M2 about the tile mean) of the rounded y (BN train) */
 int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h,
                        int w, const void* wk, int cout, int r, int s, int stride, int pad, const float* bias, int relu,
                        void* y, int ldy, float* stats, void* stream);
@@ -79,7 +79,7 @@ int unetseg_pack_input(int dtype, const float* x, int n, int c, int h, int w, in
 /* ---- BatchNorm2d, training and eval (model/resnet_backbone.py:127,169; model/unet_plain.py:10,13;
  *      model/unet_attention.py:17,21,25) -------------------------------------------------------- */
 
-/* Chan-merge conv partials -> batch mean/invstd, scale/shift; update running stats (momentum,
+/* Chan-merge conv partials part[G][2][C] -> batch mean/invstd, scale/shift; update running stats (momentum,
  * unbiased var) and num_batches_tracked when rmean != NULL */
 int unetseg_bn_finalize(const float* part, int C, int G, long M, int tile, const float* gamma, const float* beta,
                         float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* mean,
@@ -92,15 +92,19 @@ int unetseg_bn_apply(int dtype, const void* y, int ldy, const float* sc, const f
                      void* stream);
 /* partial-buffer geometry of the channel reductions below: returns G (row groups) */
 int unetseg_reduce_tiles(int dtype, long M, int C, int* tv_out, int* ppb_out);
-/* backward through [relu](BN(y1) [+ BN(y2)]): per-channel partials of dz and dz*xhat */
-int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const void* A, int lda, const void* y1, int ld1,
-                          const float* mean1, const float* inv1, const void* y2, int ld2, const float* mean2,
-                          const float* inv2, long M, int C, float* part, int G, void* stream);
+/* backward through [relu](BN(y1) [+ BN(y2)]): per-channel partials of dz and dz*xhat.  The ReLU
+ * mask comes from the activation A, or (A == NULL, msc != NULL: no residual) is recomputed from y1
+ * as fmaf(y1, msc, msh) > 0 -- the forward's BN scale/shift -- saving one tensor read. */
+int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const void* A, int lda, const float* msc,
+                          const float* msh, const void* y1, int ld1, const float* mean1, const float* inv1,
+                          const void* y2, int ld2, const float* mean2, const float* inv2, long M, int C, float* part,
+                          int G, void* stream);
 int unetseg_bn_bwd_finalize(const float* part, int C, int G, long M, int nbranch, const float* g1, const float* inv1,
                             float* dg1, float* db1, const float* g2, const float* inv2, float* dg2, float* db2,
                             float* coef, void* stream);
-int unetseg_bn_bwd_apply(int dtype, const void* dA, int ldd, const void* A, int lda, const void* y1, int ld1,
-                         const float* mean1, const float* inv1, void* dy1, int ldo1, const void* y2, int ld2,
+int unetseg_bn_bwd_apply(int dtype, const void* dA, int ldd, const void* A, int lda, const float* msc,
+                         const float* msh, const void* y1, int ld1, const float* mean1, const float* inv1, void* dy1,
+                         int ldo1, const void* y2, int ld2,
                          const float* mean2, const float* inv2, void* dy2, int ldo2, const float* coef, void* dzout,
                          int ldz, int dz_acc, long M, int C, void* stream);
 /* ReLU backward (mask from the activation A) + per-channel bias-grad partials */
@@ -124,7 +128,7 @@ int unetseg_add(int dtype, const void* x, int ldx, void* out, int ldo, long M, i
 /* ---- narrow 1x1 heads (final / outc / seg_head / psi: model/unet_resnet.py:78,
  *      model/unet_plain.py:69, model/unet_multitask.py:69, model/unet_attention.py:24) ------------ */
 int unetseg_pw_small_tiles(long M);
-/* y fp32 planar [n][k][hw] (k <= 2); stats (k == 1, may be NULL) [2][unetseg_pw_small_tiles(M)] */
+/* y fp32 planar [n][k][hw] (k <= 2); stats (k == 1, may be NULL) [unetseg_pw_small_tiles(M)][2] */
 int unetseg_pw_small_fwd(int dtype, const void* x, int ldx, long M, int hw, int c, int k, const float* w,
                          const float* b, float* y, float* stats, void* stream);
 int unetseg_pw_small_bwd(int dtype, const float* dy, const void* x, int ldx, long M, int hw, int c, int k,

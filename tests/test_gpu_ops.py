@@ -74,6 +74,8 @@ CONV_CASES = [
     # 3x3 halo kernel (64 input channels, H % 8 == 0, W % 32 == 0): fwd 64->192, dgrad 192<-64
     (2, 16, 64, 64, 0, 192, 3, 1, 1, True, True),
     (1, 24, 32, 192, 0, 64, 3, 1, 1, False, False),
+    # one K step (64 input channels, 1x1): single-stage 128x128 TN configuration
+    (2, 16, 24, 64, 0, 256, 1, 1, 0, False, False),
 ]
 
 

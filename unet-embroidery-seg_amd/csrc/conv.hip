@@ -53,7 +53,7 @@ struct IgemmArgs {
   int ldy, accumulate;
   const float* bias;
   int relu;
-  float* stats;            // [2][Ng][stats_ld] (sum, M2 about the tile mean) per M tile
+  float* stats;            // [M tiles][2][Ng] (sum, M2 about the tile mean)
   int stats_ld;
   int M;
 };
@@ -287,8 +287,8 @@ __global__ __launch_bounds__(256) void igemm_tn_kernel(IgemmArgs a) {
     for (int c = tid; c < BN; c += 256) {
       const int n = n0 + c;
       if (n < a.Ng) {
-        a.stats[(long)n * a.stats_ld + blockIdx.x] = red[c] + red[BN + c];
-        a.stats[((long)a.Ng + n) * a.stats_ld + blockIdx.x] = red[2 * BN + c] + red[3 * BN + c];
+        a.stats[(long)blockIdx.x * 2 * a.Ng + n] = red[c] + red[BN + c];
+        a.stats[(long)blockIdx.x * 2 * a.Ng + a.Ng + n] = red[2 * BN + c] + red[3 * BN + c];
       }
     }
   }
@@ -621,7 +621,7 @@ UNETSEG_API int unetseg_conv_tile_m(void) { return kBM; }
 // Forward conv.  x = cat([x1 (c1 ch, pixel stride ldc1), x2 (c2 ch, ldc2)], C) NHWC [n,h,w,*];
 // wk: dtype [cout][r][s][c1+c2]; y: NHWC [n,p,q,*] pixel stride ldy.
 // Epilogue: + bias[cout] (fp32, may be NULL), ReLU if relu, and when stats != NULL the per-M-tile
-// BN partials stats[2][cout][ceil(M/128)] (column sum, M2 about the tile mean) of the rounded y.
+// BN partials stats[ceil(M/tile)][2][cout] (column sum, M2 about the tile mean) of the rounded y.
 static IgemmArgs fwd_args(const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h, int w,
                           const void* wk, int cout, int r, int s, int stride, int pad) {
   const int p = (h + 2 * pad - r) / stride + 1, q = (w + 2 * pad - s) / stride + 1;
@@ -643,7 +643,7 @@ static int fwd_tile_m(int dtype, const IgemmArgs& a) {
 }
 
 // Row tile of the BN partial statistics written by unetseg_conv2d_fwd for this shape:
-// stats is [2][cout][ceil(n*p*q / tile)].
+// stats is [ceil(n*p*q / tile)][2][cout].
 UNETSEG_API int unetseg_conv2d_fwd_tile_m(int dtype, int c1, int ldc1, int c2, int ldc2, int n, int h, int w,
                                           int cout, int r, int s, int stride, int pad) {
   IgemmArgs a = fwd_args(nullptr, c1, ldc1, nullptr, c2, ldc2, n, h, w, nullptr, cout, r, s, stride, pad);
@@ -653,7 +653,7 @@ UNETSEG_API int unetseg_conv2d_fwd_tile_m(int dtype, int c1, int ldc1, int c2, i
 // Forward conv.  x = cat([x1 (c1 ch, pixel stride ldc1), x2 (c2 ch, ldc2)], C) NHWC [n,h,w,*];
 // wk: dtype [cout][r][s][c1+c2]; y: NHWC [n,p,q,*] pixel stride ldy.
 // Epilogue: + bias[cout] (fp32, may be NULL), ReLU if relu, and when stats != NULL the per-row-tile
-// BN partials stats[2][cout][ceil(M/tile)] (column sum, M2 about the tile mean) of the rounded y,
+// BN partials stats[ceil(M/tile)][2][cout] (column sum, M2 about the tile mean) of the rounded y,
 // tile = unetseg_conv2d_fwd_tile_m(...).
 UNETSEG_API int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2,
                                    int n, int h, int w, const void* wk, int cout, int r, int s, int stride,

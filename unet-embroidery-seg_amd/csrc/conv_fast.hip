@@ -18,13 +18,14 @@
 #include "conv_fast.h"
 #include "fast_util.h"
 
+
 namespace {
 
 
 // ------------------------------------------------------------------------------------------
 // TN (fwd / dgrad).  Tile: BM pixels x BN output channels, K step 64 channels of one tap.
 // ------------------------------------------------------------------------------------------
-template <int BM, int BN, int NWM, int NWN>
+template <int BM, int BN, int NWM, int NWN, int ST>
 __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int WTM = BM / NWM, WTN = BN / NWN;
@@ -138,8 +139,8 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
   }
   for (int kt = 0; kt < nsteps; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nsteps) gload();
-    const uint4* As = lds + cur * STAGE;
+    if (ST > 1 && kt + 1 < nsteps) gload();
+    const uint4* As = lds + (ST > 1 ? cur : 0) * STAGE;
     const uint4* Bs = As + BM * 8;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -163,21 +164,24 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
         for (int p = 0; p < FP; ++p)
           acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], pf[p], acc[c][p], 0, 0, 0);
     }
-    if (kt + 1 < nsteps) sstore(cur ^ 1);
+    if (ST > 1 && kt + 1 < nsteps) sstore(cur ^ 1);
     __syncthreads();
   }
 
   // ---- epilogue: lane holds D[cout = (lane>>4)*4 + e][pixel = lane&15] per (c, p) subtile ----
-  // bias + ReLU + bf16 rounding in registers; per-wave BN partials over the wave's WTM rows (no
-  // barrier: the stats row tile is WTM = 64); then each wave transposes its WTM x WTN tile through
-  // LDS (the operand stages are free after the K loop's last barrier) and writes whole 16-B chunks
-  // of each pixel's channel run: coalesced stores instead of 8-B pieces.
-  static_assert(WTM == 64, "stats row tile == 64 rows per wave");
+  // bias + ReLU + bf16 rounding in registers; per-wave BN partials (sum, M2 about the wave's
+  // mean) by shuffles; each wave transposes its WTM x WTN tile through LDS (the operand stages are
+  // free after the K loop's last barrier) and writes whole 16-B chunks of each pixel's channel
+  // run; finally one barrier and a Chan merge of the row-waves' partials per output channel.
+  static_assert(WTM == 64, "64 rows per wave");
   const int kg = lane >> 4, j16 = lane & 15;
   const int row0 = m0 + wm * WTM;
   const int cnt = min(WTM, a.M - row0);
   constexpr int LROW = WTN * 2 + 16;  // bytes per LDS row (padded: conflict-free 8-B writes)
   char* tl = reinterpret_cast<char*>(lds) + wid * (WTM * LROW);
+  // per-wave (sum, M2) of the stats, after every wave's transpose tile: [2][NWM][BN]
+  float* red = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + NWM * NWN * WTM * LROW);
+
   float csum[FC][4];
 #pragma unroll
   for (int c = 0; c < FC; ++c)
@@ -196,31 +200,6 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
     const int hh = rem / a.wc, ww = rem - hh * a.wc;
     return ((long)nb * a.OH + hh * a.ostride + a.ph) * a.OW + ww * a.ostride + a.pw;
   };
-  if (a.accumulate) {
-    // dx += dgrad: read-add-round per 8-B piece (rare: gradients meeting at a fork)
-#pragma unroll
-    for (int p = 0; p < FP; ++p) {
-      if (p * 16 + j16 >= cnt) continue;
-      const long opix = out_pix(row0 + p * 16 + j16);
-#pragma unroll
-      for (int c = 0; c < FC; ++c) {
-        const int nb = n0 + wn * WTN + c * 16 + kg * 4;
-        if (nb >= a.Ng) continue;
-        bf16* ptr = (bf16*)a.y + opix * a.ldy + nb;
-        uint2 old = *reinterpret_cast<const uint2*>(ptr);
-        const bf16* ob = reinterpret_cast<const bf16*>(&old);
-        bf16 o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = acc[c][p][e] + bias[c][e];
-          if (a.relu) v = fmaxf(v, 0.f);
-          o[e] = (bf16)(v + (float)ob[e]);
-        }
-        *reinterpret_cast<uint2*>(ptr) = *reinterpret_cast<uint2*>(o);
-      }
-    }
-    return;
-  }
 #pragma unroll
   for (int p = 0; p < FP; ++p) {
     const bool mok = p * 16 + j16 < cnt;
@@ -244,10 +223,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float sm = csum[c][e];
-        sm += __shfl_xor(sm, 1, 64);
-        sm += __shfl_xor(sm, 2, 64);
-        sm += __shfl_xor(sm, 4, 64);
-        sm += __shfl_xor(sm, 8, 64);
+        sm = row16_sum(sm);
         const float mean = sm / (float)max(cnt, 1);
         float q = 0.f;
 #pragma unroll
@@ -256,15 +232,11 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
             const float d = acc[c][p][e] - mean;
             q += d * d;
           }
-        q += __shfl_xor(q, 1, 64);
-        q += __shfl_xor(q, 2, 64);
-        q += __shfl_xor(q, 4, 64);
-        q += __shfl_xor(q, 8, 64);
-        const int n = n0 + wn * WTN + c * 16 + kg * 4 + e;
-        if (j16 == 0 && n < a.Ng && cnt > 0) {
-          const long col = (long)blockIdx.x * NWM + wm;
-          a.stats[(long)n * a.stats_ld + col] = sm;
-          a.stats[((long)a.Ng + n) * a.stats_ld + col] = q;
+        q = row16_sum(q);
+        if (j16 == 0) {
+          const int col = wn * WTN + c * 16 + kg * 4 + e;
+          red[wm * BN + col] = sm;
+          red[(NWM + wm) * BN + col] = q;
         }
       }
   }
@@ -280,7 +252,43 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
     const int r = i * RPI + rsub;
     if (r >= cnt || nc >= a.Ng) continue;
     bf16* ptr = (bf16*)a.y + out_pix(row0 + r) * a.ldy + nc;
-    *reinterpret_cast<uint4*>(ptr) = *reinterpret_cast<const uint4*>(tl + r * LROW + ck * 16);
+    uint4 v = *reinterpret_cast<const uint4*>(tl + r * LROW + ck * 16);
+    if (a.accumulate) {  // dx += dgrad (two bf16 tensors summed in fp32, like autograd's accumulation)
+      const uint4 old = *reinterpret_cast<const uint4*>(ptr);
+      const bf16* ob = reinterpret_cast<const bf16*>(&old);
+      bf16* nv = reinterpret_cast<bf16*>(&v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) nv[e] = (bf16)((float)nv[e] + (float)ob[e]);
+    }
+    *reinterpret_cast<uint4*>(ptr) = v;
+  }
+  if (a.stats) {
+    // Chan merge of the NWM row-wave partials -> one (sum, M2) per block row tile (BM rows),
+    // written contiguously: stats[blockIdx.x][2][Ng].  Raw barrier: LDS visibility only -- a
+    // __syncthreads() would also wait for this block's output stores to retire.
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int col = tid; col < BN; col += NT) {
+      const int n = n0 + col;
+      if (n >= a.Ng) continue;
+      float st = 0.f, nt = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWM; ++w) {
+        st += red[w * BN + col];
+        nt += (float)max(0, min(WTM, a.M - (m0 + w * WTM)));
+      }
+      const float mean = st / fmaxf(nt, 1.f);
+      float q = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWM; ++w) {
+        const float nw = (float)max(0, min(WTM, a.M - (m0 + w * WTM)));
+        if (nw > 0.f) {
+          const float d = red[w * BN + col] / nw - mean;
+          q += red[(NWM + w) * BN + col] + nw * d * d;
+        }
+      }
+      a.stats[(long)blockIdx.x * 2 * a.Ng + n] = st;
+      a.stats[(long)blockIdx.x * 2 * a.Ng + a.Ng + n] = q;
+    }
   }
 }
 
@@ -445,19 +453,34 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     }
 }
 
-template <int BM, int BN, int NWM, int NWN>
+template <int BM, int BN, int NWM, int NWN, int ST>
 int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   constexpr int NT = 64 * NWM * NWN;
-  const size_t lds = 2 * (size_t)(BM + BN) * 8 * 16;
+  // operand stages, or the epilogue's per-wave transpose tiles + stats scratch if larger
+  const size_t stages = (size_t)ST * (BM + BN) * 8 * 16;
+  const size_t epi = (size_t)NWM * NWN * 64 * ((BN / NWN) * 2 + 16) + 2 * NWM * BN * 4;
+  const size_t lds = stages > epi ? stages : epi;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_fast_kernel<BM, BN, NWM, NWN>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_fast_kernel<BM, BN, NWM, NWN, ST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   dim3 grid(ceil_div(a.M, BM), ceil_div(a.Ng, BN), 1);
-  hipLaunchKernelGGL((tn_fast_kernel<BM, BN, NWM, NWN>), grid, dim3(NT), lds, st, a);
+  hipLaunchKernelGGL((tn_fast_kernel<BM, BN, NWM, NWN, ST>), grid, dim3(NT), lds, st, a);
   return 0;
+}
+
+// TN configuration: 0 = halo, 1 = 256x64, 2 = 256x128, 3 = 128x128, 4 = 128x128 single stage
+// (one K step: the prefetch stage would only cost occupancy)
+static int tn_config(const FastTNArgs& a) {
+  if (halo3_ok(a)) return 0;
+  const int nsteps = a.nr * a.ns * (a.cin >> 6);
+  if (nsteps == 1 && a.Ng > 64) return 4;
+  if (a.Ng <= 64) return 1;
+  if (nsteps <= 4) return 3;
+  const long tiles_big = (long)ceil_div(a.M, 256) * ceil_div(a.Ng, 128);
+  return tiles_big >= 256 ? 2 : 3;
 }
 
 }  // namespace
@@ -466,25 +489,22 @@ bool tn_fast_ok(const FastTNArgs& a) {
   return a.cin % 64 == 0 && a.c1 % 64 == 0 && a.nr * a.ns <= 32 && a.Ng % 8 == 0;
 }
 
-// 256-row tiles when they still fill the chip, else 128
-static bool tn_big_tiles(const FastTNArgs& a) {
-  const long tiles_big = (long)ceil_div(a.M, 256) * ceil_div(a.Ng, 128);
-  return tiles_big >= 256;
-}
-
-// Row tile of the BN partial statistics: per wave (64 rows) on the TN kernels, per 8x32 spatial
-// tile on the halo kernel.
+// Row tile of the BN partial statistics = the block's rows (BM) on the TN kernels, one 8x32
+// spatial tile on the halo kernel.
 int tn_fast_tile_m(const FastTNArgs& a) {
-  if (halo3_ok(a)) return halo_tile_m();
-  return 64;
+  const int cfg = tn_config(a);
+  return cfg == 0 ? halo_tile_m() : (cfg <= 2 ? 256 : 128);
 }
 
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
   if (a.M <= 0 || a.Ng <= 0) return 0;
-  if (halo3_ok(a)) return launch_halo3(a, st);
-  if (a.Ng <= 64) return launch_tn_cfg<256, 64, 4, 1>(a, st);
-  if (tn_big_tiles(a)) return launch_tn_cfg<256, 128, 4, 2>(a, st);
-  return launch_tn_cfg<128, 128, 2, 2>(a, st);
+  switch (tn_config(a)) {
+    case 0: return launch_halo3(a, st);
+    case 1: return launch_tn_cfg<256, 64, 4, 1, 2>(a, st);
+    case 2: return launch_tn_cfg<256, 128, 4, 2, 2>(a, st);
+    case 4: return launch_tn_cfg<128, 128, 2, 2, 1>(a, st);
+    default: return launch_tn_cfg<128, 128, 2, 2, 2>(a, st);
+  }
 }
 
 bool wgrad_fast_ok(const FastWgradArgs& a) {

@@ -200,10 +200,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float s = csum[c][e];
-          s += __shfl_xor(s, 1, 64);
-          s += __shfl_xor(s, 2, 64);
-          s += __shfl_xor(s, 4, 64);
-          s += __shfl_xor(s, 8, 64);
+          s = row16_sum(s);
           if (j16 == 0) red[wid * 64 + c * 16 + kg * 4 + e] = s;
         }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -223,10 +220,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
             const float d = acc[c][p][e] - mean;
             q += d * d;
           }
-          q += __shfl_xor(q, 1, 64);
-          q += __shfl_xor(q, 2, 64);
-          q += __shfl_xor(q, 4, 64);
-          q += __shfl_xor(q, 8, 64);
+          q = row16_sum(q);
           qv[c][e] = q;
         }
       float stot = 0.f;
@@ -244,8 +238,8 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
         float q = 0.f;
 #pragma unroll
         for (int w = 0; w < NW; ++w) q += red[w * 64 + tid];
-        a.stats[(long)(n0 + tid) * a.stats_ld + sp] = stot;
-        a.stats[((long)a.Ng + n0 + tid) * a.stats_ld + sp] = q;
+        a.stats[(long)sp * 2 * a.Ng + n0 + tid] = stot;
+        a.stats[(long)sp * 2 * a.Ng + a.Ng + n0 + tid] = q;
       }
     }
     // output stores last: exactly FP*FC buffer stores per wave after the next tile's DMA

@@ -29,17 +29,19 @@ __global__ void bn_finalize_kernel(const float* part, int C, int G, long M, int 
                                    float eps, float* mean_out, float* invstd_out, float* scale, float* shift) {
   __shared__ double sc[16];
   const int c = blockIdx.x;
-  const float* s = part + (long)c * G;
-  const float* q = part + ((long)C + c) * G;
+  // part: [G][2][C] (row tile g: column sums, then M2 about the tile mean)
+  const float* s = part + c;
+  const float* q = part + C + c;
+  const long st = 2L * C;
   double tsum = 0.0;
-  for (int g = threadIdx.x; g < G; g += blockDim.x) tsum += s[g];
+  for (int g = threadIdx.x; g < G; g += blockDim.x) tsum += s[g * st];
   tsum = block_sum(tsum, sc);
   const double mean = tsum / (double)M;
   double m2 = 0.0;
   for (int g = threadIdx.x; g < G; g += blockDim.x) {
     const long cnt = min((long)tile, M - (long)g * tile);
-    const double mg = (double)s[g] / (double)cnt;
-    m2 += (double)q[g] + (double)cnt * (mg - mean) * (mg - mean);
+    const double mg = (double)s[g * st] / (double)cnt;
+    m2 += (double)q[g * st] + (double)cnt * (mg - mean) * (mg - mean);
   }
   m2 = block_sum(m2, sc);
   if (threadIdx.x == 0) {
@@ -82,7 +84,7 @@ __global__ void bn_apply_kernel(const T* y, int ldy, const float* sc, const floa
     float v[V], rv[V];
     load_vec(y + pix * ldy + c0, v);
 #pragma unroll
-    for (int e = 0; e < V; ++e) v[e] = v[e] * sc[c0 + e] + sh[c0 + e];
+    for (int e = 0; e < V; ++e) v[e] = fmaf(v[e], sc[c0 + e], sh[c0 + e]);  // == bwd mask recompute
     if (res_mode) {
       load_vec(r + pix * ldr + c0, rv);
       if (res_mode == 2) {
@@ -106,8 +108,8 @@ __global__ void bn_apply_kernel(const T* y, int ldy, const float* sc, const floa
 // Block = tv channel-vectors x rows pixels; grid = (pixel tiles, channel groups).
 // ------------------------------------------------------------------------------------------
 template <typename T>
-__global__ void bn_bwd_reduce_kernel(const T* dA, int ldd, const T* A, int lda, const T* y1, int ld1,
-                                     const float* mean1, const float* inv1, const T* y2, int ld2,
+__global__ void bn_bwd_reduce_kernel(const T* dA, int ldd, const T* A, int lda, const float* msc, const float* msh,
+                                     const T* y1, int ld1, const float* mean1, const float* inv1, const T* y2, int ld2,
                                      const float* mean2, const float* inv2, long M, int C, int tv, int pix_per_block,
                                      float* part, int G) {
   constexpr int V = VE<T>;
@@ -116,7 +118,7 @@ __global__ void bn_bwd_reduce_kernel(const T* dA, int ldd, const T* A, int lda, 
   const int c0 = (blockIdx.y * tv + tx) * V;
   const long p0 = (long)blockIdx.x * pix_per_block;
   const long p1 = min(M, p0 + pix_per_block);
-  float s0[V], s1[V], s2[V], m1[V], i1[V], m2v[V], i2v[V];
+  float s0[V], s1[V], s2[V], m1[V], i1[V], m2v[V], i2v[V], ms[V], mh[V];
 #pragma unroll
   for (int e = 0; e < V; ++e) {
     s0[e] = s1[e] = s2[e] = 0.f;
@@ -124,16 +126,21 @@ __global__ void bn_bwd_reduce_kernel(const T* dA, int ldd, const T* A, int lda, 
     i1[e] = inv1[c0 + e];
     m2v[e] = y2 ? mean2[c0 + e] : 0.f;
     i2v[e] = y2 ? inv2[c0 + e] : 0.f;
+    ms[e] = msc ? msc[c0 + e] : 0.f;
+    mh[e] = msc ? msh[c0 + e] : 0.f;
   }
   for (long p = p0 + ty; p < p1; p += rows) {
     float d[V], a[V], x[V];
     load_vec(dA + p * ldd + c0, d);
+    load_vec(y1 + p * ld1 + c0, x);
     if (A) {
       load_vec(A + p * lda + c0, a);
 #pragma unroll
       for (int e = 0; e < V; ++e) d[e] = a[e] > 0.f ? d[e] : 0.f;
+    } else if (msc) {  // ReLU mask recomputed from y1 exactly as bn_apply produced A
+#pragma unroll
+      for (int e = 0; e < V; ++e) d[e] = fmaf(x[e], ms[e], mh[e]) > 0.f ? d[e] : 0.f;
     }
-    load_vec(y1 + p * ld1 + c0, x);
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       s0[e] += d[e];
@@ -204,7 +211,8 @@ __global__ void bn_bwd_finalize_kernel(const float* part, int C, int G, long M, 
 
 // pass 3: dy_b = coef_a*(dz - mean(dz) - xhat_b*mean(dz*xhat_b)); optional dzout (+)= dz
 template <typename T>
-__global__ void bn_bwd_apply_kernel(const T* dA, int ldd, const T* A, int lda, const T* y1, int ld1,
+__global__ void bn_bwd_apply_kernel(const T* dA, int ldd, const T* A, int lda, const float* msc, const float* msh,
+                                    const T* y1, int ld1,
                                     const float* mean1, const float* inv1, T* dy1, int ldo1, const T* y2, int ld2,
                                     const float* mean2, const float* inv2, T* dy2, int ldo2, const float* coef,
                                     T* dzout, int ldz, int dz_acc, long M, int C) {
@@ -216,12 +224,15 @@ __global__ void bn_bwd_apply_kernel(const T* dA, int ldd, const T* A, int lda, c
     const int c0 = (int)(i - pix * cv) * V;
     float d[V], a[V], x[V], o[V];
     load_vec(dA + pix * ldd + c0, d);
+    load_vec(y1 + pix * ld1 + c0, x);
     if (A) {
       load_vec(A + pix * lda + c0, a);
 #pragma unroll
       for (int e = 0; e < V; ++e) d[e] = a[e] > 0.f ? d[e] : 0.f;
+    } else if (msc) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) d[e] = fmaf(x[e], msc[c0 + e], msh[c0 + e]) > 0.f ? d[e] : 0.f;
     }
-    load_vec(y1 + pix * ld1 + c0, x);
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       const int c = c0 + e;
@@ -525,7 +536,7 @@ __global__ void pack_input_kernel(const float* x, int N, int C, int H, int W, in
 // ------------------------------------------------------------------------------------------
 // 1x1 conv with tiny Cout (final 64->2, seg_head 64->1, attention psi inter->1).
 // Forward: one wave per 64/ (C/V) pixels; output fp32 planar [N][K][HW] (== [M] for K=1);
-// optional BN partial stats of channel 0 per block (for psi: [2][1][G], tile = pixels/block).
+// optional BN partial stats of channel 0 per block (for psi: [G][2][1], tile = pixels/block).
 // ------------------------------------------------------------------------------------------
 template <typename T, int K>
 __global__ void pw_small_fwd_kernel(const T* x, int ldx, long M, int HW, int C, const float* w, const float* b,
@@ -584,8 +595,8 @@ __global__ void pw_small_fwd_kernel(const T* x, int ldx, long M, int HW, int C, 
   }
   const double m2 = block_sum(lm2, sred);
   if (threadIdx.x == 0) {
-    stats[blockIdx.x] = (float)tot;
-    stats[gridDim.x + blockIdx.x] = (float)m2;
+    stats[2 * blockIdx.x] = (float)tot;  // [G][2][1]
+    stats[2 * blockIdx.x + 1] = (float)m2;
   }
 }
 
@@ -899,10 +910,10 @@ UNETSEG_API int unetseg_reduce_tiles(int dtype, long M, int C, int* tv_out, int*
   return ceil_div(M, ppb);
 }
 
-UNETSEG_API int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const void* A, int lda, const void* y1,
-                                      int ld1, const float* mean1, const float* inv1, const void* y2, int ld2,
-                                      const float* mean2, const float* inv2, long M, int C, float* part, int G,
-                                      void* stream) {
+UNETSEG_API int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const void* A, int lda, const float* msc,
+                                      const float* msh, const void* y1, int ld1, const float* mean1,
+                                      const float* inv1, const void* y2, int ld2, const float* mean2,
+                                      const float* inv2, long M, int C, float* part, int G, void* stream) {
   CHECK_VEC(dtype, C, "bn_bwd_reduce");
   int tv, ppb;
   const int g = unetseg_reduce_tiles(dtype, M, C, &tv, &ppb);
@@ -910,8 +921,8 @@ UNETSEG_API int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const 
   const int V = dtype == DT_BF16 ? 8 : 4;
   dim3 grid(G, C / V / tv);
   DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)dA,
-                                       ldd, (const T*)A, lda, (const T*)y1, ld1, mean1, inv1, (const T*)y2, ld2, mean2,
-                                       inv2, M, C, tv, ppb, part, G));
+                                       ldd, (const T*)A, lda, msc, msh, (const T*)y1, ld1, mean1, inv1, (const T*)y2,
+                                       ld2, mean2, inv2, M, C, tv, ppb, part, G));
   US_LAUNCH_CHECK("bn_bwd_reduce");
   return 0;
 }
@@ -925,15 +936,16 @@ UNETSEG_API int unetseg_bn_bwd_finalize(const float* part, int C, int G, long M,
   return 0;
 }
 
-UNETSEG_API int unetseg_bn_bwd_apply(int dtype, const void* dA, int ldd, const void* A, int lda, const void* y1,
-                                     int ld1, const float* mean1, const float* inv1, void* dy1, int ldo1,
+UNETSEG_API int unetseg_bn_bwd_apply(int dtype, const void* dA, int ldd, const void* A, int lda, const float* msc,
+                                     const float* msh, const void* y1, int ld1, const float* mean1, const float* inv1,
+                                     void* dy1, int ldo1,
                                      const void* y2, int ld2, const float* mean2, const float* inv2, void* dy2,
                                      int ldo2, const float* coef, void* dzout, int ldz, int dz_acc, long M, int C,
                                      void* stream) {
   CHECK_VEC(dtype, C, "bn_bwd_apply");
   DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(M * C / VE<T>)), dim3(256), 0,
-                                       (hipStream_t)stream, (const T*)dA, ldd, (const T*)A, lda, (const T*)y1, ld1,
-                                       mean1, inv1, (T*)dy1, ldo1, (const T*)y2, ld2, mean2, inv2, (T*)dy2, ldo2, coef,
+                                       (hipStream_t)stream, (const T*)dA, ldd, (const T*)A, lda, msc, msh,
+                                       (const T*)y1, ld1, mean1, inv1, (T*)dy1, ldo1, (const T*)y2, ld2, mean2, inv2, (T*)dy2, ldo2, coef,
                                        (T*)dzout, ldz, dz_acc, M, C));
   US_LAUNCH_CHECK("bn_bwd_apply");
   return 0;
@@ -1021,7 +1033,7 @@ UNETSEG_API int unetseg_pack_input(int dtype, const float* x, int n, int c, int 
 
 UNETSEG_API int unetseg_pw_small_tiles(long M) { return ceil_div(M, 2048); }
 
-// y fp32 planar [n][k][hw]; stats (k==1 only, may be NULL): [2][G], G = unetseg_pw_small_tiles(M), tile 2048 px
+// y fp32 planar [n][k][hw]; stats (k==1 only, may be NULL): [G][2], G = unetseg_pw_small_tiles(M), tile 2048 px
 UNETSEG_API int unetseg_pw_small_fwd(int dtype, const void* x, int ldx, long M, int hw, int c, int k, const float* w,
                                      const float* b, float* y, float* stats, void* stream) {
   CHECK_VEC(dtype, c, "pw_small_fwd");

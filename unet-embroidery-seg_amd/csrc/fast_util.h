@@ -37,4 +37,15 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 __device__ __forceinline__ int swz_tr16(int row) { return ((row & 3) | ((row >> 1) & 4)) << 1; }
 __device__ __forceinline__ int swz_tr8(int row) { return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1; }
 
+// Sum over the 16 lanes of a DPP row (lanes 16r .. 16r+15), result in every lane of the row:
+// four row rotations on the VALU.  __shfl_xor goes through ds_bpermute (an LDS round trip per
+// step); in the conv epilogues that cost as much as the whole store phase.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x122, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x121, 0xF, 0xF, false));
+  return v;
+}
+
 }  // namespace

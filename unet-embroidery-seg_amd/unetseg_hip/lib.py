@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libunetseg_hip.so")
+LIB_PATH = os.environ.get("UNETSEG_LIB_PATH") or os.path.join(_HERE, "libunetseg_hip.so")  # override: A/B builds
 
 DT_F32, DT_BF16 = 0, 1
 
@@ -37,9 +37,9 @@ SIGNATURES = {
     "unetseg_bn_eval_coeffs": (I, [I, P, P, P, P, F, P, P, P]),
     "unetseg_bn_apply": (I, [I, P, I, P, P, P, I, P, P, I, I, P, I, L, I, P]),
     "unetseg_reduce_tiles": (I, [I, L, I, P, P]),
-    "unetseg_bn_bwd_reduce": (I, [I, P, I, P, I, P, I, P, P, P, I, P, P, L, I, P, I, P]),
+    "unetseg_bn_bwd_reduce": (I, [I, P, I, P, I, P, P, P, I, P, P, P, I, P, P, L, I, P, I, P]),
     "unetseg_bn_bwd_finalize": (I, [P, I, I, L, I, P, P, P, P, P, P, P, P, P, P]),
-    "unetseg_bn_bwd_apply": (I, [I, P, I, P, I, P, I, P, P, P, I, P, I, P, P, P, I, P, P, I, I, L, I, P]),
+    "unetseg_bn_bwd_apply": (I, [I, P, I, P, I, P, P, P, I, P, P, P, I, P, I, P, P, P, I, P, P, I, I, L, I, P]),
     "unetseg_relu_bwd_bias": (I, [I, P, I, P, I, P, I, L, I, P, I, P]),
     "unetseg_colsum_finalize": (I, [P, I, I, P, I, P]),
     "unetseg_maxpool_fwd": (I, [I, P, I, I, I, I, I, I, I, I, P, I, P, P, P, P]),

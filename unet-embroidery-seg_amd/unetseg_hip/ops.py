@@ -220,7 +220,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
     st = None
     if stats:
         tile = lib.conv2d_fwd_tile_m(ctx.dt, C1, ldp(X1), C2, ldp(X2), N, H, W, K, R, S, stride, pad)
-        st = (ctx.f32(2, K, math.ceil(M / tile)), tile)
+        st = (ctx.f32(math.ceil(M / tile), 2, K), tile)  # [row tiles][sum, M2][K]
     b = pc.conv.bias
     flops = 2.0 * M * K * pc.C * R * S  # algorithmic (unpadded Cin)
     desc = (N, H, W, C1, C2, K, R, S, stride)
@@ -278,7 +278,7 @@ class BNState:
 
 
 def _bn_coeffs(ctx, bn, st, M, tile=None):
-    """st: (partials [2][C][G], row tile) from conv(), or a bare partials tensor with `tile` given"""
+    """st: (partials [G][2][C], row tile) from conv(), or a bare partials tensor with `tile` given"""
     if isinstance(st, tuple):
         st, tile = st
     C = bn.weight.shape[0]
@@ -286,7 +286,7 @@ def _bn_coeffs(ctx, bn, st, M, tile=None):
     s.sc, s.sh = ctx.f32(C), ctx.f32(C)
     if ctx.training:
         s.mean, s.inv = ctx.f32(C), ctx.f32(C)
-        G = st.shape[-1]
+        G = st.shape[0]
         lib.bn_finalize(P(st), C, G, M, tile, P(bn.weight), P(bn.bias), P(bn.running_mean), P(bn.running_var),
                         P(bn.num_batches_tracked), bn.momentum, bn.eps, P(s.mean), P(s.inv), P(s.sc), P(s.sh),
                         ctx.stream)
@@ -325,7 +325,11 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None):
         part = ctx.f32(3, C, Gr)
         y2 = res_bn[0] if res_bn is not None else None
         Y2 = y2.data if y2 is not None else None
-        lib.bn_bwd_reduce(ctx.dt, P(dA), ldp(dA), P(a) if relu else 0, C, P(Y), ldp(Y), P(s1.mean), P(s1.inv),
+        # plain BN-ReLU: the mask is recomputed from y (no read of the activation)
+        plain = relu and res is None and res_bn is None
+        mA = 0 if (plain or not relu) else P(a)
+        msc, msh = (P(s1.sc), P(s1.sh)) if plain else (0, 0)
+        lib.bn_bwd_reduce(ctx.dt, P(dA), ldp(dA), mA, C, msc, msh, P(Y), ldp(Y), P(s1.mean), P(s1.inv),
                           P(Y2), ldp(Y2), P(s2.mean if s2 else None), P(s2.inv if s2 else None), M, C, P(part), Gr,
                           ctx.stream)
         coef = ctx.f32(6, C)
@@ -346,7 +350,7 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None):
         dz, dzacc = None, 0
         if res is not None and res.need_grad:
             dz, dzacc = gbuf(ctx, res)
-        lib.bn_bwd_apply(ctx.dt, P(dA), ldp(dA), P(a) if relu else 0, C, P(Y), ldp(Y), P(s1.mean), P(s1.inv),
+        lib.bn_bwd_apply(ctx.dt, P(dA), ldp(dA), mA, C, msc, msh, P(Y), ldp(Y), P(s1.mean), P(s1.inv),
                          P(dy1), ldp(dy1), P(Y2), ldp(Y2), P(s2.mean if s2 else None), P(s2.inv if s2 else None),
                          P(dy2), ldp(dy2), P(coef), P(dz), ldp(dz), dzacc, M, C, ctx.stream)
 
@@ -441,7 +445,7 @@ def attention_gate(ctx, skip, gate, gm, pth, pph):
     psi_conv, psi_bn = gm.psi[0], gm.psi[1]
     psi = ctx.f32(M)
     G = lib.pw_small_tiles(M)
-    pst = ctx.f32(2, 1, G)
+    pst = ctx.f32(G, 2, 1)
     lib.pw_small_fwd(ctx.dt, P(F_), ldp(F_), M, M, Ci, 1, P(psi_conv.weight), P(psi_conv.bias), P(psi),
                      P(pst) if ctx.training else 0, ctx.stream)
     s = _bn_coeffs(ctx, psi_bn, pst, M, PW_TILE)
