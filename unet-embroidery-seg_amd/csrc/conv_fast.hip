@@ -25,6 +25,8 @@ namespace {
 // ------------------------------------------------------------------------------------------
 // TN (fwd / dgrad).  Tile: BM pixels x BN output channels, K step 64 channels of one tap.
 // ------------------------------------------------------------------------------------------
+// ST: 1 = a single K step, 2 = global loads one K step ahead, 3 = two steps ahead (two register
+// sets; only where the registers fit at two waves per SIMD)
 template <int BM, int BN, int NWM, int NWN, int ST>
 __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
   constexpr int NT = 64 * NWM * NWN;
@@ -79,10 +81,12 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
 
   const int nch = a.cin >> 6;
   const int nsteps = a.nr * a.ns * nch;
-  uint4 ra[A_PER], rbv[B_PER];
+  // two register sets: the loads of K step kt+2 are issued while step kt is computed and
+  // step kt+1's registers are written to LDS, so each load has two steps of MFMA to land
+  uint4 ra0[A_PER], rb0[B_PER], ra1[A_PER], rb1[B_PER];
   // scalar K-step state
   int s_jr = 0, s_js = 0, s_c = 0;
-  auto gload = [&]() {
+  auto gload = [&](uint4 (&ra)[A_PER], uint4 (&rbv)[B_PER]) {
     const int dh = a.dh0 + a.dhs * s_jr, dw = a.dw0 + a.dws * s_js;
     const int tapbit = s_jr * a.ns + s_js;
     const int tapdelta = dh * a.W + dw;
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
       if (++s_js == a.ns) { s_js = 0; ++s_jr; }
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const uint4 (&ra)[A_PER], const uint4 (&rbv)[B_PER]) {
     uint4* L = lds + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
@@ -132,15 +136,8 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
 #pragma unroll
     for (int p = 0; p < FP; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nsteps > 0) {
-    gload();
-    sstore(0);
-    __syncthreads();
-  }
-  for (int kt = 0; kt < nsteps; ++kt) {
-    const int cur = kt & 1;
-    if (ST > 1 && kt + 1 < nsteps) gload();
-    const uint4* As = lds + (ST > 1 ? cur : 0) * STAGE;
+  auto compute = [&](int buf) {
+    const uint4* As = lds + buf * STAGE;
     const uint4* Bs = As + BM * 8;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -164,8 +161,49 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
         for (int p = 0; p < FP; ++p)
           acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], pf[p], acc[c][p], 0, 0, 0);
     }
-    if (ST > 1 && kt + 1 < nsteps) sstore(cur ^ 1);
+  };
+
+  if (ST == 1) {  // one K step
+    if (nsteps > 0) {
+      gload(ra0, rb0);
+      sstore(0, ra0, rb0);
+      __syncthreads();
+      compute(0);
+    }
     __syncthreads();
+  } else if (ST == 2) {  // loads one step ahead (one register set)
+    if (nsteps > 0) {
+      gload(ra0, rb0);
+      sstore(0, ra0, rb0);
+      __syncthreads();
+    }
+    for (int kt = 0; kt < nsteps; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nsteps) gload(ra0, rb0);
+      compute(cur);
+      if (kt + 1 < nsteps) sstore(cur ^ 1, ra0, rb0);
+      __syncthreads();
+    }
+  } else {  // ST == 3: loads two steps ahead (two register sets)
+    if (nsteps > 0) {
+      gload(ra0, rb0);
+      sstore(0, ra0, rb0);
+      if (nsteps > 1) gload(ra1, rb1);
+      __syncthreads();
+    }
+    for (int kt = 0; kt < nsteps; kt += 2) {
+      // even step: stage 0 holds kt, registers 1 hold kt+1 (in flight)
+      if (kt + 2 < nsteps) gload(ra0, rb0);
+      compute(0);
+      if (kt + 1 < nsteps) sstore(1, ra1, rb1);
+      __syncthreads();
+      if (kt + 1 >= nsteps) break;
+      // odd step: stage 1 holds kt+1, registers 0 hold kt+2 (in flight)
+      if (kt + 3 < nsteps) gload(ra1, rb1);
+      compute(1);
+      if (kt + 2 < nsteps) sstore(0, ra0, rb0);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: lane holds D[cout = (lane>>4)*4 + e][pixel = lane&15] per (c, p) subtile ----
@@ -457,7 +495,7 @@ template <int BM, int BN, int NWM, int NWN, int ST>
 int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   constexpr int NT = 64 * NWM * NWN;
   // operand stages, or the epilogue's per-wave transpose tiles + stats scratch if larger
-  const size_t stages = (size_t)ST * (BM + BN) * 8 * 16;
+  const size_t stages = (size_t)(ST == 1 ? 1 : 2) * (BM + BN) * 8 * 16;
   const size_t epi = (size_t)NWM * NWN * 64 * ((BN / NWN) * 2 + 16) + 2 * NWM * BN * 4;
   const size_t lds = stages > epi ? stages : epi;
   static bool attr = false;
@@ -501,7 +539,7 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
   switch (tn_config(a)) {
     case 0: return launch_halo3(a, st);
     case 1: return launch_tn_cfg<256, 64, 4, 1, 2>(a, st);
-    case 2: return launch_tn_cfg<256, 128, 4, 2, 2>(a, st);
+    case 2: return launch_tn_cfg<256, 128, 4, 2, 3>(a, st);
     case 4: return launch_tn_cfg<128, 128, 2, 2, 1>(a, st);
     default: return launch_tn_cfg<128, 128, 2, 2, 2>(a, st);
   }

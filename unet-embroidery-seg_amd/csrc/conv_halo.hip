@@ -25,6 +25,10 @@ namespace {
 
 constexpr int HW_TW = 32;  // output tile width (pixels)
 
+// Halo pixel rows are read 16 at a time from an arbitrary start (the tap shift); XOR the chunk
+// with hp & 7 (not (hp>>1) & 7 as for aligned rows): conflict-free ds_read_b128 for every start.
+__device__ __forceinline__ int swzh(int hp, int ch) { return ch ^ (hp & 7); }
+
 __device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, unsigned off, uint2 v) {
   asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
 }
@@ -100,7 +104,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
       const int hp = hr * (HW_TW + 2) + hc;
       const int pc = lane & 7;
       const bool ok = v >= 0 && gh >= 0 && gh < a.H && gw >= 0 && gw < a.W;
-      const unsigned off = ok ? (unsigned)((nb * a.H + gh) * a.W + gw) * (unsigned)a.ldc1b + swz8(hp, pc) * 16u : kOOB;
+      const unsigned off = ok ? (unsigned)((nb * a.H + gh) * a.W + gw) * (unsigned)a.ldc1b + swzh(hp, pc) * 16u : kOOB;
       if (v >= 0 || HCH % (64 * NW) == 0) dma16(rx, base + (unsigned)((i * NW + wid) * 1024), off);
     }
   };
@@ -140,7 +144,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
           const int r = wid * RPW + p / (HW_TW / 16);
           const int col = (p % (HW_TW / 16)) * 16 + j16;
           const int hp = (r + 1 + dh) * (HW_TW + 2) + col + 1 + dw;
-          uint4 v = hs[hp * 8 + swz8(hp, ch)];
+          uint4 v = hs[hp * 8 + swzh(hp, ch)];
           pf[p] = *reinterpret_cast<bf16x8*>(&v);
         }
 #pragma unroll
@@ -445,13 +449,25 @@ bool halo3_wgrad_ok(const HaloWgradArgs& a) {
   return a.cin % 64 == 0 && a.c1 % 64 == 0 && a.Cout % 64 == 0 && a.H % 8 == 0 && a.W % HW_TW == 0;
 }
 
+// Blocks per (cout, cin) group: one persistent block per CU at a time (152 KiB LDS), so the
+// makespan is ceil(groups*G / 256) rounds of ceil(n_sp / G) tiles, plus the split-K reduce that
+// reads G slabs.  Pick the G that minimises that estimate (tile ~2 us, reduce ~4 TB/s).
 int halo3_wgrad_splits(const HaloWgradArgs& a) {
   const int groups = (a.Cout / 64) * (a.cin / 64);
   const int n_sp = a.N * (a.H / 8) * (a.W / HW_TW);
-  int g = 256 / groups;
-  if (g < 1) g = 1;
-  if (g > n_sp) g = n_sp;
-  return g;
+  const double slab = 4.0 * a.Cout * 9.0 * a.cin;
+  int best = 1;
+  double best_t = 1e30;
+  for (int g = 1; g <= 512 && g <= n_sp; ++g) {
+    if (slab * g > 768.0 * (1 << 20)) break;  // workspace cap
+    const double rounds = (double)((groups * g + 255) / 256);
+    const double t = rounds * ((n_sp + g - 1) / g) * 2e-6 + slab * g / 4e12;
+    if (t < best_t * 0.999) {
+      best_t = t;
+      best = g;
+    }
+  }
+  return best;
 }
 
 int launch_halo3_wgrad(const HaloWgradArgs& a, int G_per, hipStream_t st) {
