@@ -102,7 +102,7 @@ def main():
     from model.model_factory import create_model
     from unetseg_hip import ops
     from unetseg_hip.arena import FusedAdam
-    from unetseg_hip.losses import binary_segmentation_loss
+    from unetseg_hip.losses import binary_segmentation_loss, multitask_loss
     from utils.synthetic import make_batch
 
     kw = dict(num_classes=1) if args.model == "multitask_unet" else dict(num_classes=2)
@@ -111,17 +111,21 @@ def main():
     buckets = GradBuckets(model) if world > 1 else None
     opt = FusedAdam(model, lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4)
     nbatches = 2
+    multitask = args.model == "multitask_unet"
     data = []
     for i in range(nbatches):
-        x, y = make_batch(args.batch, args.size, seed=1234 + 100000 * rank + i)
-        data.append((x.to(dev), y.to(dev)))
+        x, y, c = make_batch(args.batch, args.size, seed=1234 + 100000 * rank + i, with_cls=True)
+        data.append((x.to(dev), y.to(dev), c.to(dev)))
 
     def step(i):
-        x, y = data[i % nbatches]
+        x, y, c = data[i % nbatches]
         opt.zero_grad()
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            out = model(x)
-            loss = binary_segmentation_loss(out, y, args.loss)
+            if multitask:  # seg BCE/Lovasz + 1.0 * CE (train.py:213-219 defaults)
+                seg, cls = model(x)
+                loss = multitask_loss(seg, cls, y, c, 1.0, args.loss)[0]
+            else:
+                loss = binary_segmentation_loss(model(x), y, args.loss)
         loss.backward()
         opt.step()
         return loss
@@ -152,7 +156,8 @@ def main():
     imgs_per_s = args.batch * world * args.steps / wall
     final_loss = float(loss.item())
 
-    workload = f"{args.model} binary seg {args.size}x{args.size}, per-GPU batch {args.batch}, {args.loss} + Adam"
+    task = "seg+cls multitask" if multitask else "binary seg"
+    workload = f"{args.model} {task} {args.size}x{args.size}, per-GPU batch {args.batch}, {args.loss} + Adam"
     roof = None
     if args.probe:
         ops.PROBE = []
@@ -178,7 +183,7 @@ def main():
                                 "launches": v[2]} for k, v in kinds.items()}}
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_baseline:
+    if rank == 0 and world == 1 and args.cpu_baseline and not multitask:
         cpu = cpu_baseline(args.model, args.size, args.cpu_batch)
 
     if rank == 0:

@@ -76,6 +76,8 @@ CONV_CASES = [
     (1, 24, 32, 192, 0, 64, 3, 1, 1, False, False),
     # one K step (64 input channels, 1x1): single-stage 128x128 TN configuration
     (2, 16, 24, 64, 0, 256, 1, 1, 0, False, False),
+    # small M, long K: 64-row tiles
+    (1, 8, 8, 320, 0, 256, 3, 1, 1, True, True),
 ]
 
 

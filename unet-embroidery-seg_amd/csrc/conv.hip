@@ -716,7 +716,8 @@ static int wgrad_splits(int Cout, int Ng, long Kpix, int bkw) {
 }
 
 static bool wgrad_fast_eligible(int dtype, int q, int cin, int cout) {
-  return dtype == DT_BF16 && !getenv("UNETSEG_NO_FAST") && q % 32 == 0 && cin % 8 == 0 && cout % 64 == 0;
+  (void)q;
+  return dtype == DT_BF16 && !getenv("UNETSEG_NO_FAST") && cin % 8 == 0 && cout % 64 == 0;
 }
 
 // shape test of the halo wgrad path (3x3, stride 1, pad 1, output grid == input grid)

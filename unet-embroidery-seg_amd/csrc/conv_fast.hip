@@ -332,17 +332,22 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
 
 // ------------------------------------------------------------------------------------------
 // wgrad: C[cout][(tap, c)] = sum_pix dY[pix][cout] * X[n][p*st+dh][q*st+dw][c];
-// tile BM couts x BN (tap,c) columns, K step = 32 pixels of one image row.
+// tile BM couts x BN (tap,c) columns, K step = kWgBK consecutive output pixels.  Each thread
+// tracks (image, row, col) of the pixels it stages and advances them by one step at a time, so
+// any output width works.
 // ------------------------------------------------------------------------------------------
+constexpr int kWgBK = 32;  // 64 halves the barriers but costs a wave per SIMD: slower here
+
 template <int BM, int BN, int NWM, int NWN>
 __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArgs a) {
   constexpr int NT = 64 * NWM * NWN;
-  constexpr int BKW = 32;
+  constexpr int BKW = kWgBK;
   constexpr int CPA = BM / 8, CPB = BN / 8;  // 16-B chunks per LDS row
   constexpr int A_PER = BKW * CPA / NT, B_PER = BKW * CPB / NT;
   constexpr int WTM = BM / NWM, WTN = BN / NWN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
-  __shared__ __attribute__((aligned(16))) uint4 lds[2][BKW * (CPA + CPB)];
+  constexpr int STAGE = BKW * (CPA + CPB);  // uint4
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // [2][STAGE]
   static_assert(A_PER >= 1 && B_PER >= 1, "tile too small for the block");
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -362,9 +367,14 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     a_cv[i] = id % CPA;
     a_row[i] = id / CPA;
   }
-  // B (X) chunk: column fixed -> (tap, c) fixed
+  // B (X) chunk: column fixed -> (tap, c) fixed; row -> a pixel whose (n, p, q) we track
   int b_row[B_PER], b_dh[B_PER], b_dw[B_PER], b_src[B_PER], b_cv[B_PER];
+  int b_n[B_PER], b_p[B_PER], b_q[B_PER];
   unsigned b_cb[B_PER];
+  const long nkt_total = (a.Kpix + BKW - 1) / BKW;
+  const long kt0 = (long)blockIdx.z * a.kt_per_split;
+  const long kt1 = min(nkt_total, kt0 + a.kt_per_split);
+  const int PQ = a.P * a.Q;
 #pragma unroll
   for (int i = 0; i < B_PER; ++i) {
     const int id = tid + NT * i;
@@ -385,19 +395,17 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
       b_src[i] = 0;
       b_cb[i] = 0;
     }
+    const long k = kt0 * BKW + b_row[i];
+    const int nb = (int)(k / PQ), rem = (int)(k - (long)nb * PQ);
+    b_n[i] = nb;
+    b_p[i] = rem / a.Q;
+    b_q[i] = rem - b_p[i] * a.Q;
   }
   const unsigned a_colb0 = (unsigned)m0 * 2u;
-  const long nkt_total = (a.Kpix + BKW - 1) / BKW;
-  const long kt0 = (long)blockIdx.z * a.kt_per_split;
-  const long kt1 = min(nkt_total, kt0 + a.kt_per_split);
-  const int PQ = a.P * a.Q;
 
   uint4 ra[A_PER], rbv[B_PER];
   auto gload = [&](long kt) {
     const long k0 = kt * BKW;  // first pixel of the step (uniform)
-    const int nb = (int)(k0 / PQ);
-    const int rem = (int)(k0 - (long)nb * PQ);
-    const int p = rem / a.Q, q0 = rem - p * a.Q;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const long k = k0 + a_row[i];
@@ -407,28 +415,41 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
-      const int ih = p * a.stride + b_dh[i];
-      const int iw = (q0 + b_row[i]) * a.stride + b_dw[i];
+      const int ih = b_p[i] * a.stride + b_dh[i];
+      const int iw = b_q[i] * a.stride + b_dw[i];
       const bool ok = (k0 + b_row[i]) < a.Kpix && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-      const unsigned pixi = (unsigned)((nb * a.H + ih) * a.W + iw);
+      const unsigned pixi = (unsigned)((b_n[i] * a.H + ih) * a.W + iw);
       if (b_src[i] == 0)
         rbv[i] = bload(r1, ok ? pixi * (unsigned)a.ldc1b + b_cb[i] : kOOB);
       else
         rbv[i] = bload(r2, ok ? pixi * (unsigned)a.ldc2b + b_cb[i] : kOOB);
+      // advance this row's pixel by one K step
+      int q = b_q[i] + BKW, p = b_p[i], nb = b_n[i];
+      while (q >= a.Q) {
+        q -= a.Q;
+        if (++p == a.P) {
+          p = 0;
+          ++nb;
+        }
+      }
+      b_q[i] = q;
+      b_p[i] = p;
+      b_n[i] = nb;
     }
   };
   auto sstore = [&](int buf) {
+    uint4* L = lds + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int row = a_row[i];
       const int sw = CPA >= 16 ? swz_tr16(row) : swz_tr8(row);
-      lds[buf][row * CPA + (a_cv[i] ^ sw)] = ra[i];
+      L[row * CPA + (a_cv[i] ^ sw)] = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int row = b_row[i];
       const int sw = CPB >= 16 ? swz_tr16(row) : swz_tr8(row);
-      lds[buf][BKW * CPA + row * CPB + (b_cv[i] ^ sw)] = rbv[i];
+      L[BKW * CPA + row * CPB + (b_cv[i] ^ sw)] = rbv[i];
     }
   };
 
@@ -448,10 +469,10 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nkt) gload(kt0 + kt + 1);
-    const char* base = reinterpret_cast<const char*>(&lds[cur][0]);
-    auto trfrag = [&](int off_bytes, int cpr, int col0) -> bf16x8 {
+    const char* base = reinterpret_cast<const char*>(lds + cur * STAGE);
+    auto trfrag = [&](int off_bytes, int cpr, int col0, int r0) -> bf16x8 {
       const int chunk = (col0 >> 3) + (pp >> 1);
-      const int ra_ = 8 * g + qq, rb_ = 8 * g + qq + 4;
+      const int ra_ = r0 + 8 * g + qq, rb_ = r0 + 8 * g + qq + 4;
       const int swa = cpr >= 16 ? swz_tr16(ra_) : swz_tr8(ra_);
       const int swb = cpr >= 16 ? swz_tr16(rb_) : swz_tr8(rb_);
       const char* pa = base + off_bytes + ra_ * (cpr * 16) + ((chunk ^ swa) * 16) + (pp & 1) * 8;
@@ -462,16 +483,19 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
       s16x8 v = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
       return *reinterpret_cast<bf16x8*>(&v);
     };
-    bf16x8 af[FM], bfr[FN];
 #pragma unroll
-    for (int i = 0; i < FM; ++i) af[i] = trfrag(0, CPA, wm * WTM + i * 16);
+    for (int kk = 0; kk < BKW / 32; ++kk) {
+      bf16x8 af[FM], bfr[FN];
 #pragma unroll
-    for (int j = 0; j < FN; ++j) bfr[j] = trfrag(BKW * CPA * 16, CPB, wn * WTN + j * 16);
+      for (int i = 0; i < FM; ++i) af[i] = trfrag(0, CPA, wm * WTM + i * 16, kk * 32);
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int j = 0; j < FN; ++j) bfr[j] = trfrag(BKW * CPA * 16, CPB, wn * WTN + j * 16, kk * 32);
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
     if (kt + 1 < nkt) sstore(cur ^ 1);
     __syncthreads();
   }
@@ -510,7 +534,7 @@ int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
 }
 
 // TN configuration: 0 = halo, 1 = 256x64, 2 = 256x128, 3 = 128x128, 4 = 128x128 single stage
-// (one K step: the prefetch stage would only cost occupancy)
+// (one K step: the prefetch stage would only cost occupancy), 5 = 64x128
 static int tn_config(const FastTNArgs& a) {
   if (halo3_ok(a)) return 0;
   const int nsteps = a.nr * a.ns * (a.cin >> 6);
@@ -518,7 +542,9 @@ static int tn_config(const FastTNArgs& a) {
   if (a.Ng <= 64) return 1;
   if (nsteps <= 4) return 3;
   const long tiles_big = (long)ceil_div(a.M, 256) * ceil_div(a.Ng, 128);
-  return tiles_big >= 256 ? 2 : 3;
+  if (tiles_big >= 256) return 2;
+  const long tiles_mid = (long)ceil_div(a.M, 128) * ceil_div(a.Ng, 128);
+  return tiles_mid >= 256 ? 3 : 5;  // 5: 64-row tiles so that small-M layers still fill the chip
 }
 
 }  // namespace
@@ -531,7 +557,7 @@ bool tn_fast_ok(const FastTNArgs& a) {
 // spatial tile on the halo kernel.
 int tn_fast_tile_m(const FastTNArgs& a) {
   const int cfg = tn_config(a);
-  return cfg == 0 ? halo_tile_m() : (cfg <= 2 ? 256 : 128);
+  return cfg == 0 ? halo_tile_m() : cfg <= 2 ? 256 : cfg == 5 ? 64 : 128;
 }
 
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
@@ -541,19 +567,20 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 1: return launch_tn_cfg<256, 64, 4, 1, 2>(a, st);
     case 2: return launch_tn_cfg<256, 128, 4, 2, 3>(a, st);
     case 4: return launch_tn_cfg<128, 128, 2, 2, 1>(a, st);
+    case 5: return launch_tn_cfg<64, 128, 1, 4, 2>(a, st);
     default: return launch_tn_cfg<128, 128, 2, 2, 2>(a, st);
   }
 }
 
 bool wgrad_fast_ok(const FastWgradArgs& a) {
-  return a.Q % 32 == 0 && a.cin % 8 == 0 && a.c1 % 8 == 0 && a.Cout % 64 == 0;
+  return a.cin % 8 == 0 && a.c1 % 8 == 0 && a.Cout % 64 == 0;
 }
 
 int wgrad_fast_splits(int Cout, int Ng, long Kpix) {
   const int bm = Cout <= 64 ? 64 : 128;
   const int bn = Cout <= 64 ? 256 : 128;
   const int tiles = ceil_div(Cout, bm) * ceil_div(Ng, bn);
-  const long nkt = (Kpix + 31) / 32;
+  const long nkt = (Kpix + kWgBK - 1) / kWgBK;
   int sp = ceil_div(Cout <= 64 ? 1024 : 512, tiles);  // 2-4 blocks per CU
   const long max_sp = nkt / 32 > 0 ? nkt / 32 : 1;  // >= 32 K steps per split
   if (sp > max_sp) sp = (int)max_sp;
@@ -562,15 +589,25 @@ int wgrad_fast_splits(int Cout, int Ng, long Kpix) {
   return sp;
 }
 
-int launch_wgrad_fast(FastWgradArgs a, int splits, hipStream_t st) {
-  const long nkt = (a.Kpix + 31) / 32;
-  a.kt_per_split = (int)((nkt + splits - 1) / splits);
-  if (a.Cout <= 64) {
-    dim3 grid(ceil_div(a.Cout, 64), ceil_div(a.Ng, 256), splits);
-    hipLaunchKernelGGL((wgrad_fast_kernel<64, 256, 1, 4>), grid, dim3(256), 0, st, a);
-  } else {
-    dim3 grid(ceil_div(a.Cout, 128), ceil_div(a.Ng, 128), splits);
-    hipLaunchKernelGGL((wgrad_fast_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, a);
+template <int BM, int BN, int NWM, int NWN>
+static void launch_wgrad_cfg(const FastWgradArgs& a, int splits, hipStream_t st) {
+  const size_t lds = 2 * (size_t)kWgBK * (BM / 8 + BN / 8) * 16;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_fast_kernel<BM, BN, NWM, NWN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
   }
+  dim3 grid(ceil_div(a.Cout, BM), ceil_div(a.Ng, BN), splits);
+  hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN, NWM, NWN>), grid, dim3(64 * NWM * NWN), lds, st, a);
+}
+
+int launch_wgrad_fast(FastWgradArgs a, int splits, hipStream_t st) {
+  const long nkt = (a.Kpix + kWgBK - 1) / kWgBK;
+  a.kt_per_split = (int)((nkt + splits - 1) / splits);
+  if (a.Cout <= 64)
+    launch_wgrad_cfg<64, 256, 1, 4>(a, splits, st);
+  else
+    launch_wgrad_cfg<128, 128, 2, 2>(a, splits, st);
   return 0;
 }
