@@ -495,18 +495,27 @@ __global__ void upsample_bwd_kernel(const T* dy, int ldy, int N, int H, int W, i
     }
     ohl = max(ohl, 0); owl = max(owl, 0);
     ohh = min(ohh, OH - 1); owh = min(owh, OW - 1);
+    // per-axis weights first (<= 6 candidates each for a x2 resize, most zero), then only the
+    // nonzero pairs load
+    float whv[8], wwv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      whv[k] = ohl + k <= ohh ? up_w(ohl + k, h, H, OH, align) : 0.f;
+      wwv[k] = owl + k <= owh ? up_w(owl + k, w, W, OW, align) : 0.f;
+    }
     float acc[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) acc[e] = 0.f;
-    for (int oh = ohl; oh <= ohh; ++oh) {
-      const float wh = up_w(oh, h, H, OH, align);
-      if (wh == 0.f) continue;
-      for (int ow = owl; ow <= owh; ++ow) {
-        const float ww = up_w(ow, w, W, OW, align);
-        if (ww == 0.f) continue;
+#pragma unroll
+    for (int kh = 0; kh < 8; ++kh) {
+      if (whv[kh] == 0.f) continue;
+      const long rowb = (long)(n * OH + ohl + kh) * OW;
+#pragma unroll
+      for (int kw = 0; kw < 8; ++kw) {
+        if (wwv[kw] == 0.f) continue;
         float g[V];
-        load_vec(dy + ((long)(n * OH + oh) * OW + ow) * ldy + c0, g);
-        const float wt = wh * ww;
+        load_vec(dy + (rowb + owl + kw) * ldy + c0, g);
+        const float wt = whv[kh] * wwv[kw];
 #pragma unroll
         for (int e = 0; e < V; ++e) acc[e] += wt * g[e];
       }
