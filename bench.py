@@ -106,7 +106,10 @@ def main():
     from utils.synthetic import make_batch
 
     kw = dict(num_classes=1) if args.model == "multitask_unet" else dict(num_classes=2)
-    model = create_model(args.model, weights="", **kw).to(dev).train()
+    import contextlib
+
+    with contextlib.redirect_stdout(sys.stderr):  # weights_init's banner (reference behaviour) -> stderr
+        model = create_model(args.model, weights="", **kw).to(dev).train()
     model.compute_dtype = "bf16"
     buckets = GradBuckets(model) if world > 1 else None
     opt = FusedAdam(model, lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4)

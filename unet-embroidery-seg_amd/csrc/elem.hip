@@ -103,80 +103,131 @@ __global__ void bn_apply_kernel(const T* y, int ldy, const float* sc, const floa
 }
 
 // ------------------------------------------------------------------------------------------
-// BatchNorm backward, pass 1: per-(channel, pixel tile) partials of
-//   sum dz, sum dz*xhat1, sum dz*xhat2     where dz = dA * (A > 0 if A else 1)
-// Block = tv channel-vectors x rows pixels; grid = (pixel tiles, channel groups).
+// Channel reductions over pixels (BN backward pass 1, ReLU-backward bias gradient).
+// Block = 256 threads = tv channel vectors (16 B each) x rows pixel rows; each thread walks its
+// pixel rows RU at a time with every load of the group issued before any use (the loads of a
+// group are independent, so a wave keeps RU x tensors 16-B requests in flight).  Per-thread sums
+// are folded across the wave's pixel rows with xor-shuffles (lanes with equal tx), then across
+// the 4 waves through LDS.  Partials: part[k][C][G] (k = quantity), one column per block row.
 // ------------------------------------------------------------------------------------------
+constexpr int RU = 4;
+
 template <typename T>
-__global__ void bn_bwd_reduce_kernel(const T* dA, int ldd, const T* A, int lda, const float* msc, const float* msh,
-                                     const T* y1, int ld1, const float* mean1, const float* inv1, const T* y2, int ld2,
-                                     const float* mean2, const float* inv2, long M, int C, int tv, int pix_per_block,
-                                     float* part, int G) {
+__device__ __forceinline__ void cvt16(const uint4& raw, float (&out)[16 / sizeof(T)]) {
+  const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+  for (int i = 0; i < 16 / (int)sizeof(T); ++i) out[i] = (float)e[i];
+}
+
+// sum over the lanes of a wave that share (lane % tv); result valid in every lane
+__device__ __forceinline__ float rows_sum(float v, int tv) {
+  for (int o = tv; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// NQ quantities x V channels per thread -> part[k][C][G] column blockIdx.x
+template <int NQ, int V>
+__device__ __forceinline__ void store_partials(float (&s)[NQ][V], int tv, int c0, int C, int G, float* part,
+                                               float* red /* [4][NQ][64][V] */) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tx = threadIdx.x % tv;
+#pragma unroll
+  for (int k = 0; k < NQ; ++k)
+#pragma unroll
+    for (int e = 0; e < V; ++e) s[k][e] = rows_sum(s[k][e], tv);
+  if (lane < tv) {
+#pragma unroll
+    for (int k = 0; k < NQ; ++k)
+#pragma unroll
+      for (int e = 0; e < V; ++e) red[((w * NQ + k) * 64 + tx) * V + e] = s[k][e];
+  }
+  __syncthreads();
+  constexpr int nw = 4;  // waves per block (256 threads)
+  const int cb = c0 - tx * V;        // first channel of this block's group
+  for (int idx = threadIdx.x; idx < NQ * tv * V; idx += 256) {
+    const int k = idx / (tv * V), rem = idx - k * tv * V;
+    const int cx = rem / V, e = rem - cx * V;
+    float t = 0.f;
+    for (int ww = 0; ww < nw; ++ww) t += red[((ww * NQ + k) * 64 + cx) * V + e];
+    part[((long)k * C + cb + cx * V + e) * G + blockIdx.x] = t;
+  }
+}
+
+// BatchNorm backward, pass 1: per-(channel, pixel tile) partials of
+//   sum dz, sum dz*xhat1, sum dz*xhat2     where dz = dA * mask
+// MASK: 0 none, 1 (A > 0), 2 (y1*msc + msh > 0) -- the ReLU mask recomputed exactly as bn_apply
+// produced A.  Y2: second BN branch (downsample shortcut) present.
+template <typename T, int MASK, bool Y2>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dA, int ldd, const T* A, int lda,
+                                                            const float* msc, const float* msh, const T* y1, int ld1,
+                                                            const float* mean1, const float* inv1, const T* y2, int ld2,
+                                                            const float* mean2, const float* inv2, long M, int C,
+                                                            int tv, int pix_per_block, float* part, int G) {
   constexpr int V = VE<T>;
-  __shared__ float red[3][256][V];
-  const int tx = threadIdx.x % tv, ty = threadIdx.x / tv, rows = blockDim.x / tv;
+  constexpr int NQ = Y2 ? 3 : 2;
+  __shared__ float red[4 * 3 * 64 * V];
+  const int tx = threadIdx.x % tv, ty = threadIdx.x / tv, rows = 256 / tv;
   const int c0 = (blockIdx.y * tv + tx) * V;
   const long p0 = (long)blockIdx.x * pix_per_block;
   const long p1 = min(M, p0 + pix_per_block);
-  float s0[V], s1[V], s2[V], m1[V], i1[V], m2v[V], i2v[V], ms[V], mh[V];
+  float s[NQ][V], m1[V], i1[V], m2v[V], i2v[V], ms[V], mh[V];
 #pragma unroll
   for (int e = 0; e < V; ++e) {
-    s0[e] = s1[e] = s2[e] = 0.f;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) s[k][e] = 0.f;
     m1[e] = mean1[c0 + e];
     i1[e] = inv1[c0 + e];
-    m2v[e] = y2 ? mean2[c0 + e] : 0.f;
-    i2v[e] = y2 ? inv2[c0 + e] : 0.f;
-    ms[e] = msc ? msc[c0 + e] : 0.f;
-    mh[e] = msc ? msh[c0 + e] : 0.f;
+    m2v[e] = Y2 ? mean2[c0 + e] : 0.f;
+    i2v[e] = Y2 ? inv2[c0 + e] : 0.f;
+    ms[e] = MASK == 2 ? msc[c0 + e] : 0.f;
+    mh[e] = MASK == 2 ? msh[c0 + e] : 0.f;
   }
-  for (long p = p0 + ty; p < p1; p += rows) {
-    float d[V], a[V], x[V];
-    load_vec(dA + p * ldd + c0, d);
-    load_vec(y1 + p * ld1 + c0, x);
-    if (A) {
-      load_vec(A + p * lda + c0, a);
+  auto acc = [&](const uint4& rd, const uint4& rx, const uint4& ra, const uint4& r2) {
+    float d[V], x[V];
+    cvt16<T>(rd, d);
+    cvt16<T>(rx, x);
+    if (MASK == 1) {
+      float a[V];
+      cvt16<T>(ra, a);
 #pragma unroll
       for (int e = 0; e < V; ++e) d[e] = a[e] > 0.f ? d[e] : 0.f;
-    } else if (msc) {  // ReLU mask recomputed from y1 exactly as bn_apply produced A
+    } else if (MASK == 2) {
 #pragma unroll
       for (int e = 0; e < V; ++e) d[e] = fmaf(x[e], ms[e], mh[e]) > 0.f ? d[e] : 0.f;
     }
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      s0[e] += d[e];
-      s1[e] += d[e] * (x[e] - m1[e]) * i1[e];
+      s[0][e] += d[e];
+      s[1][e] += d[e] * ((x[e] - m1[e]) * i1[e]);
     }
-    if (y2) {
-      load_vec(y2 + p * ld2 + c0, x);
+    if (Y2) {
+      float x2[V];
+      cvt16<T>(r2, x2);
 #pragma unroll
-      for (int e = 0; e < V; ++e) s2[e] += d[e] * (x[e] - m2v[e]) * i2v[e];
+      for (int e = 0; e < V; ++e) s[NQ - 1][e] += d[e] * ((x2[e] - m2v[e]) * i2v[e]);
     }
-  }
+  };
+  long p = p0 + ty;
+  for (; p + (long)(RU - 1) * rows < p1; p += (long)RU * rows) {
+    uint4 rd[RU], rx[RU], ra[RU], r2[RU];
 #pragma unroll
-  for (int e = 0; e < V; ++e) {
-    red[0][threadIdx.x][e] = s0[e];
-    red[1][threadIdx.x][e] = s1[e];
-    red[2][threadIdx.x][e] = s2[e];
-  }
-  __syncthreads();
-  for (int half = rows >> 1; half > 0; half >>= 1) {
-    __syncthreads();
-    if (ty < half) {
-#pragma unroll
-      for (int e = 0; e < V; ++e) {
-        red[0][threadIdx.x][e] += red[0][threadIdx.x + half * tv][e];
-        red[1][threadIdx.x][e] += red[1][threadIdx.x + half * tv][e];
-        red[2][threadIdx.x][e] += red[2][threadIdx.x + half * tv][e];
-      }
+    for (int u = 0; u < RU; ++u) {
+      const long q = p + (long)u * rows;
+      rd[u] = *reinterpret_cast<const uint4*>(dA + q * ldd + c0);
+      rx[u] = *reinterpret_cast<const uint4*>(y1 + q * ld1 + c0);
+      if (MASK == 1) ra[u] = *reinterpret_cast<const uint4*>(A + q * lda + c0);
+      if (Y2) r2[u] = *reinterpret_cast<const uint4*>(y2 + q * ld2 + c0);
     }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) acc(rd[u], rx[u], ra[u], r2[u]);
   }
-  __syncthreads();
-  // 3*V partial sums per channel vector: spread the global stores over the first rows of threads
-  for (int idx = threadIdx.x; idx < 3 * tv * V; idx += blockDim.x) {
-    const int k = idx / (tv * V), rem = idx - k * tv * V;
-    const int cx = rem / V, e = rem - cx * V;
-    part[((long)k * C + (blockIdx.y * tv + cx) * V + e) * G + blockIdx.x] = red[k][cx][e];
+  for (; p < p1; p += rows) {
+    uint4 rd = *reinterpret_cast<const uint4*>(dA + p * ldd + c0), ra = rd, r2 = rd;
+    const uint4 rx = *reinterpret_cast<const uint4*>(y1 + p * ld1 + c0);
+    if (MASK == 1) ra = *reinterpret_cast<const uint4*>(A + p * lda + c0);
+    if (Y2) r2 = *reinterpret_cast<const uint4*>(y2 + p * ld2 + c0);
+    acc(rd, rx, ra, r2);
   }
+  store_partials<NQ, V>(s, tv, c0, C, G, part, red);
 }
 
 // pass 2: coefficients.  For branch b (1 or 2): dgamma_b += sum dz*xhat_b, dbeta_b += sum dz;
@@ -209,104 +260,140 @@ __global__ void bn_bwd_finalize_kernel(const float* part, int C, int G, long M, 
   }
 }
 
-// pass 3: dy_b = coef_a*(dz - mean(dz) - xhat_b*mean(dz*xhat_b)); optional dzout (+)= dz
-template <typename T>
-__global__ void bn_bwd_apply_kernel(const T* dA, int ldd, const T* A, int lda, const float* msc, const float* msh,
-                                    const T* y1, int ld1,
-                                    const float* mean1, const float* inv1, T* dy1, int ldo1, const T* y2, int ld2,
-                                    const float* mean2, const float* inv2, T* dy2, int ldo2, const float* coef,
-                                    T* dzout, int ldz, int dz_acc, long M, int C) {
+// pass 3: dy_b = coef_a*(dz - mean(dz) - xhat_b*mean(dz*xhat_b)); optional dzout (+)= dz.
+// Same block geometry as pass 1 (fixed channels per thread): the per-channel coefficients are
+// folded once into dy_b = P_b*dz + Q_b*(y_b - mean_b) + R_b and kept in registers.  DZ: 0 none, 1 store,
+// 2 accumulate.
+template <typename T, int MASK, bool Y2, int DZ>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dA, int ldd, const T* A, int lda,
+                                                           const float* msc, const float* msh, const T* y1, int ld1,
+                                                           const float* mean1, const float* inv1, T* dy1, int ldo1,
+                                                           const T* y2, int ld2, const float* mean2, const float* inv2,
+                                                           T* dy2, int ldo2, const float* coef, T* dzout, int ldz,
+                                                           long M, int C, int tv, int pix_per_block) {
   constexpr int V = VE<T>;
-  const int cv = C / V;
-  const long total = M * cv;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long pix = i / cv;
-    const int c0 = (int)(i - pix * cv) * V;
-    float d[V], a[V], x[V], o[V];
-    load_vec(dA + pix * ldd + c0, d);
-    load_vec(y1 + pix * ld1 + c0, x);
-    if (A) {
-      load_vec(A + pix * lda + c0, a);
+  const int tx = threadIdx.x % tv, ty = threadIdx.x / tv, rows = 256 / tv;
+  const int c0 = (blockIdx.y * tv + tx) * V;
+  const long p0 = (long)blockIdx.x * pix_per_block;
+  const long p1 = min(M, p0 + pix_per_block);
+  float P1[V], Q1[V], R1[V], M1[V], P2[V], Q2[V], R2[V], M2[V], ms[V], mh[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    const int c = c0 + e;
+    const float k1 = coef[c], cx1 = coef[2 * C + c] * inv1[c];
+    P1[e] = k1;
+    Q1[e] = -k1 * cx1;
+    R1[e] = -k1 * coef[C + c];
+    M1[e] = mean1[c];
+    if (Y2) {
+      const float k2 = coef[3 * C + c], cx2 = coef[5 * C + c] * inv2[c];
+      P2[e] = k2;
+      Q2[e] = -k2 * cx2;
+      R2[e] = -k2 * coef[4 * C + c];
+      M2[e] = mean2[c];
+    }
+    ms[e] = MASK == 2 ? msc[c] : 0.f;
+    mh[e] = MASK == 2 ? msh[c] : 0.f;
+  }
+  auto one = [&](long q, const uint4& rd, const uint4& rx, const uint4& ra, const uint4& r2, const uint4& rz) {
+    float d[V], x[V], o[V];
+    cvt16<T>(rd, d);
+    cvt16<T>(rx, x);
+    if (MASK == 1) {
+      float a[V];
+      cvt16<T>(ra, a);
 #pragma unroll
       for (int e = 0; e < V; ++e) d[e] = a[e] > 0.f ? d[e] : 0.f;
-    } else if (msc) {
+    } else if (MASK == 2) {
 #pragma unroll
-      for (int e = 0; e < V; ++e) d[e] = fmaf(x[e], msc[c0 + e], msh[c0 + e]) > 0.f ? d[e] : 0.f;
+      for (int e = 0; e < V; ++e) d[e] = fmaf(x[e], ms[e], mh[e]) > 0.f ? d[e] : 0.f;
     }
 #pragma unroll
-    for (int e = 0; e < V; ++e) {
-      const int c = c0 + e;
-      const float xh = (x[e] - mean1[c]) * inv1[c];
-      o[e] = coef[c] * (d[e] - coef[C + c] - xh * coef[2 * C + c]);
-    }
-    store_vec(dy1 + pix * ldo1 + c0, o);
-    if (y2) {
-      load_vec(y2 + pix * ld2 + c0, x);
+    for (int e = 0; e < V; ++e) o[e] = fmaf(P1[e], d[e], fmaf(Q1[e], x[e] - M1[e], R1[e]));
+    store_vec(dy1 + q * ldo1 + c0, o);
+    if (Y2) {
+      cvt16<T>(r2, x);
 #pragma unroll
-      for (int e = 0; e < V; ++e) {
-        const int c = c0 + e;
-        const float xh = (x[e] - mean2[c]) * inv2[c];
-        o[e] = coef[3 * C + c] * (d[e] - coef[4 * C + c] - xh * coef[5 * C + c]);
-      }
-      store_vec(dy2 + pix * ldo2 + c0, o);
+      for (int e = 0; e < V; ++e) o[e] = fmaf(P2[e], d[e], fmaf(Q2[e], x[e] - M2[e], R2[e]));
+      store_vec(dy2 + q * ldo2 + c0, o);
     }
-    if (dzout) {
-      if (dz_acc) {
-        load_vec(dzout + pix * ldz + c0, o);
+    if (DZ == 2) {
+      cvt16<T>(rz, o);
 #pragma unroll
-        for (int e = 0; e < V; ++e) o[e] += d[e];
-        store_vec(dzout + pix * ldz + c0, o);
-      } else {
-        store_vec(dzout + pix * ldz + c0, d);
-      }
+      for (int e = 0; e < V; ++e) o[e] += d[e];
+      store_vec(dzout + q * ldz + c0, o);
+    } else if (DZ == 1) {
+      store_vec(dzout + q * ldz + c0, d);
     }
+  };
+  long p = p0 + ty;
+  for (; p + (long)(RU - 1) * rows < p1; p += (long)RU * rows) {
+    uint4 rd[RU], rx[RU], ra[RU], r2[RU], rz[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const long q = p + (long)u * rows;
+      rd[u] = *reinterpret_cast<const uint4*>(dA + q * ldd + c0);
+      rx[u] = *reinterpret_cast<const uint4*>(y1 + q * ld1 + c0);
+      if (MASK == 1) ra[u] = *reinterpret_cast<const uint4*>(A + q * lda + c0);
+      if (Y2) r2[u] = *reinterpret_cast<const uint4*>(y2 + q * ld2 + c0);
+      if (DZ == 2) rz[u] = *reinterpret_cast<const uint4*>(dzout + q * ldz + c0);
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) one(p + (long)u * rows, rd[u], rx[u], ra[u], r2[u], rz[u]);
+  }
+  for (; p < p1; p += rows) {
+    const uint4 rd = *reinterpret_cast<const uint4*>(dA + p * ldd + c0);
+    const uint4 rx = *reinterpret_cast<const uint4*>(y1 + p * ld1 + c0);
+    uint4 ra = rd, r2 = rd, rz = rd;
+    if (MASK == 1) ra = *reinterpret_cast<const uint4*>(A + p * lda + c0);
+    if (Y2) r2 = *reinterpret_cast<const uint4*>(y2 + p * ld2 + c0);
+    if (DZ == 2) rz = *reinterpret_cast<const uint4*>(dzout + p * ldz + c0);
+    one(p, rd, rx, ra, r2, rz);
   }
 }
 
 // dY = dA * (A > 0) and per-tile column sums of dY (bias gradient partials [C][G])
 template <typename T>
-__global__ void relu_bwd_bias_kernel(const T* dA, int ldd, const T* A, int lda, T* dY, int ldy, long M, int C, int tv,
-                                     int pix_per_block, float* part, int G) {
+__global__ __launch_bounds__(256) void relu_bwd_bias_kernel(const T* dA, int ldd, const T* A, int lda, T* dY, int ldy,
+                                                            long M, int C, int tv, int pix_per_block, float* part,
+                                                            int G) {
   constexpr int V = VE<T>;
-  __shared__ float red[256][V];
-  const int tx = threadIdx.x % tv, ty = threadIdx.x / tv, rows = blockDim.x / tv;
+  __shared__ float red[4 * 64 * V];
+  const int tx = threadIdx.x % tv, ty = threadIdx.x / tv, rows = 256 / tv;
   const int c0 = (blockIdx.y * tv + tx) * V;
   const long p0 = (long)blockIdx.x * pix_per_block;
   const long p1 = min(M, p0 + pix_per_block);
-  float s[V];
+  float s[1][V];
 #pragma unroll
-  for (int e = 0; e < V; ++e) s[e] = 0.f;
-  for (long p = p0 + ty; p < p1; p += rows) {
+  for (int e = 0; e < V; ++e) s[0][e] = 0.f;
+  auto one = [&](long q, const uint4& rd, const uint4& ra) {
     float d[V], a[V];
-    load_vec(dA + p * ldd + c0, d);
-    load_vec(A + p * lda + c0, a);
-#pragma unroll
-    for (int e = 0; e < V; ++e) {
-      d[e] = a[e] > 0.f ? d[e] : 0.f;
-    }
+    cvt16<T>(rd, d);
+    cvt16<T>(ra, a);
     // round like the stored gradient so db == sum of the dY actually fed to wgrad
     T tmp[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      tmp[e] = (T)d[e];
-      s[e] += (float)tmp[e];
+      tmp[e] = (T)(a[e] > 0.f ? d[e] : 0.f);
+      s[0][e] += (float)tmp[e];
     }
-    *reinterpret_cast<uint4*>(dY + p * ldy + c0) = *reinterpret_cast<uint4*>(tmp);
-  }
+    *reinterpret_cast<uint4*>(dY + q * ldy + c0) = *reinterpret_cast<uint4*>(tmp);
+  };
+  long p = p0 + ty;
+  for (; p + (long)(RU - 1) * rows < p1; p += (long)RU * rows) {
+    uint4 rd[RU], ra[RU];
 #pragma unroll
-  for (int e = 0; e < V; ++e) red[threadIdx.x][e] = s[e];
-  for (int half = rows >> 1; half > 0; half >>= 1) {
-    __syncthreads();
-    if (ty < half) {
-#pragma unroll
-      for (int e = 0; e < V; ++e) red[threadIdx.x][e] += red[threadIdx.x + half * tv][e];
+    for (int u = 0; u < RU; ++u) {
+      const long q = p + (long)u * rows;
+      rd[u] = *reinterpret_cast<const uint4*>(dA + q * ldd + c0);
+      ra[u] = *reinterpret_cast<const uint4*>(A + q * lda + c0);
     }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) one(p + (long)u * rows, rd[u], ra[u]);
   }
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < tv * V; idx += blockDim.x) {
-    const int cx = idx / V, e = idx - cx * V;
-    part[(long)((blockIdx.y * tv + cx) * V + e) * G + blockIdx.x] = red[cx][e];
-  }
+  for (; p < p1; p += rows)
+    one(p, *reinterpret_cast<const uint4*>(dA + p * ldd + c0), *reinterpret_cast<const uint4*>(A + p * lda + c0));
+  store_partials<1, V>(s, tv, c0, C, G, part, red);
 }
 
 // out[c] (+)= sum_g part[c][g]   (fp64 accumulation, fixed order)
@@ -908,11 +995,15 @@ UNETSEG_API int unetseg_reduce_tiles(int dtype, long M, int C, int* tv_out, int*
   const int cv = C / V;
   const int tv = pow2_le(cv, 64);
   const int rows = 256 / tv;
-  // pixels per thread sized for ~2048 blocks over the (pixels x channel groups) grid
-  const long items = M * (long)cv;
-  long per = items / (2048L * 256);
-  if (per < 4) per = 4;
-  if (per > 64) per = 64;
+  const int groups = cv / tv;
+  // ~2048 blocks over (pixel tiles x channel groups); at least 2 unrolled groups of rows per
+  // thread so the partials stay a few % of the data
+  long target = 2048 / groups;
+  if (target < 64) target = 64;
+  long per = (M + rows * target - 1) / (rows * target);
+  per = (per + RU - 1) / RU * RU;
+  if (per < 2 * RU) per = 2 * RU;
+  if (per > 256) per = 256;
   const int ppb = rows * (int)per;
   if (tv_out) *tv_out = tv;
   if (ppb_out) *ppb_out = ppb;
@@ -929,9 +1020,23 @@ UNETSEG_API int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const 
   US_CHECK_ARG(g == G, "bn_bwd_reduce: G mismatch (%d vs %d)", G, g);
   const int V = dtype == DT_BF16 ? 8 : 4;
   dim3 grid(G, C / V / tv);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)dA,
-                                       ldd, (const T*)A, lda, msc, msh, (const T*)y1, ld1, mean1, inv1, (const T*)y2,
-                                       ld2, mean2, inv2, M, C, tv, ppb, part, G));
+  const int mask = A ? 1 : (msc ? 2 : 0);
+  hipStream_t st = (hipStream_t)stream;
+#define BN_RED_LAUNCH(MK, Y2)                                                                                     \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MK, Y2>), grid, dim3(256), 0, st, (const T*)dA, ldd, (const T*)A, lda, \
+                     msc, msh, (const T*)y1, ld1, mean1, inv1, (const T*)y2, ld2, mean2, inv2, M, C, tv, ppb, part, G)
+  DISPATCH_T(dtype, {
+    if (y2) {
+      if (mask == 1) BN_RED_LAUNCH(1, true);
+      else if (mask == 2) BN_RED_LAUNCH(2, true);
+      else BN_RED_LAUNCH(0, true);
+    } else {
+      if (mask == 1) BN_RED_LAUNCH(1, false);
+      else if (mask == 2) BN_RED_LAUNCH(2, false);
+      else BN_RED_LAUNCH(0, false);
+    }
+  });
+#undef BN_RED_LAUNCH
   US_LAUNCH_CHECK("bn_bwd_reduce");
   return 0;
 }
@@ -952,10 +1057,36 @@ UNETSEG_API int unetseg_bn_bwd_apply(int dtype, const void* dA, int ldd, const v
                                      int ldo2, const float* coef, void* dzout, int ldz, int dz_acc, long M, int C,
                                      void* stream) {
   CHECK_VEC(dtype, C, "bn_bwd_apply");
-  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(M * C / VE<T>)), dim3(256), 0,
-                                       (hipStream_t)stream, (const T*)dA, ldd, (const T*)A, lda, msc, msh,
-                                       (const T*)y1, ld1, mean1, inv1, (T*)dy1, ldo1, (const T*)y2, ld2, mean2, inv2, (T*)dy2, ldo2, coef,
-                                       (T*)dzout, ldz, dz_acc, M, C));
+  int tv, ppb;
+  const int G = unetseg_reduce_tiles(dtype, M, C, &tv, &ppb);
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  dim3 grid(G, C / V / tv);
+  const int mask = A ? 1 : (msc ? 2 : 0);
+  const int dzm = dzout ? (dz_acc ? 2 : 1) : 0;
+  hipStream_t st = (hipStream_t)stream;
+#define BN_APP_LAUNCH(MK, Y2, DZ)                                                                                  \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, MK, Y2, DZ>), grid, dim3(256), 0, st, (const T*)dA, ldd, (const T*)A,   \
+                     lda, msc, msh, (const T*)y1, ld1, mean1, inv1, (T*)dy1, ldo1, (const T*)y2, ld2, mean2, inv2,  \
+                     (T*)dy2, ldo2, coef, (T*)dzout, ldz, M, C, tv, ppb)
+#define BN_APP_DZ(MK, Y2)                  \
+  do {                                     \
+    if (dzm == 2) BN_APP_LAUNCH(MK, Y2, 2); \
+    else if (dzm == 1) BN_APP_LAUNCH(MK, Y2, 1); \
+    else BN_APP_LAUNCH(MK, Y2, 0);          \
+  } while (0)
+  DISPATCH_T(dtype, {
+    if (y2) {
+      if (mask == 1) BN_APP_DZ(1, true);
+      else if (mask == 2) BN_APP_DZ(2, true);
+      else BN_APP_DZ(0, true);
+    } else {
+      if (mask == 1) BN_APP_DZ(1, false);
+      else if (mask == 2) BN_APP_DZ(2, false);
+      else BN_APP_DZ(0, false);
+    }
+  });
+#undef BN_APP_DZ
+#undef BN_APP_LAUNCH
   US_LAUNCH_CHECK("bn_bwd_apply");
   return 0;
 }

@@ -7,12 +7,16 @@ The reference is single-process (train.py:98); this is the build's DP path (SURV
     reports each finished parameter (``param_done``) and a bucket's all-reduce (AVG) is issued the
     moment its last parameter is final, overlapping the rest of backward (RCCL runs on its own
     stream, fenced against the compute stream by torch.distributed);
-  * BatchNorm uses per-GPU batch statistics and rank-local running stats (DDP without SyncBN).
+  * BatchNorm uses per-GPU batch statistics and rank-local running stats (DDP without SyncBN);
+  * with the op layer's weight-gradient stream (ops.OVERLAP) a bucket's collective is enqueued on
+    that stream after it has waited for the compute stream, so it follows every writer.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
+
+from . import ops
 
 
 class GradBuckets:
@@ -59,7 +63,15 @@ class GradBuckets:
     def _issue(self, i):
         s, e, _ = self.buckets[i]
         view = self.model._flat_grad[s:e]
-        self._pending.append(dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
+        side = ops.side_stream(view.device) if (ops.OVERLAP and view.is_cuda) else None
+        if side is None:
+            self._pending.append(dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
+        else:
+            # weight gradients are written on the side stream, BN/bias gradients on the compute
+            # stream: the collective is ordered after both (side waits for compute, RCCL for side)
+            side.wait_stream(torch.cuda.current_stream(view.device))
+            with torch.cuda.stream(side):
+                self._pending.append(dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
         self._issued[i] = True
 
     def _on_grad(self, p):

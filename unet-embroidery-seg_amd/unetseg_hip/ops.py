@@ -10,6 +10,7 @@ stream only; all arithmetic is in libunetseg_hip.so.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -50,26 +51,41 @@ PROBE = None
 
 
 class _probe:
-    def __init__(self, kind, flops, launches=1, desc=None):
-        self.kind, self.flops, self.launches, self.desc = kind, flops, launches, desc
+    """HIP events around one op's launches, recorded on the stream the kernels run on."""
+
+    def __init__(self, kind, flops, launches=1, desc=None, stream=None):
+        self.kind, self.flops, self.launches, self.desc, self.stream = kind, flops, launches, desc, stream
 
     def __enter__(self):
         if PROBE is not None:
             self.e0 = torch.cuda.Event(enable_timing=True)
             self.e1 = torch.cuda.Event(enable_timing=True)
-            self.e0.record()
+            self.e0.record(self.stream)
         return self
 
     def __exit__(self, *a):
         if PROBE is not None:
-            self.e1.record()
+            self.e1.record(self.stream)
             PROBE.append((self.kind, self.flops, self.launches, self.e0, self.e1, self.desc))
 
 
-def workspace(nbytes, device):
-    """Stream-ordered scratch shared by consecutive launches (never shrunk: captured graphs keep
-    pointers into every buffer ever handed out)."""
+#: weight gradients run on a second HIP stream, concurrent with the data-gradient chain of the
+#: backward pass (UNETSEG_NO_OVERLAP=1 keeps everything on the compute stream)
+OVERLAP = os.environ.get("UNETSEG_NO_OVERLAP", "0") != "1"
+_SIDE = {}
+
+
+def side_stream(device):
     key = (device.type, device.index)
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device)
+    return _SIDE[key]
+
+
+def workspace(nbytes, device, stream_key=0):
+    """Stream-ordered scratch shared by consecutive launches on one stream (never shrunk: captured
+    graphs keep pointers into every buffer ever handed out)."""
+    key = (device.type, device.index, stream_key)
     lst = _WORKSPACES.setdefault(key, [])
     if not lst or lst[-1].numel() < nbytes:
         lst.append(torch.empty(max(int(nbytes), 1 << 20), dtype=torch.uint8, device=device))
@@ -83,8 +99,10 @@ class Ctx:
         self.training = training
         self.tape = [] if record else None
         self.device = device
-        self.stream = torch.cuda.current_stream(device).cuda_stream
+        self.main = torch.cuda.current_stream(device)
+        self.stream = self.main.cuda_stream
         self.grad_hook = None  # called with a param after its gradient is final (DDP bucketing)
+        self.side = None  # weight-gradient stream, set while backward runs with OVERLAP
 
     def push(self, fn):
         if self.tape is not None:
@@ -98,8 +116,17 @@ class Ctx:
 
     def backward(self):
         tape, self.tape = self.tape, None
-        for fn in reversed(tape):
-            fn()
+        if OVERLAP:
+            self.side = side_stream(self.device)
+            self.side.wait_stream(self.main)
+        try:
+            for fn in reversed(tape):
+                fn()
+        finally:
+            if self.side is not None:
+                # everything after backward (optimizer, frees of tape tensors) follows the wgrads
+                self.main.wait_stream(self.side)
+                self.side = None
 
     def param_done(self, *params):
         if self.grad_hook is not None:
@@ -244,13 +271,22 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
         else:
             assert b is None, "conv with bias and no ReLU is not on the hot path"
             dY = dA
-        # weight gradient
+        # weight gradient: on the side stream when overlapping (it only needs dY and the inputs,
+        # and nothing in the data-gradient chain reads its output)
         cin = C1 + C2
         ws_bytes = lib.conv2d_wgrad_workspace(ctx.dt, N, Pq, Qq, K, cin, R, S)
-        ws = workspace(ws_bytes, dev)
-        with _probe("wgrad", flops, 1, ("wgrad",) + desc):
+        side = ctx.side
+        if side is not None:
+            side.wait_stream(ctx.main)
+            dY.record_stream(side)  # a local dY may be freed (main-stream order) before the wgrad runs
+            ws = workspace(ws_bytes, dev, 1)
+            wst = side.cuda_stream
+        else:
+            ws = workspace(ws_bytes, dev)
+            wst = ctx.stream
+        with _probe("wgrad", flops, 1, ("wgrad",) + desc, stream=side):
             lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(dY), ldp(dY), K, R, S,
-                             stride, pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, ctx.stream)
+                             stride, pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, wst)
         ctx.param_done(pc.conv.weight, b)
         # data gradient
         if x2 is None:
