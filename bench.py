@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (N=1)")
     ap.add_argument("--cpu-batch", type=int, default=4, help="images in the bounded CPU sample")
     ap.add_argument("--probe", type=int, default=1)
+    ap.add_argument("--graph", type=int, default=0, help="replay the whole step (fwd+loss+bwd+Adam) as a HIP graph")
+    ap.add_argument("--stream", type=int, default=1, help="run the steps on a created (non-default) HIP stream")
     return ap.parse_args()
 
 
@@ -98,6 +100,10 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     torch.manual_seed(11)
+    if args.stream:
+        # the legacy default stream synchronises implicitly with other streams, which makes the
+        # compute stream's final join with the weight-gradient stream slow; work on a created one
+        torch.cuda.set_stream(torch.cuda.Stream(dev))
 
     from model.model_factory import create_model
     from unetseg_hip import ops
@@ -112,7 +118,8 @@ def main():
         model = create_model(args.model, weights="", **kw).to(dev).train()
     model.compute_dtype = "bf16"
     buckets = GradBuckets(model) if world > 1 else None
-    opt = FusedAdam(model, lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4)
+    use_graph = bool(args.graph) and world == 1  # N>1: RCCL collectives stay eager
+    opt = FusedAdam(model, lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4, capturable=use_graph)
     nbatches = 2
     multitask = args.model == "multitask_unet"
     data = []
@@ -133,8 +140,31 @@ def main():
         opt.step()
         return loss
 
+    run = step
+    if use_graph:
+        # one captured step per resident batch; every replay is a full fwd + loss + bwd + Adam step
+        # (Adam's lr and step count are device-resident, so replays advance the optimizer state)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for i in range(max(2, args.warmup)):
+                step(i)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize()
+        graphs = []
+        for i in range(nbatches):
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                li = step(i)
+            graphs.append((gr, li))
+
+        def run(i):
+            gr, li = graphs[i % nbatches]
+            gr.replay()
+            return li
+
     for i in range(args.warmup):
-        step(i)
+        run(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -143,7 +173,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record()
     for i in range(args.steps):
-        loss = step(i)
+        loss = run(i)
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -202,6 +232,7 @@ def main():
             "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
             "step_tflops_per_gpu": round(step_tflops, 2),
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 3), "final_loss": round(final_loss, 5),
+            "hip_graph": use_graph,
         }
         print(json.dumps(line))
     if world > 1:

@@ -166,6 +166,11 @@ int unetseg_ce_fwd(const float* logits, const int64_t* tgt, int B, int K, float*
 int unetseg_scale_grad(const float* g, long n, const float* s1, float a1, const float* s2, float a2, float* out,
                        void* stream);
 
+/* ---- streams ---------------------------------------------------------------------------------- */
+/* `waiter` waits for everything enqueued so far on `signaler` (device-scope release event; no
+   reference counterpart: orders the weight-gradient stream against the compute stream) */
+int unetseg_stream_wait(void* waiter, void* signaler);
+
 /* ---- multitask classification head (model/unet_multitask.py:73-80) -------------------------- */
 int unetseg_gap_fwd(int dtype, const void* x, int ldx, int B, int HW, int C, float* g, void* stream);
 int unetseg_gap_bwd(int dtype, const float* dg, int B, int HW, int C, void* dx, int ldx, int accumulate,
@@ -182,6 +187,10 @@ int unetseg_linear_bwd(const float* dy, const float* pre, const float* mask, flo
  *      arena; grad_scale (may be NULL) multiplies g first ------------------------------------------ */
 int unetseg_adam(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2, float eps,
                  float wd, int step, const float* grad_scale, void* stream);
+/* capturable Adam (hipGraph replay): hyper[0] = lr and *step (steps taken; advanced by one after the
+   update) are read from device memory */
+int unetseg_adam_dev(float* p, const float* g, float* m, float* v, long n, const float* hyper, int* step, float beta1,
+                     float beta2, float eps, float wd, const float* grad_scale, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,13 +1,15 @@
-# A/B of the bench (overlap on / off) after the GPU test suite; run from the repo root on the box
+# bench A/B: BENCH_A / BENCH_B are extra bench.py args (or env prefixes); tests first unless NOTEST=1
 set -o pipefail
+if [ -z "$NOTEST" ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/gpu_tests.log; exit 1; }
 tail -2 gpurun_out/gpu_tests.log
-timeout -k 10 300 python bench.py --cpu-baseline 0 > gpurun_out/bench_on.json 2> gpurun_out/bench_on.err && \
-UNETSEG_NO_OVERLAP=1 timeout -k 10 300 python bench.py --cpu-baseline 0 > gpurun_out/bench_off.json 2> gpurun_out/bench_off.err
+fi
+eval "$ENV_A timeout -k 10 300 python bench.py --cpu-baseline 0 $BENCH_A" > gpurun_out/bench_a.json 2> gpurun_out/bench_a.err && \
+eval "$ENV_B timeout -k 10 300 python bench.py --cpu-baseline 0 $BENCH_B" > gpurun_out/bench_b.json 2> gpurun_out/bench_b.err
 rc=$?
 python - <<'PY'
 import json
-for f in ("on", "off"):
+for f in ("a", "b"):
     try:
         d = json.loads(open(f"gpurun_out/bench_{f}.json").read().strip().splitlines()[-1])
         print(f, d["value"], "img/s", d["ms_per_step"], "ms", {k: v["ms_per_step"] for k, v in d["roofline"]["kernels"].items()})

@@ -332,6 +332,39 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, long n
   }
 }
 
+// Capturable form (hipGraph replay): lr and the step count live in device memory, so a replayed
+// step uses the current values.  hyper[0] = lr; *step is the count of steps already taken (the
+// update uses *step + 1; adam_step_commit advances it afterwards).
+__global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, long n, const float* hyper,
+                                const int* step, float beta1, float beta2, float eps, float wd,
+                                const float* grad_scale) {
+  __shared__ float k[2];
+  if (threadIdx.x == 0) {
+    const double t = (double)(step[0] + 1);
+    const double bc1 = 1.0 - pow((double)beta1, t);
+    const double bc2 = 1.0 - pow((double)beta2, t);
+    k[0] = (float)bc1;
+    k[1] = (float)sqrt(bc2);
+  }
+  __syncthreads();
+  const float bc1 = k[0], bc2_sqrt = k[1], lr = hyper[0];
+  const float inv_scale = grad_scale ? 1.0f / grad_scale[0] : 1.0f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gr = g[i] * inv_scale;
+    const float pv = p[i];
+    if (wd != 0.f) gr = gr + wd * pv;
+    float mv = m[i];
+    mv = mv + (1.f - beta1) * (gr - mv);
+    float vv = v[i] * beta2 + (1.f - beta2) * gr * gr;
+    m[i] = mv;
+    v[i] = vv;
+    const float denom = sqrtf(vv) / bc2_sqrt + eps;
+    p[i] = pv - (lr / bc1) * (mv / denom);
+  }
+}
+
+__global__ void adam_step_commit_kernel(int* step) { step[0] += 1; }
+
 // ------------------------------------------------------------------------------------------
 // multitask classification head (model/unet_multitask.py:73-80)
 // ------------------------------------------------------------------------------------------
@@ -553,6 +586,17 @@ UNETSEG_API int unetseg_adam(float* p, const float* g, float* m, float* v, long 
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 16384)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, beta1,
                      beta2, eps, wd, (float)bc1, (float)sqrt(bc2), grad_scale);
   US_LAUNCH_CHECK("adam");
+  return 0;
+}
+
+UNETSEG_API int unetseg_adam_dev(float* p, const float* g, float* m, float* v, long n, const float* hyper, int* step,
+                                 float beta1, float beta2, float eps, float wd, const float* grad_scale,
+                                 void* stream) {
+  US_CHECK_ARG(hyper && step, "adam_dev: hyper and step must be device pointers");
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n, 16384)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
+                     hyper, step, beta1, beta2, eps, wd, grad_scale);
+  hipLaunchKernelGGL(adam_step_commit_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step);
+  US_LAUNCH_CHECK("adam_dev");
   return 0;
 }
 

@@ -67,6 +67,8 @@ SIGNATURES = {
     "unetseg_linear_bwd": (I, [P, P, P, F, I, P, P, I, I, I, P, P, P, P, P]),
     "unetseg_ce_fwd": (I, [P, P, I, I, P, P, P]),
     "unetseg_scale_grad": (I, [P, L, P, F, P, F, P, P]),
+    "unetseg_stream_wait": (I, [P, P]),
+    "unetseg_adam_dev": (I, [P, P, P, P, L, P, P, F, F, F, F, P, P]),
 }
 
 _lib = None

@@ -197,6 +197,9 @@ class HipModel(nn.Module):
 
     def _attach_grads(self, force=False):
         """make every param.grad a view of the flat gradient arena (None -> zeros, foreign -> copied)"""
+        views = getattr(self, "_grad_views", None)
+        if not force and views is not None and all(p.grad is v for p, v in views):
+            return  # fast path (every step): nothing was detached or replaced
         base = self._flat_grad.data_ptr()
         esz = self._flat_grad.element_size()
         for p in self._param_list:
@@ -211,6 +214,7 @@ class HipModel(nn.Module):
                 else:
                     view.copy_(g)
             p.grad = view
+        self._grad_views = [(p, p.grad) for p in self._param_list]
 
     def flat_slice(self, p):
         return self._slices[id(p)]

@@ -118,14 +118,19 @@ class Ctx:
         tape, self.tape = self.tape, None
         if OVERLAP:
             self.side = side_stream(self.device)
-            self.side.wait_stream(self.main)
+            lib.stream_wait(self.side.cuda_stream, self.stream)
         try:
-            for fn in reversed(tape):
+            # pop each closure as it runs: its tensors are released during the pass (lower peak,
+            # and the host frees them while it would otherwise wait on the launch queue, not in
+            # one burst between the last backward launch and the optimizer)
+            while tape:
+                fn = tape.pop()
                 fn()
+                del fn
         finally:
             if self.side is not None:
                 # everything after backward (optimizer, frees of tape tensors) follows the wgrads
-                self.main.wait_stream(self.side)
+                lib.stream_wait(self.stream, self.side.cuda_stream)
                 self.side = None
 
     def param_done(self, *params):
@@ -277,8 +282,11 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
         ws_bytes = lib.conv2d_wgrad_workspace(ctx.dt, N, Pq, Qq, K, cin, R, S)
         side = ctx.side
         if side is not None:
-            side.wait_stream(ctx.main)
-            dY.record_stream(side)  # a local dY may be freed (main-stream order) before the wgrad runs
+            lib.stream_wait(side.cuda_stream, ctx.stream)
+            # dY and the inputs may be freed (compute-stream order) before the wgrad has run
+            for t in (dY, X1, X2):
+                if t is not None:
+                    t.record_stream(side)
             ws = workspace(ws_bytes, dev, 1)
             wst = side.cuda_stream
         else:
