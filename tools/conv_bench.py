@@ -12,6 +12,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (REPO, os.path.join(REPO, "unet-embroidery-seg_amd")):
     sys.path.insert(0, p)
 
+os.environ.setdefault("UNETSEG_NO_OVERLAP", "1")  # per-op timing: no wgrad/dgrad concurrency
 import torch  # noqa: E402
 
 DEFAULT = [

@@ -27,8 +27,13 @@ namespace {
 // ------------------------------------------------------------------------------------------
 // ST: 1 = a single K step, 2 = global loads one K step ahead, 3 = two steps ahead (two register
 // sets; only where the registers fit at two waves per SIMD)
+// waves per SIMD each configuration is sized for (LDS allows that many blocks per CU); caps the
+// register allocation so the two-step register prefetch cannot cost occupancy
+template <int BM, int BN, int NWM, int NWN>
+constexpr int tn_waves_per_simd() { return (BM == 64) ? 3 : 2; }
+
 template <int BM, int BN, int NWM, int NWN, int ST>
-__global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
+__global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN>())) void tn_fast_kernel(FastTNArgs a) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int WTM = BM / NWM, WTN = BN / NWN;
   constexpr int FP = WTM / 16, FC = WTN / 16;
@@ -86,16 +91,20 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
   uint4 ra0[A_PER], rb0[B_PER], ra1[A_PER], rb1[B_PER];
   // scalar K-step state
   int s_jr = 0, s_js = 0, s_c = 0;
-  auto gload = [&](uint4 (&ra)[A_PER], uint4 (&rbv)[B_PER]) {
+  // live == false (a K step past the end): every offset is out of range, so the loads return
+  // zeros without touching memory.  Issuing them anyway keeps the loop free of conditional loads,
+  // which lets hipcc count vmcnt exactly (with conditional loads it waits for the loads of the
+  // step in flight too, exposing their latency every K step).
+  auto gload = [&](uint4 (&ra)[A_PER], uint4 (&rbv)[B_PER], bool live = true) {
     const int dh = a.dh0 + a.dhs * s_jr, dw = a.dw0 + a.dws * s_js;
-    const int tapbit = s_jr * a.ns + s_js;
+    const int tapbit = (s_jr * a.ns + s_js) & 31;
     const int tapdelta = dh * a.W + dw;
     const unsigned wofs = (unsigned)(((a.r0 + a.rs * s_jr) * a.S + (a.s0 + a.ss * s_js)) * a.cin + s_c) * 2u;
     if (s_c < a.c1) {
       const unsigned cb = (unsigned)s_c * 2u + kv * 16;
 #pragma unroll
       for (int i = 0; i < A_PER; ++i) {
-        const bool ok = (vmask[i] >> tapbit) & 1u;
+        const bool ok = live && ((vmask[i] >> tapbit) & 1u);
         const unsigned off = (unsigned)(pix[i] + tapdelta) * (unsigned)a.ldc1b + cb;
         ra[i] = bload(r1, ok ? off : kOOB);
       }
@@ -103,13 +112,13 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
       const unsigned cb = (unsigned)(s_c - a.c1) * 2u + kv * 16;
 #pragma unroll
       for (int i = 0; i < A_PER; ++i) {
-        const bool ok = (vmask[i] >> tapbit) & 1u;
+        const bool ok = live && ((vmask[i] >> tapbit) & 1u);
         const unsigned off = (unsigned)(pix[i] + tapdelta) * (unsigned)a.ldc2b + cb;
         ra[i] = bload(r2, ok ? off : kOOB);
       }
     }
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) rbv[i] = bload(rw, boff[i] == kOOB ? kOOB : boff[i] + wofs);
+    for (int i = 0; i < B_PER; ++i) rbv[i] = bload(rw, (!live || boff[i] == kOOB) ? kOOB : boff[i] + wofs);
     s_c += 64;
     if (s_c >= a.cin) {
       s_c = 0;
@@ -185,23 +194,26 @@ __global__ __launch_bounds__(64 * NWM * NWN) void tn_fast_kernel(FastTNArgs a) {
       __syncthreads();
     }
   } else {  // ST == 3: loads two steps ahead (two register sets)
+    // Loads and LDS stores are unconditional inside the loop (past-the-end steps load zeros), so
+    // the in-order vmcnt bookkeeping is the same on every path: each sstore waits only for the
+    // register set it writes, while the set issued in the same half stays in flight.
     if (nsteps > 0) {
       gload(ra0, rb0);
       sstore(0, ra0, rb0);
-      if (nsteps > 1) gload(ra1, rb1);
+      gload(ra1, rb1, nsteps > 1);
       __syncthreads();
     }
     for (int kt = 0; kt < nsteps; kt += 2) {
       // even step: stage 0 holds kt, registers 1 hold kt+1 (in flight)
-      if (kt + 2 < nsteps) gload(ra0, rb0);
+      gload(ra0, rb0, kt + 2 < nsteps);
       compute(0);
-      if (kt + 1 < nsteps) sstore(1, ra1, rb1);
+      sstore(1, ra1, rb1);
       __syncthreads();
       if (kt + 1 >= nsteps) break;
       // odd step: stage 1 holds kt+1, registers 0 hold kt+2 (in flight)
-      if (kt + 3 < nsteps) gload(ra1, rb1);
+      gload(ra1, rb1, kt + 3 < nsteps);
       compute(1);
-      if (kt + 2 < nsteps) sstore(0, ra0, rb0);
+      sstore(0, ra0, rb0);
       __syncthreads();
     }
   }
@@ -567,8 +579,8 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 1: return launch_tn_cfg<256, 64, 4, 1, 2>(a, st);
     case 2: return launch_tn_cfg<256, 128, 4, 2, 3>(a, st);
     case 4: return launch_tn_cfg<128, 128, 2, 2, 1>(a, st);
-    case 5: return launch_tn_cfg<64, 128, 1, 4, 2>(a, st);
-    default: return launch_tn_cfg<128, 128, 2, 2, 2>(a, st);
+    case 5: return launch_tn_cfg<64, 128, 1, 4, 3>(a, st);
+    default: return launch_tn_cfg<128, 128, 2, 2, 3>(a, st);
   }
 }
 
