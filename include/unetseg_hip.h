@@ -68,6 +68,16 @@ int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, const void* 
 int unetseg_conv2d_dgrad(int dtype, const void* dy, int ldy, int n, int p, int q, const void* wt, int cout, int cin,
                          int r, int s, int stride, int pad, void* dx, int ldx, int h, int w, int accumulate,
                          void* stream);
+/* data gradient whose epilogue applies the producer's ReLU (post 1: aux = ReLU output) or BN-ReLU
+   (post 2: aux = BN input z; psc/psh = BN affine, pmean/pinv = batch stats) mask and writes the
+   first backward reduction of that op: part[rows][2][cin] = (sum d, sum d*xhat) per row tile
+   (fuses model/resnet_backbone.py:95-110 ReLU+BN backward pass 1 / unet_resnet.py:37-40 ReLU+bias
+   into the consumer conv's dgrad).  part == NULL: returns rows, or -1 when the shape has no fused
+   path (bf16 fast kernels only). */
+int unetseg_conv2d_dgrad_post(int dtype, const void* dy, int ldy, int n, int p, int q, const void* wt, int cout,
+                              int cin, int r, int s, int stride, int pad, void* dx, int ldx, int h, int w, int post,
+                              const void* aux, int ld_aux, const float* psc, const float* psh, const float* pmean,
+                              const float* pinv, float* part, int rows, void* stream);
 size_t unetseg_conv2d_wgrad_workspace(int dtype, int n, int p, int q, int cout, int cin, int r, int s);
 /* dw fp32 [cout][dw_c][r][s] (PyTorch layout) (+)= sum_pix dy x; ws of the size queried above */
 int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h,
@@ -111,6 +121,11 @@ int unetseg_bn_bwd_apply(int dtype, const void* dA, int ldd, const void* A, int 
 int unetseg_relu_bwd_bias(int dtype, const void* dA, int ldd, const void* A, int lda, void* dY, int ldy, long M, int C,
                           float* part, int G, void* stream);
 int unetseg_colsum_finalize(const float* part, int C, int G, float* out, int accumulate, void* stream);
+/* BN backward coefficients / ReLU bias gradient from the row partials part[G][2][C] written by
+   unetseg_conv2d_dgrad_post (model/resnet_backbone.py BatchNorm2d backward, unet_resnet.py ReLU) */
+int unetseg_bn_bwd_finalize_rows(const float* part, int C, int G, long M, const float* g1, const float* inv1,
+                                 float* dg1, float* db1, float* coef, void* stream);
+int unetseg_colsum_rows(const float* part, int C, int G, int k, float* out, int accumulate, void* stream);
 
 /* ---- pooling / resampling (nn.MaxPool2d: model/resnet_backbone.py:131, model/unet_plain.py:25,
  *      model/unet_attention.py:66-69; UpsamplingBilinear2d / Upsample / interpolate:

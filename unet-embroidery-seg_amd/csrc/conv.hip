@@ -694,6 +694,9 @@ UNETSEG_API int unetseg_conv2d_dgrad(int dtype, const void* dy, int ldy, int n, 
       a.dw0 = (pw + pad - a.s0) / stride; a.dws = -1;
       if (a.nr < 0) a.nr = 0;
       if (a.ns <= 0) { a.ns = 1; a.nr = 0; }
+      // a parity class no tap reaches (e.g. odd pixels of a 1x1 stride-2 conv) contributes zeros:
+      // written when this call initialises dx, skipped when it accumulates
+      if (a.nr == 0 && accumulate) continue;
       a.S = s; a.cin = cout; a.wt = wt; a.ldw = (long)r * s * cout; a.Ng = cin;
       a.ostride = stride; a.ph = ph; a.pw = pw; a.OH = h; a.OW = w;
       a.y = dx; a.ldy = ldx; a.accumulate = accumulate; a.bias = nullptr; a.relu = 0;
@@ -701,6 +704,70 @@ UNETSEG_API int unetseg_conv2d_dgrad(int dtype, const void* dy, int ldy, int n, 
       int rc = dtype == DT_BF16 ? launch_tn<bf16>(a, st) : launch_tn<float>(a, st);
       if (rc) return rc;
     }
+  return 0;
+}
+
+// Data gradient with a post-op fused into the epilogue (bf16 fast path only).  The produced
+// gradient belongs to a tensor that was the output of a ReLU (post 1: aux = that output) or of a
+// BN-ReLU (post 2: aux = the BN input z, psc/psh its affine, pmean/pinv its batch statistics);
+// what is stored is the masked gradient d, and part[row][2][cin] receives per-row-tile column sums
+// of d and (post 2) of d * (z - mean) * inv -- the first pass of the ReLU bias / BN backward.
+// part == NULL: returns the number of partial rows for this shape, or -1 if the shape has no fused
+// path (the caller then runs the plain dgrad and the separate reduction).
+static int dgrad_classes(const void* dy, int ldy, int n, int p, int q, const void* wt, int cout, int cin, int r, int s,
+                         int stride, int pad, void* dx, int ldx, int h, int w, int ph, int pw, IgemmArgs& a) {
+  a = IgemmArgs{};
+  a.x1 = dy; a.x2 = nullptr; a.c1 = cout; a.c2 = 0; a.ldc1 = ldy; a.ldc2 = 0;
+  a.N = n; a.H = p; a.W = q; a.istride = 1;
+  a.hc = (h - ph + stride - 1) / stride; a.wc = (w - pw + stride - 1) / stride;
+  if (a.hc <= 0 || a.wc <= 0) return 0;
+  a.r0 = (ph + pad) % stride; a.rs = stride; a.nr = (r - a.r0 + stride - 1) / stride;
+  a.dh0 = (ph + pad - a.r0) / stride; a.dhs = -1;
+  a.s0 = (pw + pad) % stride; a.ss = stride; a.ns = (s - a.s0 + stride - 1) / stride;
+  a.dw0 = (pw + pad - a.s0) / stride; a.dws = -1;
+  if (a.nr < 0) a.nr = 0;
+  if (a.ns <= 0) { a.ns = 1; a.nr = 0; }
+  a.S = s; a.cin = cout; a.wt = wt; a.ldw = (long)r * s * cout; a.Ng = cin;
+  a.ostride = stride; a.ph = ph; a.pw = pw; a.OH = h; a.OW = w;
+  a.y = dx; a.ldy = ldx; a.accumulate = 0; a.bias = nullptr; a.relu = 0;
+  a.M = n * a.hc * a.wc; a.stats = nullptr;
+  return 1;
+}
+
+UNETSEG_API int unetseg_conv2d_dgrad_post(int dtype, const void* dy, int ldy, int n, int p, int q, const void* wt,
+                                          int cout, int cin, int r, int s, int stride, int pad, void* dx, int ldx,
+                                          int h, int w, int post, const void* aux, int ld_aux, const float* psc,
+                                          const float* psh, const float* pmean, const float* pinv, float* part,
+                                          int rows, void* stream) {
+  US_CHECK_ARG(post == 1 || post == 2, "conv2d_dgrad_post: post must be 1 (ReLU) or 2 (BN-ReLU)");
+  if (dtype != DT_BF16 || stride < 1 || stride > 2 || cout % 8 || ldy % 8) return -1;
+  // every parity class must take the fast path (the generic kernel has no post-op epilogue)
+  int total = 0;
+  FastTNArgs fs[4];
+  int ncls = 0;
+  for (int ph = 0; ph < stride; ++ph)
+    for (int pw = 0; pw < stride; ++pw) {
+      IgemmArgs a;
+      if (!dgrad_classes(dy, ldy, n, p, q, wt, cout, cin, r, s, stride, pad, dx, ldx, h, w, ph, pw, a)) continue;
+      if (a.M <= 0) continue;
+      FastTNArgs f;
+      if (!fast_tn_args(a, f)) return -1;
+      f.post = post; f.aux = aux; f.ld_aux = ld_aux; f.psc = psc; f.psh = psh; f.pmean = pmean; f.pinv = pinv;
+      fs[ncls++] = f;
+      total += tn_fast_post_rows(f);
+    }
+  if (!part) return total;
+  US_CHECK_ARG(dy && wt && dx && aux, "conv2d_dgrad_post: null pointer");
+  US_CHECK_ARG(rows == total, "conv2d_dgrad_post: rows %d != %d", rows, total);
+  US_CHECK_ARG(post == 1 || (psc && psh && pmean && pinv), "conv2d_dgrad_post: BN post needs its coefficients");
+  hipStream_t st = (hipStream_t)stream;
+  int off = 0;
+  for (int i = 0; i < ncls; ++i) {
+    fs[i].ppart = part + (long)off * 2 * cin;
+    off += tn_fast_post_rows(fs[i]);
+    launch_tn_fast(fs[i], st);
+  }
+  US_LAUNCH_CHECK("conv2d_dgrad_post");
   return 0;
 }
 

@@ -26,6 +26,18 @@ struct FastTNArgs {
   float* stats;
   int stats_ld;
   int M;
+  // data-gradient post-op (dgrad of the consumer of a ReLU / BN-ReLU output; never with
+  // accumulate): post 1 = ReLU mask from aux (the ReLU output), 2 = BN-ReLU mask from aux (the BN
+  // input z: z*psc + psh > 0).  The masked gradient d is what is stored; ppart[tile][2][Ng] gets the
+  // per-row-tile column sums of d and (post 2) of d * (z - pmean) * pinv.
+  int post;
+  const void* aux;
+  int ld_aux;
+  const float* psc;
+  const float* psh;
+  const float* pmean;
+  const float* pinv;
+  float* ppart;
 };
 
 struct FastWgradArgs {
@@ -58,6 +70,8 @@ struct HaloWgradArgs {
 bool tn_fast_ok(const FastTNArgs& a);
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st);
 int tn_fast_tile_m(const FastTNArgs& a);
+int tn_fast_post_rows(const FastTNArgs& a);  // partial rows (ppart) a launch_tn_fast call writes
+int halo3_blocks(const FastTNArgs& a);
 bool halo3_ok(const FastTNArgs& a);
 int launch_halo3(const FastTNArgs& a, hipStream_t st);
 int halo_tile_m();

@@ -250,23 +250,84 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
     const int hh = rem / a.wc, ww = rem - hh * a.wc;
     return ((long)nb * a.OH + hh * a.ostride + a.ph) * a.OW + ww * a.ostride + a.pw;
   };
+  // post-op aux values, loaded first so their latency overlaps the rounding pass
+  uint2 zr[FC][FP];
+  if (a.post) {
+#pragma unroll
+    for (int c = 0; c < FC; ++c) {
+      const int nb = n0 + wn * WTN + c * 16 + kg * 4;
+#pragma unroll
+      for (int p = 0; p < FP; ++p) {
+        const bool ok = nb < a.Ng && p * 16 + j16 < cnt;
+        zr[c][p] = ok ? *reinterpret_cast<const uint2*>((const bf16*)a.aux + out_pix(row0 + p * 16 + j16) * a.ld_aux + nb)
+                      : uint2{0u, 0u};
+      }
+    }
+  }
 #pragma unroll
   for (int p = 0; p < FP; ++p) {
     const bool mok = p * 16 + j16 < cnt;
 #pragma unroll
     for (int c = 0; c < FC; ++c) {
-      bf16 ob[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float v = acc[c][p][e] + bias[c][e];
         if (a.relu) v = fmaxf(v, 0.f);
-        ob[e] = (bf16)v;
-        acc[c][p][e] = mok ? (float)ob[e] : 0.f;  // BN statistics are of the stored (rounded) values
+        acc[c][p][e] = mok ? (float)(bf16)v : 0.f;  // BN statistics are of the stored (rounded) values
         csum[c][e] += acc[c][p][e];
       }
-      *reinterpret_cast<uint2*>(tl + (p * 16 + j16) * LROW + (c * 16 + kg * 4) * 2) = *reinterpret_cast<uint2*>(ob);
     }
   }
+  if (a.post) {
+    // mask the rounded gradient with the producer's ReLU (recomputed from aux) and reduce its
+    // backward partials over the wave's rows: q0 = sum d, q1 = sum d * xhat (BN)
+#pragma unroll
+    for (int c = 0; c < FC; ++c) {
+      const int nb = n0 + wn * WTN + c * 16 + kg * 4;
+      const bool nok = nb < a.Ng;
+      float sc4[4], sh4[4], mu4[4], iv4[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool bn = a.post == 2 && nok;
+        sc4[e] = bn ? a.psc[nb + e] : 0.f;
+        sh4[e] = bn ? a.psh[nb + e] : 0.f;
+        mu4[e] = bn ? a.pmean[nb + e] : 0.f;
+        iv4[e] = bn ? a.pinv[nb + e] : 0.f;
+      }
+      float q0[4] = {0.f, 0.f, 0.f, 0.f}, q1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < FP; ++p) {
+        const bf16* z = reinterpret_cast<const bf16*>(&zr[c][p]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float zf = (float)z[e];
+          const bool on = a.post == 2 ? fmaf(zf, sc4[e], sh4[e]) > 0.f : zf > 0.f;
+          const float d = on ? acc[c][p][e] : 0.f;
+          acc[c][p][e] = d;
+          q0[e] += d;
+          q1[e] += d * ((zf - mu4[e]) * iv4[e]);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float t0 = row16_sum(q0[e]), t1 = row16_sum(q1[e]);
+        if (j16 == 0) {
+          const int col = wn * WTN + c * 16 + kg * 4 + e;
+          red[wm * BN + col] = t0;
+          red[(NWM + wm) * BN + col] = t1;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < FP; ++p)
+#pragma unroll
+    for (int c = 0; c < FC; ++c) {
+      bf16 ob[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ob[e] = (bf16)acc[c][p][e];  // exact: acc holds rounded values
+      *reinterpret_cast<uint2*>(tl + (p * 16 + j16) * LROW + (c * 16 + kg * 4) * 2) = *reinterpret_cast<uint2*>(ob);
+    }
   if (a.stats) {
 #pragma unroll
     for (int c = 0; c < FC; ++c)
@@ -311,6 +372,22 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
       for (int e = 0; e < 8; ++e) nv[e] = (bf16)((float)nv[e] + (float)ob[e]);
     }
     *reinterpret_cast<uint4*>(ptr) = v;
+  }
+  if (a.post) {
+    // plain sums of the NWM row-waves' partials -> ppart[blockIdx.x][2][Ng]
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int col = tid; col < BN; col += NT) {
+      const int n = n0 + col;
+      if (n >= a.Ng) continue;
+      float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWM; ++w) {
+        t0 += red[w * BN + col];
+        t1 += red[(NWM + w) * BN + col];
+      }
+      a.ppart[(long)blockIdx.x * 2 * a.Ng + n] = t0;
+      a.ppart[(long)blockIdx.x * 2 * a.Ng + a.Ng + n] = t1;
+    }
   }
   if (a.stats) {
     // Chan merge of the NWM row-wave partials -> one (sum, M2) per block row tile (BM rows),
@@ -548,6 +625,10 @@ int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
 // TN configuration: 0 = halo, 1 = 256x64, 2 = 256x128, 3 = 128x128, 4 = 128x128 single stage
 // (one K step: the prefetch stage would only cost occupancy), 5 = 64x128
 static int tn_config(const FastTNArgs& a) {
+  if (const char* e = getenv("UNETSEG_TN_CFG")) {  // experiments: force a configuration (1..5)
+    const int c = atoi(e);
+    if (c >= 1 && c <= 5) return c;
+  }
   if (halo3_ok(a)) return 0;
   const int nsteps = a.nr * a.ns * (a.cin >> 6);
   if (nsteps == 1 && a.Ng > 64) return 4;
@@ -570,6 +651,12 @@ bool tn_fast_ok(const FastTNArgs& a) {
 int tn_fast_tile_m(const FastTNArgs& a) {
   const int cfg = tn_config(a);
   return cfg == 0 ? halo_tile_m() : cfg <= 2 ? 256 : cfg == 5 ? 64 : 128;
+}
+
+int tn_fast_post_rows(const FastTNArgs& a) {
+  if (a.M <= 0 || a.Ng <= 0) return 0;
+  const int cfg = tn_config(a);
+  return cfg == 0 ? halo3_blocks(a) : ceil_div(a.M, cfg <= 2 ? 256 : cfg == 5 ? 64 : 128);
 }
 
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {

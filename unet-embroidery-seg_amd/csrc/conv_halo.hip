@@ -65,6 +65,14 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   (void)ntn;
 
   if (a.bias && tid < 64) sbias[tid] = a.bias[n0 + tid];
+  // BN post-op coefficients of this block's 64 channels live in `red` (free in dgrad: no stats)
+  float* pco = red;  // [4][64]: sc, sh, mean, inv
+  if (a.post == 2 && tid < 64) {
+    pco[tid] = a.psc[n0 + tid];
+    pco[64 + tid] = a.psh[n0 + tid];
+    pco[128 + tid] = a.pmean[n0 + tid];
+    pco[192 + tid] = a.pinv[n0 + tid];
+  }
 
   // ---- resident weights: LDS row (jt, k) = weights of output channel n0+k at halo tap jt ----
   {
@@ -110,6 +118,13 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   };
 
   f32x4 acc[FC][FP];
+  // data-gradient post-op (a.post): running per-lane sums of the masked gradient over all tiles of
+  // this block, reduced once at the end into ppart[blockIdx.x][2][Ng]
+  float pq0[FC][4], pq1[FC][4];
+#pragma unroll
+  for (int c = 0; c < FC; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pq0[c][e] = pq1[c][e] = 0.f;
   if (my_tiles > 0) issue_halo(0, 0);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
@@ -120,6 +135,22 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   for (int t = 0; t < my_tiles; ++t) {
     const int stage = t & 1;
     if (t + 1 < my_tiles) issue_halo(t + 1, stage ^ 1);
+    // post-op: this tile's aux values are loaded now, so their latency hides under the tap loop
+    uint2 zr[FC][FP];
+    if (a.post) {
+      const int sp = slot + t * G_per;
+      const int tw = sp % tiles_w, rest = sp / tiles_w;
+      const int th = rest % tiles_h, nb = rest / tiles_h;
+#pragma unroll
+      for (int p = 0; p < FP; ++p) {
+        const int r = wid * RPW + p / (HW_TW / 16);
+        const int col = (p % (HW_TW / 16)) * 16 + j16;
+        const long opix = ((long)nb * a.OH + th * TH + r) * a.OW + tw * HW_TW + col;
+#pragma unroll
+        for (int c = 0; c < FC; ++c)
+          zr[c][p] = *reinterpret_cast<const uint2*>((const bf16*)a.aux + opix * a.ld_aux + n0 + c * 16 + kg * 4);
+      }
+    }
 #pragma unroll
     for (int c = 0; c < FC; ++c)
 #pragma unroll
@@ -191,6 +222,27 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
         for (int e = 0; e < 4; ++e) {
           o[e] = (bf16)v[e];
           v[e] = (float)o[e];
+        }
+        if (a.post) {  // mask with the producer's ReLU (from aux) and accumulate backward partials
+          const bf16* z = reinterpret_cast<const bf16*>(&zr[c][p]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float zf = (float)z[e];
+            bool on = zf > 0.f;
+            float xh = 0.f;
+            if (a.post == 2) {
+              const int ch = cb + e;
+              on = fmaf(zf, pco[ch], pco[64 + ch]) > 0.f;
+              xh = (zf - pco[128 + ch]) * pco[192 + ch];
+            }
+            v[e] = on ? v[e] : 0.f;
+            o[e] = (bf16)v[e];
+            pq0[c][e] += v[e];
+            pq1[c][e] += v[e] * xh;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
           csum[c][e] += v[e];
           acc[c][p][e] = v[e];
         }
@@ -256,6 +308,29 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(FP * FC) : "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a.post) {
+    // lanes -> waves -> block: ppart[blockIdx.x][2][Ng] for this block's 64 output channels (the
+    // halo stages are free now: every wave has passed the last tile's barrier)
+    float* pr = reinterpret_cast<float*>(hl);  // [NW][2][64]
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float t0 = row16_sum(pq0[c][e]), t1 = row16_sum(pq1[c][e]);
+        if (j16 == 0) {
+          pr[(wid * 2 + 0) * 64 + c * 16 + kg * 4 + e] = t0;
+          pr[(wid * 2 + 1) * 64 + c * 16 + kg * 4 + e] = t1;
+        }
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (tid < 128) {
+      const int k = tid >> 6, ch = tid & 63;
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += pr[(w * 2 + k) * 64 + ch];
+      a.ppart[(long)blockIdx.x * 2 * a.Ng + k * a.Ng + n0 + ch] = t;
+    }
+  }
 }
 
 
@@ -436,6 +511,16 @@ static int launch_halo3_cfg(const FastTNArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((halo3_kernel<TH, NW>), dim3(ntn * G_per), dim3(64 * NW), lds, st, a, tiles_w, tiles_h, n_sp,
                      G_per, y_bytes);
   return 0;
+}
+
+// blocks (= post-op partial rows) of a launch_halo3 call
+int halo3_blocks(const FastTNArgs& a) {
+  const int n_sp = (a.M / (a.hc * a.wc)) * (a.hc / 8) * (a.wc / HW_TW);
+  const int ntn = a.Ng / 64;
+  int G_per = 256 / ntn;
+  if (G_per < 1) G_per = 1;
+  if (G_per > n_sp) G_per = n_sp;
+  return ntn * G_per;
 }
 
 int launch_halo3(const FastTNArgs& a, hipStream_t st) {

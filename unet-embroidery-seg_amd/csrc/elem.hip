@@ -396,6 +396,38 @@ __global__ __launch_bounds__(256) void relu_bwd_bias_kernel(const T* dA, int ldd
   store_partials<1, V>(s, tv, c0, C, G, part, red);
 }
 
+// The same coefficients from the row partials of a fused data-gradient post-op
+// (unetseg_conv2d_dgrad_post): part[g][2][C] = (sum dz, sum dz*xhat) per row tile.
+__global__ void bn_bwd_finalize_rows_kernel(const float* part, int C, int G, long M, const float* g1,
+                                            const float* inv1, float* dg1, float* db1, float* coef) {
+  __shared__ double sc[16];
+  const int c = blockIdx.x;
+  double a0 = 0.0, a1 = 0.0;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    a0 += part[(long)g * 2 * C + c];
+    a1 += part[(long)g * 2 * C + C + c];
+  }
+  a0 = block_sum(a0, sc);
+  a1 = block_sum(a1, sc);
+  if (threadIdx.x == 0) {
+    dg1[c] += (float)a1;
+    db1[c] += (float)a0;
+    coef[0 * C + c] = g1[c] * inv1[c];
+    coef[1 * C + c] = (float)(a0 / (double)M);
+    coef[2 * C + c] = (float)(a1 / (double)M);
+  }
+}
+
+// out[c] (+)= sum_g part[g][k][c] for part [G][2][C] (bias gradient from the fused ReLU post-op)
+__global__ void colsum_rows_kernel(const float* part, int C, int G, int k, float* out, int accumulate) {
+  __shared__ double sc[16];
+  const int c = blockIdx.x;
+  double acc = 0.0;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) acc += part[(long)g * 2 * C + k * C + c];
+  acc = block_sum(acc, sc);
+  if (threadIdx.x == 0) out[c] = accumulate ? out[c] + (float)acc : (float)acc;
+}
+
 // out[c] (+)= sum_g part[c][g]   (fp64 accumulation, fixed order)
 __global__ void colsum_finalize_kernel(const float* part, int C, int G, float* out, int accumulate) {
   __shared__ double sc[16];
@@ -1102,6 +1134,21 @@ UNETSEG_API int unetseg_relu_bwd_bias(int dtype, const void* dA, int ldd, const 
   DISPATCH_T(dtype, hipLaunchKernelGGL(relu_bwd_bias_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream,
                                        (const T*)dA, ldd, (const T*)A, lda, (T*)dY, ldy, M, C, tv, ppb, part, G));
   US_LAUNCH_CHECK("relu_bwd_bias");
+  return 0;
+}
+
+UNETSEG_API int unetseg_bn_bwd_finalize_rows(const float* part, int C, int G, long M, const float* g1,
+                                             const float* inv1, float* dg1, float* db1, float* coef, void* stream) {
+  US_CHECK_ARG(part && g1 && inv1 && dg1 && db1 && coef && M > 0, "bn_bwd_finalize_rows: bad args");
+  hipLaunchKernelGGL(bn_bwd_finalize_rows_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, C, G, M, g1, inv1,
+                     dg1, db1, coef);
+  US_LAUNCH_CHECK("bn_bwd_finalize_rows");
+  return 0;
+}
+
+UNETSEG_API int unetseg_colsum_rows(const float* part, int C, int G, int k, float* out, int accumulate, void* stream) {
+  hipLaunchKernelGGL(colsum_rows_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, C, G, k, out, accumulate);
+  US_LAUNCH_CHECK("colsum_rows");
   return 0;
 }
 

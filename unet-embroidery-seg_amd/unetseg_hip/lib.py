@@ -68,6 +68,10 @@ SIGNATURES = {
     "unetseg_ce_fwd": (I, [P, P, I, I, P, P, P]),
     "unetseg_scale_grad": (I, [P, L, P, F, P, F, P, P]),
     "unetseg_stream_wait": (I, [P, P]),
+    "unetseg_conv2d_dgrad_post": (I, [I, P, I, I, I, I, P, I, I, I, I, I, I, P, I, I, I, I, P, I, P, P, P, P, P, I,
+                                      P]),
+    "unetseg_bn_bwd_finalize_rows": (I, [P, I, I, L, P, P, P, P, P, P]),
+    "unetseg_colsum_rows": (I, [P, I, I, I, P, I, P]),
     "unetseg_adam_dev": (I, [P, P, P, P, L, P, P, F, F, F, F, P, P]),
 }
 
@@ -110,7 +114,8 @@ class _Caller:
     def __getattr__(self, item):
         fn = getattr(load(), "unetseg_" + item)
         if SIGNATURES["unetseg_" + item][0] is I and item not in ("reduce_tiles", "pw_small_tiles", "conv_tile_m",
-                                                                    "abi_version", "conv2d_fwd_tile_m"):
+                                                                    "abi_version", "conv2d_fwd_tile_m",
+                                                                    "conv2d_dgrad_post"):
             def call(*args):
                 rc = fn(*args)
                 if rc != 0:

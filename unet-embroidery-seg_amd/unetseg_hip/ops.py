@@ -31,16 +31,33 @@ def ldp(t):
 
 
 class Node:
-    __slots__ = ("data", "grad", "need_grad")
+    """An activation.  ``uses`` counts the ops that consumed it; ``fuse`` describes the ReLU that
+    produced it, so that a sole consumer conv can apply that op's backward mask and first reduction
+    in its data-gradient epilogue (``fused`` then holds the partials for the producer's backward)."""
+
+    __slots__ = ("data", "grad", "need_grad", "uses", "fuse", "fused")
 
     def __init__(self, data, need_grad=True):
         self.data = data
         self.grad = None
         self.need_grad = need_grad
+        self.uses = 0
+        self.fuse = None
+        self.fused = None
 
     @property
     def shape(self):
         return self.data.shape
+
+
+def use(*nodes):
+    for n in nodes:
+        if n is not None:
+            n.uses += 1
+
+
+#: fuse ReLU / BN-ReLU backward pass 1 into the consumer conv's dgrad (UNETSEG_NO_FUSE=1 disables)
+FUSE = os.environ.get("UNETSEG_NO_FUSE", "0") != "1"
 
 
 _WORKSPACES = {}
@@ -240,6 +257,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
     """y = conv(cat[x1, x2]) (+bias if the conv has one, ReLU).  Stride/padding come from the
     Conv2d container.  Returns (Node y, BN partials or None)."""
     stride, pad = pc.conv.stride, pc.conv.padding
+    use(x1, x2)
     X1 = x1.data
     N, H, W, C1 = X1.shape
     X2 = x2.data if x2 is not None else None
@@ -260,13 +278,21 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
         lib.conv2d_fwd(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride, pad,
                        P(b), int(relu), P(y), K, P(st[0] if st else None), ctx.stream)
     out = Node(y)
+    if relu:
+        out.fuse = (1, y, None)
 
     def bwd():
         dA = out.grad
         if dA is None:
             return
         dev = ctx.device
-        if relu:
+        if relu and out.fused is not None:
+            # the consumer's dgrad stored the masked gradient and the bias partials
+            part, rows = out.fused
+            dY = dA
+            if b is not None:
+                lib.colsum_rows(P(part), K, rows, 0, P(b.grad), 1, ctx.stream)
+        elif relu:
             Gr = lib.reduce_tiles(ctx.dt, M, K, None, None)
             part = ctx.f32(K, Gr)
             dY = ctx.empty(N, Pq, Qq, K)
@@ -298,7 +324,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
         ctx.param_done(pc.conv.weight, b)
         # data gradient
         if x2 is None:
-            if x1.need_grad:
+            if x1.need_grad and not _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
                 g, acc = gbuf(ctx, x1)
                 with _probe("igemm_tn", flops, stride * stride, ("dgrad",) + desc):
                     lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, R, S, stride, pad, P(g),
@@ -313,6 +339,36 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
 
     ctx.push(bwd)
     return out, st
+
+
+def _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
+    """dgrad into x1.grad with the backward mask + first reduction of the ReLU / BN-ReLU that
+    produced x1 fused into the epilogue.  Only when this conv is x1's sole consumer (so its dgrad
+    is x1's whole gradient) and the shape has a fused kernel; returns False otherwise."""
+    if not (FUSE and x1.fuse is not None and x1.grad is None and x1.uses == 1 and ctx.dt == DT_BF16):
+        return False
+    kind, aux, st = x1.fuse
+    K, R, S = pc.K, pc.R, pc.S
+    stride, pad = pc.conv.stride, pc.conv.padding
+    args = [ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, R, S, stride, pad]
+    coeffs = [P(st.sc), P(st.sh), P(st.mean), P(st.inv)] if kind == 2 else [0, 0, 0, 0]
+    rows = lib.conv2d_dgrad_post(*args, 0, C1, H, W, kind, P(aux), ldp(aux), *coeffs, 0, 0, ctx.stream)
+    if rows <= 0:
+        return False
+    g = ctx.empty(N, H, W, C1)
+    part = ctx.f32(rows, 2, C1)
+    with _probe("igemm_tn", flops, stride * stride, ("dgrad",) + desc):
+        rc = lib.conv2d_dgrad_post(*args, P(g), C1, H, W, kind, P(aux), ldp(aux), *coeffs, P(part), rows, ctx.stream)
+    if rc != 0:
+        raise RuntimeError(f"unetseg_conv2d_dgrad_post failed ({rc}): {lib_last_error()}")
+    x1.grad = g
+    x1.fused = (part, rows)
+    return True
+
+
+def lib_last_error():
+    from .lib import last_error
+    return last_error()
 
 
 class BNState:
@@ -344,6 +400,7 @@ def _bn_coeffs(ctx, bn, st, M, tile=None):
 def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None):
     """a = act(BN(y) [+ res | + BN2(y2)]).  y: conv output Node with partial stats st.
     res: raw residual Node; res_bn: (Node y2, stats2, bn module 2)."""
+    use(y, res, res_bn[0] if res_bn is not None else None)
     Y = y.data
     N, H, W, C = Y.shape
     M = N * H * W
@@ -358,6 +415,9 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None):
     lib.bn_apply(ctx.dt, P(Y), ldp(Y), P(s1.sc), P(s1.sh), P(R), ldp(R), P(s2.sc if s2 else None),
                  P(s2.sh if s2 else None), mode, int(relu), P(a), C, M, C, ctx.stream)
     out = Node(a)
+    plain_relu = relu and res is None and res_bn is None
+    if plain_relu and ctx.training:
+        out.fuse = (2, Y, s1)
 
     def bwd():
         dA = out.grad
@@ -365,6 +425,18 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None):
             return
         if not ctx.training:
             raise NotImplementedError("backward through eval-mode BatchNorm is not on the hot path")
+        if out.fused is not None:
+            # the consumer's dgrad stored dz = dA * mask and the (sum dz, sum dz*xhat) row partials
+            part, rows = out.fused
+            coef = ctx.f32(6, C)
+            lib.bn_bwd_finalize_rows(P(part), C, rows, M, P(bnm.weight), P(s1.inv), P(bnm.weight.grad),
+                                     P(bnm.bias.grad), P(coef), ctx.stream)
+            ctx.param_done(bnm.weight, bnm.bias)
+            dy1, acc1 = gbuf(ctx, y)
+            assert acc1 == 0
+            lib.bn_bwd_apply(ctx.dt, P(dA), ldp(dA), 0, C, 0, 0, P(Y), ldp(Y), P(s1.mean), P(s1.inv),
+                             P(dy1), ldp(dy1), 0, 0, 0, 0, 0, 0, P(coef), 0, 0, 0, M, C, ctx.stream)
+            return
         Gr = lib.reduce_tiles(ctx.dt, M, C, None, None)
         part = ctx.f32(3, C, Gr)
         y2 = res_bn[0] if res_bn is not None else None
@@ -411,6 +483,7 @@ def pool_out(h, k, s, ceil_mode):
 
 
 def maxpool(ctx, x, k, s, ceil_mode):
+    use(x)
     X = x.data
     N, H, W, C = X.shape
     Pq, Qq = pool_out(H, k, s, ceil_mode), pool_out(W, k, s, ceil_mode)
@@ -431,6 +504,7 @@ def maxpool(ctx, x, k, s, ceil_mode):
 
 
 def upsample2x(ctx, x, align_corners):
+    use(x)
     X = x.data
     N, H, W, C = X.shape
     y = ctx.empty(N, 2 * H, 2 * W, C)
@@ -450,6 +524,7 @@ def upsample2x(ctx, x, align_corners):
 
 def pw_head(ctx, x, conv_mod):
     """1x1 conv with Cout in {1,2} -> fp32 NCHW logits (the reference's output layout)"""
+    use(x)
     X = x.data
     N, H, W, C = X.shape
     K = conv_mod.weight.shape[0]
@@ -480,6 +555,7 @@ def pw_head(ctx, x, conv_mod):
 def attention_gate(ctx, skip, gate, gm, pth, pph):
     """model/unet_attention.py:30-35.  gm: AttentionGate container; pth/pph: packed theta/phi convs.
     Returns the gated skip Node (skip * alpha)."""
+    use(skip)  # read again by attn_apply
     th, st_t = conv(ctx, skip, pth, stats=True)
     ph, st_p = conv(ctx, gate, pph, stats=True)
     f = bn(ctx, th, st_t, gm.theta[1], relu=True, res_bn=(ph, st_p, gm.phi[1]))
@@ -528,6 +604,7 @@ def attention_gate(ctx, skip, gate, gm, pth, pph):
 
 def cls_head(ctx, feat, head, dropout_mask=None, seed=0):
     """model/unet_multitask.py:73-80: GAP -> FC 2048->512 -> ReLU -> Dropout(0.5) -> FC 512->3"""
+    use(feat)
     X = feat.data
     N, H, W, C = X.shape
     fc1, fc2 = head[2], head[5]
