@@ -38,6 +38,7 @@ struct FastTNArgs {
   const float* pmean;
   const float* pinv;
   float* ppart;
+  int t2d;  // rows of a 2D spatial tile (BM = t2d x 32 pixels), 0 = row-major GEMM rows (set by the launcher)
 };
 
 struct FastWgradArgs {

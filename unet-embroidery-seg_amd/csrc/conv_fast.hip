@@ -32,7 +32,7 @@ namespace {
 template <int BM, int BN, int NWM, int NWN>
 constexpr int tn_waves_per_simd() { return (BM == 64) ? 3 : 2; }
 
-template <int BM, int BN, int NWM, int NWN, int ST>
+template <int BM, int BN, int NWM, int NWN, int ST, bool POST>
 __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN>())) void tn_fast_kernel(FastTNArgs a) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int WTM = BM / NWM, WTN = BN / NWN;
@@ -45,9 +45,28 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / NWN, wn = wid % NWN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (dispatch id d -> XCD
+  // d % 8), each with its own L2.  Give every XCD a contiguous range of tiles, N tiles fastest, so
+  // the N tiles of one row tile and the neighbouring row tiles (the 3x3 taps re-read them) share
+  // one L2.  Bijective for any tile count.
+  const int ntiles = gridDim.x * gridDim.y;
+  const int did = blockIdx.x + gridDim.x * blockIdx.y;
+  const int xq = ntiles >> 3, xr = ntiles & 7, xcd = did & 7;
+  const int lin = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (did >> 3);
+  const int tile_m = lin / gridDim.y, tile_n = lin - tile_m * gridDim.y;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int kv = tid & 7, rb = tid >> 3;
   const int hw = a.hc * a.wc;
+  // GEMM row -> linear pixel of the (hc, wc) grid.  With a.t2d = TR, a BM-row tile is a TR x 32
+  // spatial block instead of BM consecutive pixels of one image row: the nine taps then re-read
+  // one (TR+2) x 34 footprint, which stays in the XCD's L2 while the chunk's taps run.
+  auto row_pix = [&](int m) -> int {
+    if (!a.t2d) return m;
+    const int TR = a.t2d, tsz = TR * 32, tpr = a.wc >> 5;
+    const int t = m / tsz, i = m - t * tsz;
+    const int rest = t / tpr, tw = t - rest * tpr;
+    return (rest * TR + (i >> 5)) * a.wc + (tw << 5) + (i & 31);
+  };
 
   const __amdgpu_buffer_rsrc_t r1 = srd(a.x1, a.x1_bytes);
   const __amdgpu_buffer_rsrc_t r2 = srd(a.x2 ? a.x2 : a.x1, a.x2 ? a.x2_bytes : 0u);
@@ -61,7 +80,8 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
     pix[i] = 0;
     vmask[i] = 0u;
     if (m < a.M) {
-      const int nb = m / hw, rem = m - nb * hw;
+      const int pm = row_pix(m);
+      const int nb = pm / hw, rem = pm - nb * hw;
       const int hh = rem / a.wc, ww = rem - hh * a.wc;
       const int ih0 = hh * a.istride, iw0 = ww * a.istride;
       pix[i] = (nb * a.H + ih0) * a.W + iw0;
@@ -119,10 +139,14 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) rbv[i] = bload(rw, (!live || boff[i] == kOOB) ? kOOB : boff[i] + wofs);
-    s_c += 64;
-    if (s_c >= a.cin) {
-      s_c = 0;
-      if (++s_js == a.ns) { s_js = 0; ++s_jr; }
+    // K order: taps fastest, 64-channel chunks outer -- the nine taps of one chunk run back to
+    // back over the same input footprint (L2-resident), instead of cycling through every chunk
+    if (++s_js == a.ns) {
+      s_js = 0;
+      if (++s_jr == a.nr) {
+        s_jr = 0;
+        s_c += 64;
+      }
     }
   };
   auto sstore = [&](int buf, const uint4 (&ra)[A_PER], const uint4 (&rbv)[B_PER]) {
@@ -244,7 +268,8 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias[c][e] = (a.bias && nb + e < a.Ng) ? a.bias[nb + e] : 0.f;
   }
-  auto out_pix = [&](int m) -> long {
+  auto out_pix = [&](int m0_) -> long {
+    const int m = row_pix(m0_);
     if (a.ostride == 1 && a.ph == 0 && a.pw == 0 && a.OW == a.wc && a.OH == a.hc) return m;
     const int nb = m / hw, rem = m - nb * hw;
     const int hh = rem / a.wc, ww = rem - hh * a.wc;
@@ -252,7 +277,7 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
   };
   // post-op aux values, loaded first so their latency overlaps the rounding pass
   uint2 zr[FC][FP];
-  if (a.post) {
+  if (POST) {
 #pragma unroll
     for (int c = 0; c < FC; ++c) {
       const int nb = n0 + wn * WTN + c * 16 + kg * 4;
@@ -278,7 +303,7 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
       }
     }
   }
-  if (a.post) {
+  if (POST) {
     // mask the rounded gradient with the producer's ReLU (recomputed from aux) and reduce its
     // backward partials over the wave's rows: q0 = sum d, q1 = sum d * xhat (BN)
 #pragma unroll
@@ -373,8 +398,8 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
     }
     *reinterpret_cast<uint4*>(ptr) = v;
   }
-  if (a.post) {
-    // plain sums of the NWM row-waves' partials -> ppart[blockIdx.x][2][Ng]
+  if (POST) {
+    // plain sums of the NWM row-waves' partials -> ppart[tile_m][2][Ng]
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     for (int col = tid; col < BN; col += NT) {
       const int n = n0 + col;
@@ -385,13 +410,13 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
         t0 += red[w * BN + col];
         t1 += red[(NWM + w) * BN + col];
       }
-      a.ppart[(long)blockIdx.x * 2 * a.Ng + n] = t0;
-      a.ppart[(long)blockIdx.x * 2 * a.Ng + a.Ng + n] = t1;
+      a.ppart[(long)tile_m * 2 * a.Ng + n] = t0;
+      a.ppart[(long)tile_m * 2 * a.Ng + a.Ng + n] = t1;
     }
   }
   if (a.stats) {
     // Chan merge of the NWM row-wave partials -> one (sum, M2) per block row tile (BM rows),
-    // written contiguously: stats[blockIdx.x][2][Ng].  Raw barrier: LDS visibility only -- a
+    // written contiguously: stats[tile_m][2][Ng].  Raw barrier: LDS visibility only -- a
     // __syncthreads() would also wait for this block's output stores to retire.
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     for (int col = tid; col < BN; col += NT) {
@@ -413,8 +438,8 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
           q += red[(NWM + w) * BN + col] + nw * d * d;
         }
       }
-      a.stats[(long)blockIdx.x * 2 * a.Ng + n] = st;
-      a.stats[(long)blockIdx.x * 2 * a.Ng + a.Ng + n] = q;
+      a.stats[(long)tile_m * 2 * a.Ng + n] = st;
+      a.stats[(long)tile_m * 2 * a.Ng + a.Ng + n] = q;
     }
   }
 }
@@ -604,7 +629,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     }
 }
 
-template <int BM, int BN, int NWM, int NWN, int ST>
+template <int BM, int BN, int NWM, int NWN, int ST, bool POST = false>
 int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   constexpr int NT = 64 * NWM * NWN;
   // operand stages, or the epilogue's per-wave transpose tiles + stats scratch if larger
@@ -613,12 +638,17 @@ int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   const size_t lds = stages > epi ? stages : epi;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_fast_kernel<BM, BN, NWM, NWN, ST>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_fast_kernel<BM, BN, NWM, NWN, ST, POST>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   dim3 grid(ceil_div(a.M, BM), ceil_div(a.Ng, BN), 1);
-  hipLaunchKernelGGL((tn_fast_kernel<BM, BN, NWM, NWN, ST>), grid, dim3(NT), lds, st, a);
+  FastTNArgs b = a;
+  constexpr int TR = BM / 32;
+  // 2D spatial tiles measured slower than row-major tiles with the chunk-outer K order: opt-in
+  static const bool t2d = getenv("UNETSEG_T2D") != nullptr;
+  b.t2d = (t2d && a.nr * a.ns > 1 && a.wc % 32 == 0 && a.wc > 32 && a.hc % TR == 0) ? TR : 0;
+  hipLaunchKernelGGL((tn_fast_kernel<BM, BN, NWM, NWN, ST, POST>), grid, dim3(NT), lds, st, b);
   return 0;
 }
 
@@ -663,11 +693,11 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
   if (a.M <= 0 || a.Ng <= 0) return 0;
   switch (tn_config(a)) {
     case 0: return launch_halo3(a, st);
-    case 1: return launch_tn_cfg<256, 64, 4, 1, 2>(a, st);
-    case 2: return launch_tn_cfg<256, 128, 4, 2, 3>(a, st);
-    case 4: return launch_tn_cfg<128, 128, 2, 2, 1>(a, st);
-    case 5: return launch_tn_cfg<64, 128, 1, 4, 3>(a, st);
-    default: return launch_tn_cfg<128, 128, 2, 2, 3>(a, st);
+    case 1: return a.post ? launch_tn_cfg<256, 64, 4, 1, 2, true>(a, st) : launch_tn_cfg<256, 64, 4, 1, 2>(a, st);
+    case 2: return a.post ? launch_tn_cfg<256, 128, 4, 2, 3, true>(a, st) : launch_tn_cfg<256, 128, 4, 2, 3>(a, st);
+    case 4: return a.post ? launch_tn_cfg<128, 128, 2, 2, 1, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 1>(a, st);
+    case 5: return a.post ? launch_tn_cfg<64, 128, 1, 4, 3, true>(a, st) : launch_tn_cfg<64, 128, 1, 4, 3>(a, st);
+    default: return a.post ? launch_tn_cfg<128, 128, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 3>(a, st);
   }
 }
 

@@ -33,7 +33,7 @@ __device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, unsigned off,
   asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
 }
 
-template <int TH, int NW>
+template <int TH, int NW, int POST>
 __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_w, int tiles_h, int n_sp, int G_per,
                                                         unsigned y_bytes) {
   // wave w owns output rows [w*TH/NW, (w+1)*TH/NW)
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   if (a.bias && tid < 64) sbias[tid] = a.bias[n0 + tid];
   // BN post-op coefficients of this block's 64 channels live in `red` (free in dgrad: no stats)
   float* pco = red;  // [4][64]: sc, sh, mean, inv
-  if (a.post == 2 && tid < 64) {
+  if (POST == 2 && tid < 64) {
     pco[tid] = a.psc[n0 + tid];
     pco[64 + tid] = a.psh[n0 + tid];
     pco[128 + tid] = a.pmean[n0 + tid];
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     if (t + 1 < my_tiles) issue_halo(t + 1, stage ^ 1);
     // post-op: this tile's aux values are loaded now, so their latency hides under the tap loop
     uint2 zr[FC][FP];
-    if (a.post) {
+    if (POST) {
       const int sp = slot + t * G_per;
       const int tw = sp % tiles_w, rest = sp / tiles_w;
       const int th = rest % tiles_h, nb = rest / tiles_h;
@@ -223,14 +223,14 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
           o[e] = (bf16)v[e];
           v[e] = (float)o[e];
         }
-        if (a.post) {  // mask with the producer's ReLU (from aux) and accumulate backward partials
+        if (POST) {  // mask with the producer's ReLU (from aux) and accumulate backward partials
           const bf16* z = reinterpret_cast<const bf16*>(&zr[c][p]);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float zf = (float)z[e];
             bool on = zf > 0.f;
             float xh = 0.f;
-            if (a.post == 2) {
+            if (POST == 2) {
               const int ch = cb + e;
               on = fmaf(zf, pco[ch], pco[64 + ch]) > 0.f;
               xh = (zf - pco[128 + ch]) * pco[192 + ch];
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
             v[e] = on ? v[e] : 0.f;
             o[e] = (bf16)v[e];
             pq0[c][e] += v[e];
-            pq1[c][e] += v[e] * xh;
+            if (POST == 2) pq1[c][e] += v[e] * xh;
           }
         }
 #pragma unroll
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(FP * FC) : "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (a.post) {
+  if (POST) {
     // lanes -> waves -> block: ppart[blockIdx.x][2][Ng] for this block's 64 output channels (the
     // halo stages are free now: every wave has passed the last tile's barrier)
     float* pr = reinterpret_cast<float*>(hl);  // [NW][2][64]
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     for (int c = 0; c < FC; ++c)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float t0 = row16_sum(pq0[c][e]), t1 = row16_sum(pq1[c][e]);
+        const float t0 = row16_sum(pq0[c][e]), t1 = POST == 2 ? row16_sum(pq1[c][e]) : 0.f;
         if (j16 == 0) {
           pr[(wid * 2 + 0) * 64 + c * 16 + kg * 4 + e] = t0;
           pr[(wid * 2 + 1) * 64 + c * 16 + kg * 4 + e] = t1;
@@ -491,7 +491,7 @@ bool halo3_ok(const FastTNArgs& a) {
   return true;
 }
 
-template <int TH, int NW>
+template <int TH, int NW, int POST>
 static int launch_halo3_cfg(const FastTNArgs& a, hipStream_t st) {
   const int tiles_w = a.wc / HW_TW, tiles_h = a.hc / TH;
   const int n_img = a.M / (a.hc * a.wc);
@@ -503,12 +503,12 @@ static int launch_halo3_cfg(const FastTNArgs& a, hipStream_t st) {
   const size_t lds = halo_lds_bytes<TH, NW>();
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_kernel<TH, NW>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_kernel<TH, NW, POST>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const unsigned y_bytes = (unsigned)((long)a.M * a.ldy * 2);
-  hipLaunchKernelGGL((halo3_kernel<TH, NW>), dim3(ntn * G_per), dim3(64 * NW), lds, st, a, tiles_w, tiles_h, n_sp,
+  hipLaunchKernelGGL((halo3_kernel<TH, NW, POST>), dim3(ntn * G_per), dim3(64 * NW), lds, st, a, tiles_w, tiles_h, n_sp,
                      G_per, y_bytes);
   return 0;
 }
@@ -525,7 +525,10 @@ int halo3_blocks(const FastTNArgs& a) {
 
 int launch_halo3(const FastTNArgs& a, hipStream_t st) {
   static const int nw = getenv("UNETSEG_HALO_W4") ? 4 : 8;
-  return nw == 4 ? launch_halo3_cfg<8, 4>(a, st) : launch_halo3_cfg<8, 8>(a, st);
+  // fused dgrad post-ops are separate instantiations: their registers must not cost the plain path
+  if (a.post == 1) return launch_halo3_cfg<8, 8, 1>(a, st);
+  if (a.post == 2) return launch_halo3_cfg<8, 8, 2>(a, st);
+  return nw == 4 ? launch_halo3_cfg<8, 4, 0>(a, st) : launch_halo3_cfg<8, 8, 0>(a, st);
 }
 
 bool halo3_wgrad_ok(const HaloWgradArgs& a) {
