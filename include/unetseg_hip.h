@@ -83,6 +83,18 @@ size_t unetseg_conv2d_wgrad_workspace(int dtype, int n, int p, int q, int cout, 
 int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h,
                          int w, const void* dy, int ldy, int cout, int r, int s, int stride, int pad, float* ws,
                          size_t ws_bytes, float* dw, int dw_c, int accumulate, void* stream);
+
+/* ---- ResNet stem on the fast kernels (model/resnet_backbone.py:126-131, conv 7x7/s2/p3) -------
+   xp: width-padded bf16 [n][h][w+8][8] from unetseg_pack_input_stem (image column at +3);
+   wk: bf16 [K][7][64] from unetseg_stem_pack_weight (k, filter row, filter col*8 + channel) */
+int unetseg_pack_input_stem(const float* x, int n, int c, int h, int w, void* xp, void* stream);
+int unetseg_stem_pack_weight(const float* w, int K, int C, void* wk, void* stream);
+int unetseg_stem_fwd_tile_m(int n, int h, int w, int K);
+int unetseg_stem_fwd(const void* xp, int n, int h, int w, const void* wk, int K, void* y, int ldy, float* stats,
+                     void* stream);
+size_t unetseg_stem_wgrad_workspace(int n, int h, int w, int K);
+int unetseg_stem_wgrad(const void* xp, int n, int h, int w, const void* dy, int ldy, int K, float* ws,
+                       size_t ws_bytes, float* dw, int C, int accumulate, void* stream);
 /* NCHW fp32 input [n][c][h][w] -> NHWC dtype [n][h][w][cpad] (zero channel padding) */
 int unetseg_pack_input(int dtype, const float* x, int n, int c, int h, int w, int cpad, void* y, void* stream);
 

@@ -144,6 +144,38 @@ def test_conv_fwd_dgrad_wgrad(case, dtname):
         assert _rel(dx, xr.grad) < tolg, _rel(dx, xr.grad)
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 64, 64), (1, 37, 50), (3, 32, 96)])
+def test_stem_conv_fast(N, H, W):
+    """ResNet stem (7x7/s2/p3, 3->64) on the width-packed fast path (ops.stem_conv) against
+    F.conv2d on the bf16-rounded operands: output, BN partial stats (column sums) and wgrad."""
+    ops, DT_BF16, _ = _ops()
+    from unetseg_hip.nn import Conv2d
+    g = torch.Generator().manual_seed(N * 1000 + H * 10 + W)
+    conv = Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / math.sqrt(147))
+    conv = conv.to(DEV)
+    conv.weight.grad = torch.zeros_like(conv.weight)
+    x = torch.rand(N, 3, H, W, generator=g)
+    ctx = _ctx(DT_BF16)
+    y, (st, tile) = ops.stem_conv(ctx, x.to(DEV), conv)
+    xr = _round(x, DT_BF16)
+    wr = _round(conv.weight.detach().cpu(), DT_BF16).requires_grad_(True)
+    ref = F.conv2d(xr, wr, None, 2, 3)
+    out = _nchw(y.data)
+    assert out.shape == ref.shape
+    assert _rel(out, ref.detach()) < 2e-2
+    # partial stats: column sums over all row tiles == per-channel sum of the stored outputs
+    colsum = st[:, 0, :].sum(0).cpu().double()
+    assert torch.allclose(colsum, out.double().sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    dy = _round(torch.randn(ref.shape, generator=g), DT_BF16)
+    y.grad = _node(dy, DT_BF16).data
+    ctx.backward()
+    torch.cuda.synchronize()
+    ref.backward(dy)
+    assert _rel(conv.weight.grad.cpu(), wr.grad) < 3e-2, _rel(conv.weight.grad.cpu(), wr.grad)
+
+
 @pytest.mark.parametrize("dtname", ["fp32", "bf16"])
 @pytest.mark.parametrize("mode", ["plain", "res", "res_bn"])
 def test_bn_train_fwd_bwd(dtname, mode):

@@ -854,7 +854,7 @@ UNETSEG_API int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1
       FastWgradArgs f{};
       f.x1 = x1; f.x2 = c2 ? x2 : nullptr; f.x1_bytes = (unsigned)b1; f.x2_bytes = (unsigned)b2;
       f.ldc1b = ldc1 * 2; f.ldc2b = ldc2 * 2; f.c1 = c1; f.cin = c1 + c2;
-      f.H = h; f.W = w; f.P = p; f.Q = q; f.stride = stride; f.pad = pad; f.S = s;
+      f.H = h; f.W = w; f.P = p; f.Q = q; f.stride = stride; f.pad = pad; f.padw = pad; f.S = s;
       f.dy = dy; f.dy_bytes = (unsigned)bdy; f.ldyb = ldy * 2; f.Cout = cout; f.Ng = a.Ng; f.Kpix = a.Kpix;
       f.ws = ws;
       splits = wgrad_fast_splits(cout, a.Ng, a.Kpix);
@@ -919,5 +919,117 @@ UNETSEG_API int unetseg_pack_conv_weight(int dtype, const float* w, int K, int C
   else
     hipLaunchKernelGGL(pack_weights_kernel<float>, dim3(blocks), dim3(256), 0, st, w, K, C, R, S, Cpad, (float*)wk, (float*)wt);
   US_LAUNCH_CHECK("pack_weights");
+  return 0;
+}
+
+
+// =========================================================================================
+// ResNet stem (model/resnet_backbone.py:126-131: conv 7x7 / stride 2 / pad 3, 3 -> 64, no bias)
+// on the fast implicit-GEMM kernels.  The input is packed width-padded: xp bf16 [N][H][W+8][8]
+// with image column w at packed column w+3 (zeros around, channels 3..7 zero).  For output
+// column q and filter row r the 8 taps of the row (7 real + 1 zero-weight) then read 8
+// consecutive packed pixels = 128 contiguous bytes, so the conv is a GEMM with K = 7 rows x 64
+// (8 taps x 8 channels): one 64-wide K step per filter row, no per-tap column checks.
+// wk: bf16 [K][7][64] with wk[k][r][s*8+c] = w[k][c][r][s] (s < 7, c < C), else 0.
+// =========================================================================================
+namespace {
+
+__global__ void stem_pack_weight_kernel(const float* w, int K, int C, bf16* wk) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over K*7*64
+  if (i >= K * 7 * 64) return;
+  const int k = i / 448, rem = i - k * 448, r = rem / 64, j = rem - r * 64;
+  const int s = j >> 3, c = j & 7;
+  wk[i] = (bf16)((s < 7 && c < C) ? w[((k * C + c) * 7 + r) * 7 + s] : 0.f);
+}
+
+// dw[k][c][r][s] (+)= v[k][s*8 + c][r]   (c < C, s < 7): the split-reduced virtual gradient
+// (wgrad_reduce_kernel, layout [K][64][7]) permuted into PyTorch's [K][C][7][7]
+__global__ void stem_wgrad_remap_kernel(const float* v, int K, int C, float* dw, int accumulate) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over K*C*49
+  if (i >= K * C * 49) return;
+  const int k = i / (C * 49), rem = i - k * C * 49, c = rem / 49, rs = rem - c * 49;
+  const int r = rs / 7, s = rs - r * 7;
+  const float g = v[((long)k * 64 + s * 8 + c) * 7 + r];
+  dw[i] = accumulate ? dw[i] + g : g;
+}
+
+IgemmArgs stem_args(const void* xp, int n, int h, int w, const void* wk, int K) {
+  IgemmArgs a{};
+  a.x1 = xp; a.x2 = nullptr; a.c1 = 64; a.c2 = 0; a.ldc1 = 8; a.ldc2 = 0;
+  a.N = n; a.H = h; a.W = w + 8;
+  a.hc = (h + 6 - 7) / 2 + 1; a.wc = (w + 6 - 7) / 2 + 1; a.istride = 2;
+  a.r0 = 0; a.rs = 1; a.nr = 7; a.dh0 = -3; a.dhs = 1;
+  a.s0 = 0; a.ss = 1; a.ns = 1; a.dw0 = 0; a.dws = 1;
+  a.S = 1; a.cin = 64; a.wt = wk; a.ldw = 7 * 64; a.Ng = K;
+  a.ostride = 1; a.ph = 0; a.pw = 0; a.OH = a.hc; a.OW = a.wc;
+  a.M = n * a.hc * a.wc;
+  return a;
+}
+
+FastWgradArgs stem_wgrad_args(const void* xp, int n, int h, int w, const void* dy, int ldy, int K) {
+  const int p = (h + 6 - 7) / 2 + 1, q = (w + 6 - 7) / 2 + 1;
+  FastWgradArgs f{};
+  f.x1 = xp; f.x2 = nullptr; f.x1_bytes = (unsigned)((long)n * h * (w + 8) * 16); f.x2_bytes = 0;
+  f.ldc1b = 16; f.ldc2b = 0; f.c1 = 64; f.cin = 64;
+  f.H = h; f.W = w + 8; f.P = p; f.Q = q; f.stride = 2; f.pad = 3; f.padw = 0; f.S = 1;
+  f.dy = dy; f.dy_bytes = (unsigned)((long)n * p * q * ldy * 2); f.ldyb = ldy * 2; f.Cout = K; f.Ng = 7 * 64;
+  f.Kpix = (long)n * p * q;
+  return f;
+}
+
+}  // namespace
+
+UNETSEG_API int unetseg_stem_pack_weight(const float* w, int K, int C, void* wk, void* stream) {
+  US_CHECK_ARG(w && wk && C >= 1 && C <= 8 && K % 8 == 0, "stem_pack_weight: bad args");
+  hipLaunchKernelGGL(stem_pack_weight_kernel, dim3(ceil_div((long)K * 448, 256)), dim3(256), 0, (hipStream_t)stream, w,
+                     K, C, (bf16*)wk);
+  US_LAUNCH_CHECK("stem_pack_weight");
+  return 0;
+}
+
+// row tile of the stem's BN partial statistics (stats is [ceil(M/tile)][2][K])
+UNETSEG_API int unetseg_stem_fwd_tile_m(int n, int h, int w, int K) {
+  IgemmArgs a = stem_args(nullptr, n, h, w, nullptr, K);
+  FastTNArgs f;
+  if (!fast_tn_args(a, f)) return -1;
+  return tn_fast_tile_m(f);
+}
+
+UNETSEG_API int unetseg_stem_fwd(const void* xp, int n, int h, int w, const void* wk, int K, void* y, int ldy,
+                                 float* stats, void* stream) {
+  US_CHECK_ARG(xp && wk && y && K % 8 == 0 && ldy >= K, "stem_fwd: bad args");
+  IgemmArgs a = stem_args(xp, n, h, w, wk, K);
+  a.y = y; a.ldy = ldy; a.accumulate = 0; a.bias = nullptr; a.relu = 0; a.stats = stats;
+  FastTNArgs f;
+  US_CHECK_ARG(fast_tn_args(a, f), "stem_fwd: shape not supported by the fast kernels");
+  launch_tn_fast(f, (hipStream_t)stream);
+  US_LAUNCH_CHECK("stem_fwd");
+  return 0;
+}
+
+// split-K slabs followed by the [K][64][7] reduced virtual gradient
+UNETSEG_API size_t unetseg_stem_wgrad_workspace(int n, int h, int w, int K) {
+  FastWgradArgs f = stem_wgrad_args(nullptr, n, h, w, nullptr, K, K);
+  return ((size_t)wgrad_fast_splits(K, f.Ng, f.Kpix) + 1) * K * f.Ng * sizeof(float);
+}
+
+// dw: fp32 [K][C][7][7] (PyTorch layout), written or accumulated
+UNETSEG_API int unetseg_stem_wgrad(const void* xp, int n, int h, int w, const void* dy, int ldy, int K, float* ws,
+                                   size_t ws_bytes, float* dw, int C, int accumulate, void* stream) {
+  US_CHECK_ARG(xp && dy && ws && dw && K % 64 == 0 && C >= 1 && C <= 8, "stem_wgrad: bad args");
+  FastWgradArgs f = stem_wgrad_args(xp, n, h, w, dy, ldy, K);
+  f.ws = ws;
+  const int splits = wgrad_fast_splits(K, f.Ng, f.Kpix);
+  US_CHECK_ARG(ws_bytes >= ((size_t)splits + 1) * K * f.Ng * sizeof(float), "stem_wgrad: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  launch_wgrad_fast(f, splits, st);
+  // parallel deterministic split reduce into v = ws tail, [K][64 virtual channels][7 rows], then permute
+  float* v = ws + (size_t)splits * K * f.Ng;
+  const long total = (long)K * 64 * 7;
+  hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(ceil_div(total, 16)), dim3(256), 0, st, ws, splits, K, 64, 7, v, 64,
+                     0);
+  hipLaunchKernelGGL(stem_wgrad_remap_kernel, dim3(ceil_div((long)K * C * 49, 256)), dim3(256), 0, st, v, K, C, dw,
+                     accumulate);
+  US_LAUNCH_CHECK("stem_wgrad");
   return 0;
 }

@@ -47,6 +47,7 @@ struct FastWgradArgs {
   unsigned x1_bytes, x2_bytes;
   int ldc1b, ldc2b, c1, cin;
   int H, W, P, Q, stride, pad, S;
+  int padw;                     // column padding (== pad except for the width-packed stem)
   const void* dy;
   unsigned dy_bytes;
   int ldyb, Cout, Ng;

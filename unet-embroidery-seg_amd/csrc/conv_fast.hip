@@ -30,7 +30,7 @@ namespace {
 // waves per SIMD each configuration is sized for (LDS allows that many blocks per CU); caps the
 // register allocation so the two-step register prefetch cannot cost occupancy
 template <int BM, int BN, int NWM, int NWN>
-constexpr int tn_waves_per_simd() { return (BM == 64) ? 3 : 2; }
+constexpr int tn_waves_per_simd() { return (BM == 64 || (BM == 128 && BN == 64)) ? 3 : 2; }
 
 template <int BM, int BN, int NWM, int NWN, int ST, bool POST>
 __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN>())) void tn_fast_kernel(FastTNArgs a) {
@@ -500,7 +500,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
       const int tap = nn / a.cin, c = nn - tap * a.cin;
       const int r = tap / a.S, s = tap - r * a.S;
       b_dh[i] = r - a.pad;
-      b_dw[i] = s - a.pad;
+      b_dw[i] = s - a.padw;
       b_src[i] = c < a.c1 ? 0 : 1;
       b_cb[i] = (unsigned)(c < a.c1 ? c : c - a.c1) * 2u;
     } else {
@@ -655,9 +655,9 @@ int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
 // TN configuration: 0 = halo, 1 = 256x64, 2 = 256x128, 3 = 128x128, 4 = 128x128 single stage
 // (one K step: the prefetch stage would only cost occupancy), 5 = 64x128
 static int tn_config(const FastTNArgs& a) {
-  if (const char* e = getenv("UNETSEG_TN_CFG")) {  // experiments: force a configuration (1..5)
+  if (const char* e = getenv("UNETSEG_TN_CFG")) {  // experiments: force a configuration (1..6)
     const int c = atoi(e);
-    if (c >= 1 && c <= 5) return c;
+    if (c >= 1 && c <= 6) return c;
   }
   if (halo3_ok(a)) return 0;
   const int nsteps = a.nr * a.ns * (a.cin >> 6);
@@ -680,7 +680,7 @@ bool tn_fast_ok(const FastTNArgs& a) {
 // spatial tile on the halo kernel.
 int tn_fast_tile_m(const FastTNArgs& a) {
   const int cfg = tn_config(a);
-  return cfg == 0 ? halo_tile_m() : cfg <= 2 ? 256 : cfg == 5 ? 64 : 128;
+  return cfg == 0 ? halo_tile_m() : cfg <= 2 ? 256 : cfg == 5 ? 64 : 128;  // cfg 6: 128 rows
 }
 
 int tn_fast_post_rows(const FastTNArgs& a) {
@@ -697,6 +697,7 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 2: return a.post ? launch_tn_cfg<256, 128, 4, 2, 3, true>(a, st) : launch_tn_cfg<256, 128, 4, 2, 3>(a, st);
     case 4: return a.post ? launch_tn_cfg<128, 128, 2, 2, 1, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 1>(a, st);
     case 5: return a.post ? launch_tn_cfg<64, 128, 1, 4, 3, true>(a, st) : launch_tn_cfg<64, 128, 1, 4, 3>(a, st);
+    case 6: return a.post ? launch_tn_cfg<128, 64, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 64, 2, 2, 3>(a, st);
     default: return a.post ? launch_tn_cfg<128, 128, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 3>(a, st);
   }
 }

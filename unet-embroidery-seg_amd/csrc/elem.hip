@@ -1218,6 +1218,31 @@ UNETSEG_API int unetseg_pack_input(int dtype, const float* x, int n, int c, int 
   return 0;
 }
 
+// NCHW fp32 image -> width-padded stem layout bf16 [N][H][W+8][8]: image column w at packed column
+// w+3, channels >= C and the 3 + 5 border columns zero (see unetseg_stem_fwd)
+__global__ void pack_input_stem_kernel(const float* x, int N, int C, int H, int W, bf16* y) {
+  const int WP = W + 8;
+  const long total = (long)N * H * WP;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long row = i / WP;
+    const int wp = (int)(i - row * WP), w = wp - 3;
+    const long n = row / H, h = row - n * H;
+    bf16 v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      v[c] = (bf16)((c < C && w >= 0 && w < W) ? x[((n * C + c) * H + h) * (long)W + w] : 0.f);
+    *reinterpret_cast<uint4*>(y + i * 8) = *reinterpret_cast<uint4*>(v);
+  }
+}
+
+UNETSEG_API int unetseg_pack_input_stem(const float* x, int n, int c, int h, int w, void* y, void* stream) {
+  US_CHECK_ARG(x && y && c >= 1 && c <= 8, "pack_input_stem: bad args");
+  hipLaunchKernelGGL(pack_input_stem_kernel, dim3(grid_for((long)n * h * (w + 8))), dim3(256), 0, (hipStream_t)stream,
+                     x, n, c, h, w, (bf16*)y);
+  US_LAUNCH_CHECK("pack_input_stem");
+  return 0;
+}
+
 UNETSEG_API int unetseg_pw_small_tiles(long M) { return ceil_div(M, 2048); }
 
 // y fp32 planar [n][k][hw]; stats (k==1 only, may be NULL): [G][2], G = unetseg_pw_small_tiles(M), tile 2048 px

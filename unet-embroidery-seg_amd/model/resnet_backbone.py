@@ -9,6 +9,7 @@ import math
 import torch.nn as nn
 
 from unetseg_hip import ops
+from unetseg_hip.lib import DT_BF16
 from unetseg_hip.nn import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, Linear, MaxPool2d, ReLU, Seq
 
 
@@ -105,8 +106,11 @@ class ResNet(nn.Module):
 
 def run_resnet(ctx, r, x):
     """resnet_backbone.py:182-201 -> [feat1, ..., feat5] Nodes"""
-    xin = ops.pack_input(ctx, x, 8)
-    y, st = ops.conv(ctx, xin, r.conv1._pc, stats=True)
+    if ctx.dt == DT_BF16 and ops.STEM_FAST:
+        y, st = ops.stem_conv(ctx, x, r.conv1)
+    else:
+        xin = ops.pack_input(ctx, x, 8)
+        y, st = ops.conv(ctx, xin, r.conv1._pc, stats=True)
     feat1 = ops.bn(ctx, y, st, r.bn1, relu=True)
     h = ops.maxpool(ctx, feat1, r.maxpool.kernel_size, r.maxpool.stride, r.maxpool.ceil_mode)
     feats = [feat1]

@@ -72,6 +72,12 @@ SIGNATURES = {
                                       P]),
     "unetseg_bn_bwd_finalize_rows": (I, [P, I, I, L, P, P, P, P, P, P]),
     "unetseg_colsum_rows": (I, [P, I, I, I, P, I, P]),
+    "unetseg_pack_input_stem": (I, [P, I, I, I, I, P, P]),
+    "unetseg_stem_pack_weight": (I, [P, I, I, P, P]),
+    "unetseg_stem_fwd_tile_m": (I, [I, I, I, I]),
+    "unetseg_stem_fwd": (I, [P, I, I, I, P, I, P, I, P, P]),
+    "unetseg_stem_wgrad_workspace": (SZ, [I, I, I, I]),
+    "unetseg_stem_wgrad": (I, [P, I, I, I, P, I, I, P, SZ, P, I, I, P]),
     "unetseg_adam_dev": (I, [P, P, P, P, L, P, P, F, F, F, F, P, P]),
 }
 
@@ -115,7 +121,7 @@ class _Caller:
         fn = getattr(load(), "unetseg_" + item)
         if SIGNATURES["unetseg_" + item][0] is I and item not in ("reduce_tiles", "pw_small_tiles", "conv_tile_m",
                                                                     "abi_version", "conv2d_fwd_tile_m",
-                                                                    "conv2d_dgrad_post"):
+                                                                    "conv2d_dgrad_post", "stem_fwd_tile_m"):
             def call(*args):
                 rc = fn(*args)
                 if rc != 0:

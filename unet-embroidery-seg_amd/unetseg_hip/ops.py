@@ -371,6 +371,58 @@ def lib_last_error():
     return last_error()
 
 
+#: the 7x7/s2 ResNet stem on the fast kernels in bf16 (UNETSEG_NO_FAST_STEM=1: generic conv path)
+STEM_FAST = os.environ.get("UNETSEG_NO_FAST_STEM", "0") != "1"
+
+
+def stem_conv(ctx, x, conv_mod):
+    """model/resnet_backbone.py:126-131 ``conv1`` (7x7, stride 2, pad 3, no bias) from the NCHW fp32
+    image batch, bf16 only: the input is packed width-padded so one filter row's 8 taps x 8 channels
+    are 128 contiguous bytes, and the conv runs as a K = 7 x 64 implicit GEMM on the fast kernels
+    (unetseg_stem_fwd / unetseg_stem_wgrad).  Returns (Node y, BN partial stats) like conv()."""
+    x = x.contiguous()
+    if x.dtype != torch.float32:
+        x = x.float()
+    N, C, H, W = x.shape
+    K = conv_mod.weight.shape[0]
+    xp = ctx.empty(N, H, W + 8, 8)
+    lib.pack_input_stem(P(x), N, C, H, W, P(xp), ctx.stream)
+    wk = ctx.empty(K, 7, 64)
+    lib.stem_pack_weight(P(conv_mod.weight), K, C, P(wk), ctx.stream)
+    Pq, Qq = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    M = N * Pq * Qq
+    y = ctx.empty(N, Pq, Qq, K)
+    tile = lib.stem_fwd_tile_m(N, H, W, K)
+    st = (ctx.f32(math.ceil(M / tile), 2, K), tile)
+    flops = 2.0 * M * K * C * 49
+    desc = (N, H, W, C, 0, K, 7, 7, 2)
+    with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
+        lib.stem_fwd(P(xp), N, H, W, P(wk), K, P(y), K, P(st[0]), ctx.stream)
+    out = Node(y)
+
+    def bwd():
+        dY = out.grad
+        if dY is None:
+            return
+        ws_bytes = lib.stem_wgrad_workspace(N, H, W, K)
+        side = ctx.side
+        if side is not None:
+            lib.stream_wait(side.cuda_stream, ctx.stream)
+            for t in (dY, xp):
+                t.record_stream(side)
+            ws = workspace(ws_bytes, ctx.device, 1)
+            wst = side.cuda_stream
+        else:
+            ws = workspace(ws_bytes, ctx.device)
+            wst = ctx.stream
+        with _probe("wgrad", flops, 1, ("wgrad",) + desc, stream=side):
+            lib.stem_wgrad(P(xp), N, H, W, P(dY), ldp(dY), K, P(ws), ws.numel(), P(conv_mod.weight.grad), C, 1, wst)
+        ctx.param_done(conv_mod.weight)
+
+    ctx.push(bwd)
+    return out, st
+
+
 class BNState:
     """per-call BN coefficients"""
 
