@@ -91,13 +91,13 @@ def pmc_traffic(workload, kind):
 
 def main():
     args = parse()
-    from unetseg_hip.ddp import GradBuckets, init_from_env
+    from unetseg_hip.ddp import GradBuckets, init_from_env, local_device
 
     rank, world, local = init_from_env("nccl")
     if world != args.gpus:
         if rank == 0:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local_device(local))
     torch.cuda.set_device(dev)
     torch.manual_seed(11)
     if args.stream:
@@ -215,6 +215,15 @@ def main():
                 "kernels": {k: {"tflops": round(v[0] / v[1] / 1e12, 2), "ms_per_step": round(1e3 * v[1], 3),
                                 "launches": v[2]} for k, v in kinds.items()}}
 
+    # data-parallel consistency: after identical averaged updates every rank holds the same weights
+    in_sync = None
+    if world > 1:
+        cs = model._flat.double().sum().reshape(1)
+        lo, hi = cs.clone(), cs.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        in_sync = bool(float(hi.item()) == float(lo.item()))
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline and not multitask:
         cpu = cpu_baseline(args.model, args.size, args.cpu_batch)
@@ -232,7 +241,7 @@ def main():
             "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
             "step_tflops_per_gpu": round(step_tflops, 2),
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 3), "final_loss": round(final_loss, 5),
-            "hip_graph": use_graph,
+            "hip_graph": use_graph, "params_in_sync": in_sync,
         }
         print(json.dumps(line))
     if world > 1:

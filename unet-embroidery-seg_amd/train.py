@@ -35,7 +35,7 @@ from model.model_factory import SUPPORTED_MODELS, build_model, load_weights_flex
 from model.unet_multitask import MultiTaskLoss  # noqa: E402
 from model.unet_training import get_lr_scheduler, lovasz_hinge_loss, set_optimizer_lr, weights_init  # noqa: E402
 from unetseg_hip.arena import FusedAdam  # noqa: E402
-from unetseg_hip.ddp import GradBuckets, init_from_env  # noqa: E402
+from unetseg_hip.ddp import GradBuckets, init_from_env, local_device  # noqa: E402
 from utils.synthetic import SyntheticSegDataset, collate  # noqa: E402
 from utils.train_and_eval import (  # noqa: E402
     evaluate_binary,
@@ -97,7 +97,7 @@ def train(args):
     if args.task == "multiclass":
         raise NotImplementedError("the multiclass task is outside the hot-path scope (SURVEY.md §2.1)")
     num_classes = 2
-    device = torch.device("cuda", local) if world > 1 else torch.device(args.device)
+    device = torch.device("cuda", local_device(local)) if world > 1 else torch.device(args.device)
     if device.type != "cuda" or not torch.cuda.is_available():
         raise RuntimeError("the HIP training path needs a GPU (no CPU fallback)")
     if device.index is None:

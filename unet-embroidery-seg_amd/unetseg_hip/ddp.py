@@ -95,14 +95,25 @@ class GradBuckets:
 
 
 def init_from_env(backend: str = "nccl"):
-    """One process per GPU (torchrun env); returns (rank, world, local_rank)."""
+    """One process per GPU (torchrun env); returns (rank, world, local_rank).
+
+    UNETSEG_DIST_BACKEND overrides the backend (e.g. ``gloo`` to rehearse the N>1 control flow --
+    buckets, the weight-gradient stream, the joins -- with several ranks sharing one GPU; the local
+    rank then maps onto the visible devices modulo their count, see ``local_device``)."""
     import os
 
+    backend = os.environ.get("UNETSEG_DIST_BACKEND", backend)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
-        if backend == "nccl":
-            torch.cuda.set_device(local)
+        if backend == "nccl" or torch.cuda.device_count() > 0:
+            torch.cuda.set_device(local_device(local))
         dist.init_process_group(backend=backend)
     return rank, world, local
+
+
+def local_device(local: int) -> int:
+    """device index of a local rank (identity with one rank per GPU)"""
+    n = torch.cuda.device_count()
+    return local % n if n > 0 else 0
