@@ -39,8 +39,9 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
   constexpr int FP = WTM / 16, FC = WTN / 16;
   constexpr int RSTEP = NT / 8;
   constexpr int A_PER = BM / RSTEP, B_PER = BN / RSTEP;
-  extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // [2][(BM+BN)*8]
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // [2 or NS][(BM+BN)*8]
   constexpr int STAGE = (BM + BN) * 8;
+  constexpr bool kDMA = ST >= 13;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -101,7 +102,10 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
 #pragma unroll
   for (int i = 0; i < B_PER; ++i) {
     const int n = n0 + rb + RSTEP * i;
-    boff[i] = n < a.Ng ? (unsigned)n * (unsigned)a.ldwb + kv * 16 : kOOB;
+    // the LDS-DMA variant writes lane-linearly (slot = kv), so it fetches the chunk that slot holds
+    // under the XOR swizzle instead: kv ^ ((row >> 1) & 7) (row parity is the same for every i)
+    const int kvs = kDMA ? (kv ^ ((rb >> 1) & 7)) : kv;
+    boff[i] = n < a.Ng ? (unsigned)n * (unsigned)a.ldwb + kvs * 16 : kOOB;
   }
 
   const int nch = a.cin >> 6;
@@ -111,6 +115,36 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
   uint4 ra0[A_PER], rb0[B_PER], ra1[A_PER], rb1[B_PER];
   // scalar K-step state
   int s_jr = 0, s_js = 0, s_c = 0;
+  // ---- LDS-DMA ring (ST >= 13, NS = ST - 10 stages): buffer_load ... lds straight into the stage,
+  // NS - 1 K steps in flight, counted vmcnt + raw barrier (no register staging) ----
+  auto gload_dma = [&](int stage, bool live) {
+    const int dh = a.dh0 + a.dhs * s_jr, dw = a.dw0 + a.dws * s_js;
+    const int tapbit = (s_jr * a.ns + s_js) & 31;
+    const int tapdelta = dh * a.W + dw;
+    const unsigned wofs = (unsigned)(((a.r0 + a.rs * s_jr) * a.S + (a.s0 + a.ss * s_js)) * a.cin + s_c) * 2u;
+    const unsigned sbase = lds_addr(lds) + (unsigned)(stage * STAGE * 16) + (unsigned)(wid * 8 * 128);
+    const int kvs = kv ^ ((rb >> 1) & 7);
+    const bool first = s_c < a.c1;
+    const unsigned cb = (unsigned)(first ? s_c : s_c - a.c1) * 2u + kvs * 16;
+    const unsigned ldcb = first ? (unsigned)a.ldc1b : (unsigned)a.ldc2b;
+    const __amdgpu_buffer_rsrc_t rx = first ? r1 : r2;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const bool ok = live && ((vmask[i] >> tapbit) & 1u);
+      const unsigned off = ok ? (unsigned)(pix[i] + tapdelta) * ldcb + cb : kOOB;
+      dma16(rx, sbase + (unsigned)(RSTEP * i * 128), off);
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i)
+      dma16(rw, sbase + (unsigned)((BM + RSTEP * i) * 128), (!live || boff[i] == kOOB) ? kOOB : boff[i] + wofs);
+    if (++s_js == a.ns) {
+      s_js = 0;
+      if (++s_jr == a.nr) {
+        s_jr = 0;
+        s_c += 64;
+      }
+    }
+  };
   // live == false (a K step past the end): every offset is out of range, so the loads return
   // zeros without touching memory.  Issuing them anyway keeps the loop free of conditional loads,
   // which lets hipcc count vmcnt exactly (with conditional loads it waits for the loads of the
@@ -196,7 +230,21 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
     }
   };
 
-  if (ST == 1) {  // one K step
+  if constexpr (kDMA) {
+    constexpr int NS = ST - 10, PER = A_PER + B_PER;
+    static_assert(NS >= 3 && PER * (NS - 2) <= 63, "vmcnt range");
+#pragma unroll
+    for (int s0 = 0; s0 < NS - 1; ++s0) gload_dma(s0, s0 < nsteps);
+    for (int kt = 0; kt < nsteps; ++kt) {
+      // this wave's DMAs of step kt have landed (the NS-2 younger steps stay in flight), this
+      // wave's LDS reads of step kt-1 are done; the barrier makes both true for every wave
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PER * (NS - 2)) : "memory");
+      gload_dma((kt + NS - 1) % NS, kt + NS - 1 < nsteps);  // refills the stage read at kt-1
+      compute(kt % NS);
+    }
+    // every DMA (past-the-end ones write zeros) has landed before the epilogue reuses the LDS
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  } else if (ST == 1) {  // one K step
     if (nsteps > 0) {
       gload(ra0, rb0);
       sstore(0, ra0, rb0);
@@ -633,7 +681,7 @@ template <int BM, int BN, int NWM, int NWN, int ST, bool POST = false>
 int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   constexpr int NT = 64 * NWM * NWN;
   // operand stages, or the epilogue's per-wave transpose tiles + stats scratch if larger
-  const size_t stages = (size_t)(ST == 1 ? 1 : 2) * (BM + BN) * 8 * 16;
+  const size_t stages = (size_t)(ST == 1 ? 1 : ST >= 13 ? ST - 10 : 2) * (BM + BN) * 8 * 16;
   const size_t epi = (size_t)NWM * NWN * 64 * ((BN / NWN) * 2 + 16) + 2 * NWM * BN * 4;
   const size_t lds = stages > epi ? stages : epi;
   static bool attr = false;
@@ -653,24 +701,39 @@ int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
 }
 
 // TN configuration: 0 = halo, 1 = 256x64, 2 = 256x128, 3 = 128x128, 4 = 128x128 single stage
-// (one K step: the prefetch stage would only cost occupancy), 5 = 64x128
+// (one K step: the prefetch stage would only cost occupancy), 5 = 64x128, 6 = 128x64;
+// 7-10: the same tiles on the LDS-DMA ring.  Measured (tools/gpu_cfg_sweep.sh): the 256x128 ring
+// (3 stages) beats the register-staged 256x128 by 3-8 % on every large layer; the 64x128 ring (4
+// stages) is 15 % faster on deep-K small-M layers (3x3 at 16x16, 72 K steps) but slower on short K.
 static int tn_config(const FastTNArgs& a) {
-  if (const char* e = getenv("UNETSEG_TN_CFG")) {  // experiments: force a configuration (1..6)
+  if (const char* e = getenv("UNETSEG_TN_CFG")) {  // experiments: force a configuration (1..10)
     const int c = atoi(e);
-    if (c >= 1 && c <= 6) return c;
+    if (c >= 1 && c <= 10) return c;
   }
+  static const bool no_dma = getenv("UNETSEG_TN_NO_DMA") != nullptr;
   if (halo3_ok(a)) return 0;
   const int nsteps = a.nr * a.ns * (a.cin >> 6);
   if (nsteps == 1 && a.Ng > 64) return 4;
   if (a.Ng <= 64) return 1;
   if (nsteps <= 4) return 3;
   const long tiles_big = (long)ceil_div(a.M, 256) * ceil_div(a.Ng, 128);
-  if (tiles_big >= 256) return 2;
+  if (tiles_big >= 256) return no_dma ? 2 : 7;
   const long tiles_mid = (long)ceil_div(a.M, 128) * ceil_div(a.Ng, 128);
-  return tiles_mid >= 256 ? 3 : 5;  // 5: 64-row tiles so that small-M layers still fill the chip
+  if (tiles_mid >= 256) return 3;
+  // 64-row tiles so that small-M layers still fill the chip
+  return (!no_dma && nsteps >= 32) ? 9 : 5;
 }
 
 }  // namespace
+
+// row tile (BM) of each TN configuration
+static int tn_cfg_bm(int cfg) {
+  switch (cfg) {
+    case 1: case 2: case 7: return 256;
+    case 5: case 9: return 64;
+    default: return 128;
+  }
+}
 
 bool tn_fast_ok(const FastTNArgs& a) {
   return a.cin % 64 == 0 && a.c1 % 64 == 0 && a.nr * a.ns <= 32 && a.Ng % 8 == 0;
@@ -680,13 +743,13 @@ bool tn_fast_ok(const FastTNArgs& a) {
 // spatial tile on the halo kernel.
 int tn_fast_tile_m(const FastTNArgs& a) {
   const int cfg = tn_config(a);
-  return cfg == 0 ? halo_tile_m() : cfg <= 2 ? 256 : cfg == 5 ? 64 : 128;  // cfg 6: 128 rows
+  return cfg == 0 ? halo_tile_m() : tn_cfg_bm(cfg);
 }
 
 int tn_fast_post_rows(const FastTNArgs& a) {
   if (a.M <= 0 || a.Ng <= 0) return 0;
   const int cfg = tn_config(a);
-  return cfg == 0 ? halo3_blocks(a) : ceil_div(a.M, cfg <= 2 ? 256 : cfg == 5 ? 64 : 128);
+  return cfg == 0 ? halo3_blocks(a) : ceil_div(a.M, tn_cfg_bm(cfg));
 }
 
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
@@ -698,6 +761,11 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 4: return a.post ? launch_tn_cfg<128, 128, 2, 2, 1, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 1>(a, st);
     case 5: return a.post ? launch_tn_cfg<64, 128, 1, 4, 3, true>(a, st) : launch_tn_cfg<64, 128, 1, 4, 3>(a, st);
     case 6: return a.post ? launch_tn_cfg<128, 64, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 64, 2, 2, 3>(a, st);
+    // LDS-DMA ring variants (experiments via UNETSEG_TN_CFG)
+    case 7: return a.post ? launch_tn_cfg<256, 128, 4, 2, 13, true>(a, st) : launch_tn_cfg<256, 128, 4, 2, 13>(a, st);
+    case 8: return a.post ? launch_tn_cfg<128, 128, 2, 2, 14, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 14>(a, st);
+    case 9: return a.post ? launch_tn_cfg<64, 128, 1, 4, 14, true>(a, st) : launch_tn_cfg<64, 128, 1, 4, 14>(a, st);
+    case 10: return a.post ? launch_tn_cfg<128, 128, 2, 2, 15, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 15>(a, st);
     default: return a.post ? launch_tn_cfg<128, 128, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 3>(a, st);
   }
 }
