@@ -708,13 +708,13 @@ int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
 static int tn_config(const FastTNArgs& a) {
   if (const char* e = getenv("UNETSEG_TN_CFG")) {  // experiments: force a configuration (1..10)
     const int c = atoi(e);
-    if (c >= 1 && c <= 10) return c;
+    if (c >= 1 && c <= 12) return c;
   }
   static const bool no_dma = getenv("UNETSEG_TN_NO_DMA") != nullptr;
   if (halo3_ok(a)) return 0;
   const int nsteps = a.nr * a.ns * (a.cin >> 6);
   if (nsteps == 1 && a.Ng > 64) return 4;
-  if (a.Ng <= 64) return 1;
+  if (a.Ng <= 64) return 6;  // 128x64 (two-step prefetch, 3 blocks/CU): 5-10 % over 256x64
   if (nsteps <= 4) return 3;
   const long tiles_big = (long)ceil_div(a.M, 256) * ceil_div(a.Ng, 128);
   if (tiles_big >= 256) return no_dma ? 2 : 7;
@@ -729,7 +729,7 @@ static int tn_config(const FastTNArgs& a) {
 // row tile (BM) of each TN configuration
 static int tn_cfg_bm(int cfg) {
   switch (cfg) {
-    case 1: case 2: case 7: return 256;
+    case 1: case 2: case 7: case 11: return 256;
     case 5: case 9: return 64;
     default: return 128;
   }
@@ -766,6 +766,8 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 8: return a.post ? launch_tn_cfg<128, 128, 2, 2, 14, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 14>(a, st);
     case 9: return a.post ? launch_tn_cfg<64, 128, 1, 4, 14, true>(a, st) : launch_tn_cfg<64, 128, 1, 4, 14>(a, st);
     case 10: return a.post ? launch_tn_cfg<128, 128, 2, 2, 15, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 15>(a, st);
+    case 11: return a.post ? launch_tn_cfg<256, 64, 4, 1, 13, true>(a, st) : launch_tn_cfg<256, 64, 4, 1, 13>(a, st);
+    case 12: return a.post ? launch_tn_cfg<128, 64, 2, 2, 14, true>(a, st) : launch_tn_cfg<128, 64, 2, 2, 14>(a, st);
     default: return a.post ? launch_tn_cfg<128, 128, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 3>(a, st);
   }
 }
