@@ -781,7 +781,8 @@ int wgrad_fast_splits(int Cout, int Ng, long Kpix) {
   const int bn = Cout <= 64 ? 256 : 128;
   const int tiles = ceil_div(Cout, bm) * ceil_div(Ng, bn);
   const long nkt = (Kpix + kWgBK - 1) / kWgBK;
-  int sp = ceil_div(Cout <= 64 ? 1024 : 512, tiles);  // 2-4 blocks per CU
+  static const int wscale = getenv("UNETSEG_WG_BLOCKS") ? atoi(getenv("UNETSEG_WG_BLOCKS")) : 0;
+  int sp = ceil_div(wscale > 0 ? wscale : (Cout <= 64 ? 1024 : 512), tiles);  // 2-4 blocks per CU
   const long max_sp = nkt / 32 > 0 ? nkt / 32 : 1;  // >= 32 K steps per split
   if (sp > max_sp) sp = (int)max_sp;
   if (sp > 512) sp = 512;

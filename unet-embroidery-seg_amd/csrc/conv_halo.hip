@@ -546,7 +546,10 @@ int halo3_wgrad_splits(const HaloWgradArgs& a) {
   const double slab = 4.0 * a.Cout * 9.0 * a.cin;
   int best = 1;
   double best_t = 1e30;
-  for (int g = 1; g <= 512 && g <= n_sp; ++g) {
+  // with the weight gradients on their own stream the makespan matters less than the slab traffic
+  // the reduce adds beside the compute stream: UNETSEG_HALO_WG_MAXG caps G (experiments)
+  static const int maxg = getenv("UNETSEG_HALO_WG_MAXG") ? atoi(getenv("UNETSEG_HALO_WG_MAXG")) : 512;
+  for (int g = 1; g <= maxg && g <= n_sp; ++g) {
     if (slab * g > 768.0 * (1 << 20)) break;  // workspace cap
     const double rounds = (double)((groups * g + 255) / 256);
     const double t = rounds * ((n_sp + g - 1) / g) * 2e-6 + slab * g / 4e12;
