@@ -32,7 +32,12 @@ namespace {
 template <int BM, int BN, int NWM, int NWN>
 constexpr int tn_waves_per_simd() { return (BM == 64 || (BM == 128 && BN == 64)) ? 3 : 2; }
 
-template <int BM, int BN, int NWM, int NWN, int ST, bool POST>
+// TAPS (LDS-DMA ring only): the filter has exactly TAPS = nr x ns taps, known at compile time.  The
+// K loop is then unrolled over the taps and every (row, tap) gather offset is precomputed, so a K
+// step issues its loads with one multiply-add per row and a scalar channel offset (the generic
+// ring re-derives tap deltas, validity masks and offsets every step: ~70 VALU + ~90 SALU per step
+// on the 256x128 tile, which is what held its MFMA pipe at ~45 % busy).
+template <int BM, int BN, int NWM, int NWN, int ST, bool POST, int TAPS = 0>
 __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN>())) void tn_fast_kernel(FastTNArgs a) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int WTM = BM / NWM, WTN = BN / NWN;
@@ -203,34 +208,101 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
 #pragma unroll
     for (int p = 0; p < FP; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf) {
+  auto frags = [&](int buf, int kk, bf16x8 (&pf)[FP], bf16x8 (&wf)[FC]) {
     const uint4* As = lds + buf * STAGE;
     const uint4* Bs = As + BM * 8;
+    const int ch = kk * 4 + (lane >> 4);
+#pragma unroll
+    for (int p = 0; p < FP; ++p) {
+      const int row = wm * WTM + p * 16 + (lane & 15);
+      uint4 v = As[row * 8 + swz8(row, ch)];
+      pf[p] = *reinterpret_cast<bf16x8*>(&v);
+    }
+#pragma unroll
+    for (int c = 0; c < FC; ++c) {
+      const int row = wn * WTN + c * 16 + (lane & 15);
+      uint4 v = Bs[row * 8 + swz8(row, ch)];
+      wf[c] = *reinterpret_cast<bf16x8*>(&v);
+    }
+  };
+  auto mfmas = [&](const bf16x8 (&pf)[FP], const bf16x8 (&wf)[FC]) {
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int p = 0; p < FP; ++p)
+        acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], pf[p], acc[c][p], 0, 0, 0);
+  };
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const int ch = kk * 4 + (lane >> 4);
       bf16x8 pf[FP], wf[FC];
-#pragma unroll
-      for (int p = 0; p < FP; ++p) {
-        const int row = wm * WTM + p * 16 + (lane & 15);
-        uint4 v = As[row * 8 + swz8(row, ch)];
-        pf[p] = *reinterpret_cast<bf16x8*>(&v);
-      }
-#pragma unroll
-      for (int c = 0; c < FC; ++c) {
-        const int row = wn * WTN + c * 16 + (lane & 15);
-        uint4 v = Bs[row * 8 + swz8(row, ch)];
-        wf[c] = *reinterpret_cast<bf16x8*>(&v);
-      }
-#pragma unroll
-      for (int c = 0; c < FC; ++c)
-#pragma unroll
-        for (int p = 0; p < FP; ++p)
-          acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], pf[p], acc[c][p], 0, 0, 0);
+      frags(buf, kk, pf, wf);
+      mfmas(pf, wf);
     }
   };
 
-  if constexpr (kDMA) {
+  if constexpr (kDMA && TAPS > 0) {
+    constexpr int NS = ST - 10, PER = A_PER + B_PER;
+    static_assert(NS >= 3 && PER * (NS - 2) <= 63, "vmcnt range");
+    static_assert(A_PER % 2 == 0 && B_PER % 2 == 0, "rows are issued in pairs");
+    // (row, tap) -> gather pixel, or pbad: one past every source's last pixel, so pbad * ldcb is
+    // out of range for either source (the launcher checks it cannot wrap 32 bits)
+    const unsigned pb1 = a.x1_bytes / (unsigned)a.ldc1b;
+    const unsigned pb2 = a.x2 ? a.x2_bytes / (unsigned)a.ldc2b : 0u;
+    const unsigned pbad = (pb1 > pb2 ? pb1 : pb2) + 1u;
+    unsigned vpix[A_PER][TAPS];
+    unsigned tw[TAPS];  // weight byte offset of each tap
+#pragma unroll
+    for (int t = 0; t < TAPS; ++t) {
+      const int jr = t / a.ns, js = t - jr * a.ns;
+      const int tapdelta = (a.dh0 + a.dhs * jr) * a.W + a.dw0 + a.dws * js;
+      tw[t] = (unsigned)(((a.r0 + a.rs * jr) * a.S + (a.s0 + a.ss * js)) * a.cin) * 2u;
+#pragma unroll
+      for (int i = 0; i < A_PER; ++i) vpix[i][t] = ((vmask[i] >> t) & 1u) ? (unsigned)(pix[i] + tapdelta) : pbad;
+    }
+    const unsigned kv16 = (unsigned)(kv ^ ((rb >> 1) & 7)) * 16u;
+    const unsigned lbase = lds_addr(lds) + (unsigned)(wid * 8 * 128);
+    const int nch = a.cin >> 6;
+    // issue K step (chunk c, tap t) into stage `stage`; a chunk past the end loads through
+    // zero-extent descriptors (zeros, no memory traffic) so every step issues PER loads
+    auto issue = [&](int c, int t, int stage) {
+      const bool live = c < nch;
+      const int c64 = c * 64;
+      const bool first = c64 < a.c1;
+      // wave-uniform by construction; readfirstlane keeps them in SGPRs for the asm operands
+      const __amdgpu_buffer_rsrc_t rx = srd_u(first ? a.x1 : a.x2, !live ? 0u : first ? a.x1_bytes : a.x2_bytes);
+      const __amdgpu_buffer_rsrc_t rwx = srd_u(a.wt, live ? a.w_bytes : 0u);
+      const unsigned ldcb = first ? (unsigned)a.ldc1b : (unsigned)a.ldc2b;
+      const unsigned soff = __builtin_amdgcn_readfirstlane(live ? (unsigned)(first ? c64 : c64 - a.c1) * 2u : 0u);
+      const unsigned wsoff = __builtin_amdgcn_readfirstlane(live ? tw[t] + (unsigned)c64 * 2u : 0u);
+      const unsigned sb = __builtin_amdgcn_readfirstlane(lbase + (unsigned)(stage * STAGE * 16));
+#pragma unroll
+      for (int i = 0; i < A_PER; i += 2)
+        dma16x2<RSTEP * 128>(rx, sb + (unsigned)(RSTEP * i * 128), __umul24(vpix[i][t], ldcb) + kv16,
+                             __umul24(vpix[i + 1][t], ldcb) + kv16, soff);
+#pragma unroll
+      for (int i = 0; i < B_PER; i += 2)
+        dma16x2<RSTEP * 128>(rwx, sb + (unsigned)((BM + RSTEP * i) * 128), boff[i], boff[i + 1], wsoff);
+    };
+#pragma unroll
+    for (int s0 = 0; s0 < NS - 1; ++s0) issue(s0 / TAPS, s0 % TAPS, s0);
+    int stage = 0;
+    for (int c = 0; c < nch; ++c) {
+#pragma unroll
+      for (int t = 0; t < TAPS; ++t) {
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PER * (NS - 2)) : "memory");
+        bf16x8 pf[FP], wf[FC];
+        frags(stage, 0, pf, wf);  // first fragments in flight while this step's loads issue
+        const int st2 = stage == 0 ? NS - 1 : stage - 1;  // (stage + NS - 1) % NS
+        issue(c + (t + NS - 1) / TAPS, (t + NS - 1) % TAPS, st2);
+        mfmas(pf, wf);
+        frags(stage, 1, pf, wf);
+        mfmas(pf, wf);
+        stage = stage == NS - 1 ? 0 : stage + 1;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  } else if constexpr (kDMA) {
     constexpr int NS = ST - 10, PER = A_PER + B_PER;
     static_assert(NS >= 3 && PER * (NS - 2) <= 63, "vmcnt range");
 #pragma unroll
@@ -677,7 +749,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     }
 }
 
-template <int BM, int BN, int NWM, int NWN, int ST, bool POST = false>
+template <int BM, int BN, int NWM, int NWN, int ST, bool POST = false, int TAPS = 0>
 int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   constexpr int NT = 64 * NWM * NWN;
   // operand stages, or the epilogue's per-wave transpose tiles + stats scratch if larger
@@ -686,7 +758,7 @@ int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   const size_t lds = stages > epi ? stages : epi;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_fast_kernel<BM, BN, NWM, NWN, ST, POST>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_fast_kernel<BM, BN, NWM, NWN, ST, POST, TAPS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
@@ -696,8 +768,32 @@ int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   // 2D spatial tiles measured slower than row-major tiles with the chunk-outer K order: opt-in
   static const bool t2d = getenv("UNETSEG_T2D") != nullptr;
   b.t2d = (t2d && a.nr * a.ns > 1 && a.wc % 32 == 0 && a.wc > 32 && a.hc % TR == 0) ? TR : 0;
-  hipLaunchKernelGGL((tn_fast_kernel<BM, BN, NWM, NWN, ST, POST>), grid, dim3(NT), lds, st, b);
+  hipLaunchKernelGGL((tn_fast_kernel<BM, BN, NWM, NWN, ST, POST, TAPS>), grid, dim3(NT), lds, st, b);
   return 0;
+}
+
+// Compile-time tap count for the LDS-DMA ring (0 = generic ring): 3x3 and 1x1 filters, when the
+// precomputed gather offsets (pixel index < 2^24, pbad * ldcb) fit the 24-bit multiply and 32 bits.
+static int tn_taps(const FastTNArgs& a) {
+  static const bool off = getenv("UNETSEG_TN_NO_TAPS") != nullptr;
+  static const bool off1 = getenv("UNETSEG_TN_NO_TAPS1") != nullptr;
+  const int taps = a.nr * a.ns;
+  if (off || (taps != 9 && taps != 1) || (taps == 1 && off1)) return 0;
+  const unsigned long long p1 = a.x1_bytes / (unsigned)a.ldc1b;
+  const unsigned long long p2 = a.x2 ? a.x2_bytes / (unsigned)a.ldc2b : 0ull;
+  const unsigned long long pbad = (p1 > p2 ? p1 : p2) + 1ull;
+  const unsigned long long ld = (unsigned)(a.ldc1b > a.ldc2b ? a.ldc1b : a.ldc2b);
+  if (pbad >= (1ull << 24) || ld >= (1ull << 24) || pbad * ld + 256ull >= (1ull << 32)) return 0;
+  return taps;
+}
+
+template <int BM, int BN, int NWM, int NWN, int ST>
+static int launch_tn_dma(const FastTNArgs& a, hipStream_t st) {
+  switch (tn_taps(a)) {
+    case 9: return a.post ? launch_tn_cfg<BM, BN, NWM, NWN, ST, true, 9>(a, st) : launch_tn_cfg<BM, BN, NWM, NWN, ST, false, 9>(a, st);
+    case 1: return a.post ? launch_tn_cfg<BM, BN, NWM, NWN, ST, true, 1>(a, st) : launch_tn_cfg<BM, BN, NWM, NWN, ST, false, 1>(a, st);
+    default: return a.post ? launch_tn_cfg<BM, BN, NWM, NWN, ST, true>(a, st) : launch_tn_cfg<BM, BN, NWM, NWN, ST>(a, st);
+  }
 }
 
 // TN configuration: 0 = halo, 1 = 256x64, 2 = 256x128, 3 = 128x128, 4 = 128x128 single stage
@@ -762,9 +858,9 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 5: return a.post ? launch_tn_cfg<64, 128, 1, 4, 3, true>(a, st) : launch_tn_cfg<64, 128, 1, 4, 3>(a, st);
     case 6: return a.post ? launch_tn_cfg<128, 64, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 64, 2, 2, 3>(a, st);
     // LDS-DMA ring variants (experiments via UNETSEG_TN_CFG)
-    case 7: return a.post ? launch_tn_cfg<256, 128, 4, 2, 13, true>(a, st) : launch_tn_cfg<256, 128, 4, 2, 13>(a, st);
+    case 7: return launch_tn_dma<256, 128, 4, 2, 13>(a, st);
     case 8: return a.post ? launch_tn_cfg<128, 128, 2, 2, 14, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 14>(a, st);
-    case 9: return a.post ? launch_tn_cfg<64, 128, 1, 4, 14, true>(a, st) : launch_tn_cfg<64, 128, 1, 4, 14>(a, st);
+    case 9: return launch_tn_dma<64, 128, 1, 4, 14>(a, st);
     case 10: return a.post ? launch_tn_cfg<128, 128, 2, 2, 15, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 15>(a, st);
     case 11: return a.post ? launch_tn_cfg<256, 64, 4, 1, 13, true>(a, st) : launch_tn_cfg<256, 64, 4, 1, 13>(a, st);
     case 12: return a.post ? launch_tn_cfg<128, 64, 2, 2, 14, true>(a, st) : launch_tn_cfg<128, 64, 2, 2, 14>(a, st);

@@ -31,6 +31,35 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned lds_byt
       : "s"(lds_byte), "v"(voff), "s"(r)
       : "memory");
 }
+// Two LDS-DMA rows of one wave (lds_byte and lds_byte + STRIDE) with one M0 save/restore; soff is
+// a scalar byte offset added by the hardware to both.  Out-of-range rows must be expressed in voff
+// (or a zero-extent SRD), never in soff.
+// srd() of a wave-uniform (pointer, extent) chosen at run time: readfirstlane keeps the descriptor in
+// SGPRs (an inline-asm "s" operand does not force that by itself)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t srd_u(const void* p, unsigned bytes) {
+  const unsigned long long q = (unsigned long long)(size_t)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)q);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(q >> 32));
+  return srd((const void*)(size_t)(((unsigned long long)hi << 32) | lo), __builtin_amdgcn_readfirstlane(bytes));
+}
+// (M0 is set with s_mov only: an s_add would clobber SCC behind the compiler's back)
+template <int STRIDE>
+__device__ __forceinline__ void dma16x2(__amdgpu_buffer_rsrc_t r, unsigned lds_byte, unsigned v0, unsigned v1,
+                                        unsigned soff) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %3, %5, %6 offen lds\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %4, %5, %6 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds_byte), "s"(lds_byte + STRIDE), "v"(v0), "v"(v1), "s"(r), "s"(soff)
+      : "memory");
+}
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
 }
