@@ -815,7 +815,9 @@ static int tn_config(const FastTNArgs& a) {
   const long tiles_big = (long)ceil_div(a.M, 256) * ceil_div(a.Ng, 128);
   if (tiles_big >= 256) return no_dma ? 2 : 7;
   const long tiles_mid = (long)ceil_div(a.M, 128) * ceil_div(a.Ng, 128);
-  if (tiles_mid >= 256) return 3;
+  // one or two 128x128 tiles per CU and a deep K: the 5-stage ring with compile-time taps (one
+  // block per CU) beats the register-staged tile by ~25 % (3x3 256->256 at 32x32: 43 -> 34 us)
+  if (tiles_mid >= 256) return (!no_dma && nsteps >= 16 && tn_taps(a)) ? 10 : 3;
   // 64-row tiles so that small-M layers still fill the chip
   return (!no_dma && nsteps >= 32) ? 9 : 5;
 }
@@ -859,11 +861,11 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 6: return a.post ? launch_tn_cfg<128, 64, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 64, 2, 2, 3>(a, st);
     // LDS-DMA ring variants (experiments via UNETSEG_TN_CFG)
     case 7: return launch_tn_dma<256, 128, 4, 2, 13>(a, st);
-    case 8: return a.post ? launch_tn_cfg<128, 128, 2, 2, 14, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 14>(a, st);
+    case 8: return launch_tn_dma<128, 128, 2, 2, 14>(a, st);
     case 9: return launch_tn_dma<64, 128, 1, 4, 14>(a, st);
-    case 10: return a.post ? launch_tn_cfg<128, 128, 2, 2, 15, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 15>(a, st);
-    case 11: return a.post ? launch_tn_cfg<256, 64, 4, 1, 13, true>(a, st) : launch_tn_cfg<256, 64, 4, 1, 13>(a, st);
-    case 12: return a.post ? launch_tn_cfg<128, 64, 2, 2, 14, true>(a, st) : launch_tn_cfg<128, 64, 2, 2, 14>(a, st);
+    case 10: return launch_tn_dma<128, 128, 2, 2, 15>(a, st);
+    case 11: return launch_tn_dma<256, 64, 4, 1, 13>(a, st);
+    case 12: return launch_tn_dma<128, 64, 2, 2, 14>(a, st);
     default: return a.post ? launch_tn_cfg<128, 128, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 3>(a, st);
   }
 }

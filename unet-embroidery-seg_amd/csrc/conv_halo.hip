@@ -338,7 +338,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
 // wgrad of the same convolutions: dW[k][tap][c] = sum_pix dY[pix][k] * X[pix + off(tap)][c].
 // Block group = (64 output channels, 64 input channels); persistent over TH x 32 spatial tiles,
 // each tile = dY tile (256 px x 64 ch) + X halo (340 px x 64 ch) by LDS-DMA, double buffered.
-// Wave w owns 9 of the 36 (tap, 16-channel) column blocks: 4 x 9 accumulators of 16x16.
+// Wave w owns input channels 16w .. 16w+15 of the 9 taps: 4 x 9 accumulators of 16x16.
 // Fragments come from pixel-major LDS with ds_read_b64_tr_b16 (K = 32 pixels of one output row);
 // the halo rows of a tap are the output row's pixels shifted by (dh, dw), so the same transposed
 // read serves all 9 taps.  Partials go to slab[slot] in the natural [cout][tap*cin + c] layout of
@@ -416,13 +416,26 @@ __global__ __launch_bounds__(256) void halo3_wgrad_kernel(HaloWgradArgs a, int t
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
   typedef short s16x8 __attribute__((ext_vector_type(8)));
-  auto tr = [&](const char* rowbase_a, int row_a, int chunk) -> bf16x8 {
-    // rows row_a (+0..3 via qq) and row_a + 4 of a 128-B-row image starting at rowbase_a
-    const int ra = row_a + qq, rb = row_a + qq + 4;
-    const char* pa = rowbase_a + ra * 128 + ((chunk ^ swz_tr8(ra)) * 16) + (pp & 1) * 8;
-    const char* pb = rowbase_a + rb * 128 + ((chunk ^ swz_tr8(rb)) * 16) + (pp & 1) * 8;
-    s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(pa));
-    s16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(pb));
+  // Transposed fragment reads with no per-read address arithmetic.  A read covers image rows
+  // R + 8g + qq and R + 8g + qq + 4 (lane-dependent) at 16-B chunk c; the swizzle depends on row
+  // bits 1 and 3 only, so with R = B + rho (B a multiple of 16, rho = R mod 16 known at compile
+  // time once the row loop is unrolled) the lane's byte offset is B * 128 (an immediate) plus a
+  // per-lane value precomputed for each rho.  Wave w owns input channels 16w .. 16w+15 of all 9
+  // taps, so every tap's (dh, dw) -- and with it R -- is a compile-time constant.
+  auto lane_off = [&](int x, int chunk) -> unsigned {
+    return (unsigned)(x * 128 + ((chunk ^ swz_tr8(x)) * 16) + (pp & 1) * 8);
+  };
+  unsigned pa[FM][2], pb[16][2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) pa[i][k] = lane_off(8 * g + qq + 4 * k, i * 2 + (pp >> 1));
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pb[r][k] = lane_off(r + 8 * g + qq + 4 * k, wid * 2 + (pp >> 1));
+  }
+  auto tr2 = [&](const char* base, unsigned o0, unsigned o1) -> bf16x8 {
+    s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + o0));
+    s16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + o1));
     s16x8 v = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
     return *reinterpret_cast<bf16x8*>(&v);
   };
@@ -432,17 +445,16 @@ __global__ __launch_bounds__(256) void halo3_wgrad_kernel(HaloWgradArgs a, int t
     if (t + 1 < my_tiles) issue(t + 1, stage ^ 1);
     const char* dbase = reinterpret_cast<const char*>(lds + stage * STG);
     const char* hbase = dbase + DCH * 16;
-#pragma unroll 2
+#pragma unroll
     for (int rr = 0; rr < TH; ++rr) {
       bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = tr(dbase, rr * HW_TW + 8 * g, i * 2 + (pp >> 1));
+      for (int i = 0; i < FM; ++i) af[i] = tr2(dbase + rr * HW_TW * 128, pa[i][0], pa[i][1]);
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int f = wid * FN + j;
-        const int jt = f >> 2, cg = f & 3;
-        const int dh = jt / 3 - 1, dw = jt % 3 - 1;
-        bfr[j] = tr(hbase, (rr + 1 + dh) * (HW_TW + 2) + 1 + dw + 8 * g, cg * 2 + (pp >> 1));
+        const int dh = j / 3 - 1, dw = j % 3 - 1;
+        const int R = (rr + 1 + dh) * (HW_TW + 2) + 1 + dw, rho = R & 15;
+        bfr[j] = tr2(hbase + (R - rho) * 128, pb[rho][0], pb[rho][1]);
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -461,11 +473,7 @@ __global__ __launch_bounds__(256) void halo3_wgrad_kernel(HaloWgradArgs a, int t
     for (int e = 0; e < 4; ++e) {
       const int m = mt * 64 + i * 16 + g * 4 + e;
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int f = wid * FN + j;
-        const int jt = f >> 2, cg = f & 3;
-        ws[(long)m * Ng + (long)jt * a.cin + ct * 64 + cg * 16 + i16] = acc[i][j][e];
-      }
+      for (int j = 0; j < FN; ++j) ws[(long)m * Ng + (long)j * a.cin + ct * 64 + wid * 16 + i16] = acc[i][j][e];
     }
 }
 
