@@ -160,6 +160,12 @@ int unetseg_pw_small_fwd(int dtype, const void* x, int ldx, long M, int hw, int 
                          const float* b, float* y, float* stats, void* stream);
 int unetseg_pw_small_bwd(int dtype, const float* dy, const void* x, int ldx, long M, int hw, int c, int k,
                          const float* w, void* dx, int lddx, int dx_acc, float* part_w, float* part_b, void* stream);
+/* pw_small_bwd with the producer ReLU's backward fused (x = ReLU output, sole consumer; bf16):
+ * dx = (x > 0) ? dy.W : 0; part_d [G][2][c], slot 0 = column sums of dx (replaces the
+ * reference autograd's ReLU backward + conv bias grad of up_conv's last conv, model/unet_resnet.py:70-78,100-103). */
+int unetseg_pw_small_bwd_relu(int dtype, const float* dy, const void* x, int ldx, long M, int hw, int c, int k,
+                              const float* w, void* dx, int lddx, float* part_w, float* part_b, float* part_d,
+                              void* stream);
 
 /* ---- attention gate (AttentionGate.forward: model/unet_attention.py:28-36) -------------------- */
 /* alpha = sigmoid(BN1(psi)); gated = skip * alpha */

@@ -11,4 +11,5 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format cs
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/${TAG}_pmcW -o run -- python bench.py --steps 2 --warmup 1 --cpu-baseline 0 --probe 0 > gpurun_out/${TAG}_pmcW.log 2>&1 || { echo pmc write failed; exit 1; }
 python tools/pmc_traffic.py gpurun_out/${TAG}_pmcF gpurun_out/${TAG}_pmcW gpurun_out/${TAG}_traffic.json "$WL" > /dev/null
 python tools/prof_summary.py gpurun_out/${TAG}_prof 8 40 > gpurun_out/${TAG}_kernel_stats_summary.txt
+python tools/trace_streams.py gpurun_out/${TAG}_prof 4 > gpurun_out/${TAG}_streams.txt
 tail -1 gpurun_out/${TAG}_bench.json | cut -c1-200

@@ -730,10 +730,13 @@ __global__ void pw_small_fwd_kernel(const T* x, int ldx, long M, int HW, int C, 
 
 // Backward of the tiny-Cout 1x1 conv.  dy fp32 planar [N][K][HW].
 //   dx (+)= dy . W  (T, NHWC, ld), partials for dW [K][C][G] and db [K][G]
-template <typename T, int K>
+// MASK: x is the output of a ReLU whose backward is fused here (this conv is x's sole consumer):
+// dx = (x > 0) ? dy . W : 0, and part_d[G][2][C] (slot 0) gets the column sums of the stored
+// (rounded) dx -- the producer conv's bias-gradient partials, as the TN dgrad post-op writes them.
+template <typename T, int K, bool MASK = false>
 __global__ void pw_small_bwd_kernel(const float* dy, const T* x, int ldx, long M, int HW, int C, const float* w,
                                     T* dx, int lddx, int dx_acc, float* part_w, float* part_b, int G,
-                                    int pix_per_block) {
+                                    int pix_per_block, float* part_d = nullptr) {
   constexpr int V = VE<T>;
   __shared__ float red[256][V];
   __shared__ float redb[256];
@@ -755,6 +758,9 @@ __global__ void pw_small_bwd_kernel(const float* dy, const T* x, int ldx, long M
 #pragma unroll
     for (int e = 0; e < V; ++e) sw[k][e] = 0.f;
   }
+  float sd[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) sd[e] = 0.f;
   for (long p = p0 + ty; p < p1; p += rows) {
     const long n = p / HW, hw = p - n * HW;
     float g[K];
@@ -774,6 +780,13 @@ __global__ void pw_small_bwd_kernel(const float* dy, const T* x, int ldx, long M
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) sb[k] += g[k];
+    if (MASK) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        o[e] = xv[e] > 0.f ? (float)(T)o[e] : 0.f;  // the stored value, rounded
+        sd[e] += o[e];
+      }
+    }
     if (dx) {
       T* dp = dx + p * lddx + c0;
       if (dx_acc) {
@@ -805,6 +818,25 @@ __global__ void pw_small_bwd_kernel(const float* dy, const T* x, int ldx, long M
 #pragma unroll
       for (int e = 0; e < V; ++e) part_w[((long)k * C + c0 + e) * G + blockIdx.x] = s[e];
       if (tx == 0) part_b[(long)k * G + blockIdx.x] = bs;
+    }
+  }
+  if (MASK) {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < V; ++e) red[threadIdx.x][e] = sd[e];
+    __syncthreads();
+    if (ty == 0) {
+      float s[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) s[e] = 0.f;
+      for (int r = 0; r < rows; ++r)
+#pragma unroll
+        for (int e = 0; e < V; ++e) s[e] += red[r * tv + tx][e];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        part_d[(long)blockIdx.x * 2 * C + c0 + e] = s[e];
+        part_d[(long)blockIdx.x * 2 * C + C + c0 + e] = 0.f;
+      }
     }
   }
 }
@@ -1285,6 +1317,29 @@ UNETSEG_API int unetseg_pw_small_bwd(int dtype, const float* dy, const void* x, 
                          (T*)dx, lddx, dx_acc, part_w, part_b, G, 2048);
   });
   US_LAUNCH_CHECK("pw_small_bwd");
+  return 0;
+}
+
+// pw_small_bwd with the backward of the ReLU that produced x fused in (x = that ReLU's output, this
+// conv its sole consumer): dx = (x > 0) ? dy . W : 0 (no accumulate), part_d [G][2][c] with slot 0
+// = column sums of dx (the producer conv's bias-gradient partials; unetseg_colsum_rows reduces them)
+UNETSEG_API int unetseg_pw_small_bwd_relu(int dtype, const float* dy, const void* x, int ldx, long M, int hw, int c,
+                                          int k, const float* w, void* dx, int lddx, float* part_w, float* part_b,
+                                          float* part_d, void* stream) {
+  US_CHECK_ARG(dtype == DT_BF16, "pw_small_bwd_relu: bf16 only");
+  CHECK_VEC(dtype, c, "pw_small_bwd_relu");
+  US_CHECK_ARG(c / 8 <= 256 && 256 % (c / 8) == 0, "pw_small_bwd_relu: bad C");
+  US_CHECK_ARG(k == 1 || k == 2, "pw_small_bwd_relu: k must be 1 or 2");
+  US_CHECK_ARG(dx != nullptr && part_d != nullptr, "pw_small_bwd_relu: dx and part_d required");
+  const int G = unetseg_pw_small_tiles(M);
+  hipStream_t st = (hipStream_t)stream;
+  if (k == 1)
+    hipLaunchKernelGGL((pw_small_bwd_kernel<bf16, 1, true>), dim3(G), dim3(256), 0, st, dy, (const bf16*)x, ldx, M, hw,
+                       c, w, (bf16*)dx, lddx, 0, part_w, part_b, G, 2048, part_d);
+  else
+    hipLaunchKernelGGL((pw_small_bwd_kernel<bf16, 2, true>), dim3(G), dim3(256), 0, st, dy, (const bf16*)x, ldx, M, hw,
+                       c, w, (bf16*)dx, lddx, 0, part_w, part_b, G, 2048, part_d);
+  US_LAUNCH_CHECK("pw_small_bwd_relu");
   return 0;
 }
 

@@ -50,6 +50,7 @@ SIGNATURES = {
     "unetseg_pw_small_tiles": (I, [L]),
     "unetseg_pw_small_fwd": (I, [I, P, I, L, I, I, I, P, P, P, P, P]),
     "unetseg_pw_small_bwd": (I, [I, P, P, I, L, I, I, I, P, P, I, I, P, P, P]),
+    "unetseg_pw_small_bwd_relu": (I, [I, P, P, I, L, I, I, I, P, P, I, P, P, P, P]),
     "unetseg_attn_apply": (I, [I, P, I, P, P, P, P, P, I, L, I, P]),
     "unetseg_attn_bwd1": (I, [I, P, I, P, I, P, P, P, P, P, I, I, P, L, I, P, P]),
     "unetseg_attn_bwd2": (I, [I, P, P, P, P, P, P, I, P, P, I, L, I, P, P, P]),

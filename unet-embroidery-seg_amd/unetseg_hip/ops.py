@@ -593,9 +593,20 @@ def pw_head(ctx, x, conv_mod):
         dy = dy.contiguous().float()
         G = lib.pw_small_tiles(M)
         pw, pb = ctx.f32(K, C, G), ctx.f32(K, G)
-        dx, acc = (gbuf(ctx, x) if x.need_grad else (None, 0))
-        lib.pw_small_bwd(ctx.dt, P(dy), P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(dx), ldp(dx), acc,
-                         P(pw), P(pb), ctx.stream)
+        if (FUSE and x.need_grad and x.fuse is not None and x.fuse[0] == 1 and x.fuse[1] is X
+                and x.grad is None and x.uses == 1 and ctx.dt == DT_BF16):
+            # x is a ReLU output consumed only here: its backward mask and the producer conv's
+            # bias-gradient partials ride along (conv() reads them back from x.fused)
+            dx = ctx.empty(N, H, W, C)
+            part = ctx.f32(G, 2, C)
+            lib.pw_small_bwd_relu(ctx.dt, P(dy), P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(dx), ldp(dx),
+                                  P(pw), P(pb), P(part), ctx.stream)
+            x.grad = dx
+            x.fused = (part, G)
+        else:
+            dx, acc = (gbuf(ctx, x) if x.need_grad else (None, 0))
+            lib.pw_small_bwd(ctx.dt, P(dy), P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(dx), ldp(dx), acc,
+                             P(pw), P(pb), ctx.stream)
         lib.colsum_finalize(P(pw), K * C, G, P(conv_mod.weight.grad), 1, ctx.stream)
         lib.colsum_finalize(P(pb), K, G, P(conv_mod.bias.grad), 1, ctx.stream)
         ctx.param_done(conv_mod.weight, conv_mod.bias)
