@@ -299,6 +299,33 @@ def test_upsample(dtname, align, H, W):
     assert _rel(_nchw(xn.grad), xr.grad) < tol
 
 
+@pytest.mark.parametrize("dtname", ["fp32", "bf16"])
+@pytest.mark.parametrize("align", [True, False])
+@pytest.mark.parametrize("H,C", [(4, 1024), (16, 256), (32, 64)])
+def test_upsample_strided_grad(dtname, align, H, C):
+    """model-shaped upsample whose gradient arrives as a channel slice of a concat gradient
+    (ld > C), accumulated onto an existing gradient"""
+    ops, DT_BF16, DT_F32 = _ops()
+    dt = DT_BF16 if dtname == "bf16" else DT_F32
+    g = torch.Generator().manual_seed(5)
+    x = _round(torch.randn(2, C, H, H, generator=g), dt)
+    ctx = _ctx(dt)
+    xn = _node(x, dt)
+    y = ops.upsample2x(ctx, xn, align)
+    xr = x.clone().requires_grad_(True)
+    ref = F.interpolate(xr, scale_factor=2, mode="bilinear", align_corners=align)
+    tol = 1e-2 if dt == DT_BF16 else 1e-6
+    assert _rel(_nchw(y.data), ref.detach()) < tol
+    dy = _round(torch.randn(2, C + 32, 2 * H, 2 * H, generator=g), dt)
+    full = _node(dy, dt).data
+    y.grad = full[..., 32:]
+    g0 = _round(torch.randn(x.shape, generator=g), dt)
+    xn.grad = _node(g0, dt).data.clone()
+    ctx.backward()
+    ref.backward(dy[:, 32:])
+    assert _rel(_nchw(xn.grad), xr.grad + g0) < tol
+
+
 @pytest.mark.parametrize("B,H,W", [(3, 40, 48), (2, 64, 64), (1, 7, 5)])
 def test_lovasz_matches_oracle(B, H, W):
     from oracle import ref_cpu

@@ -545,32 +545,39 @@ __device__ __forceinline__ void up_src(int d, int in, int out, int align, int& i
   l1 = src - (float)i0;
 }
 
+// Row-blocked: a block covers (pixel, 8-channel) lanes of whole output rows, kRowsPB rows in turn,
+// so the per-row source index and weight are wave-uniform and the per-column ones are computed
+// once per lane (the flat form spent its time in 64-bit index division).
+constexpr int kUpRowsPB = 4;
+
 template <typename T>
 __global__ void upsample_fwd_kernel(const T* x, int ldx, int N, int H, int W, int C, int align, T* y, int ldy) {
   constexpr int V = VE<T>;
   const int cv = C / V, OH = 2 * H, OW = 2 * W;
-  const long total = (long)N * OH * OW * cv;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    long t = i;
-    const int v = (int)(t % cv); t /= cv;
-    const int ow = (int)(t % OW); t /= OW;
-    const int oh = (int)(t % OH);
-    const int n = (int)(t / OH);
-    int h0, h1, w0, w1;
-    float lh, lw;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= OW * cv) return;
+  const int ow = idx / cv, c0 = (idx - ow * cv) * V;
+  int w0, w1;
+  float lw;
+  up_src(ow, W, OW, align, w0, w1, lw);
+  const float wl0 = 1.f - lw;
+  const int r0 = blockIdx.y * kUpRowsPB, r1 = min(r0 + kUpRowsPB, N * OH);
+  for (int r = r0; r < r1; ++r) {
+    const int n = r / OH, oh = r - n * OH;
+    int h0, h1;
+    float lh;
     up_src(oh, H, OH, align, h0, h1, lh);
-    up_src(ow, W, OW, align, w0, w1, lw);
-    const int c0 = v * V;
+    const T* x0 = x + (long)(n * H + h0) * W * ldx + c0;
+    const T* x1 = x + (long)(n * H + h1) * W * ldx + c0;
     float a[V], b[V], c[V], d[V], o[V];
-    const long base = (long)n * H * W;
-    load_vec(x + (base + (long)h0 * W + w0) * ldx + c0, a);
-    load_vec(x + (base + (long)h0 * W + w1) * ldx + c0, b);
-    load_vec(x + (base + (long)h1 * W + w0) * ldx + c0, c);
-    load_vec(x + (base + (long)h1 * W + w1) * ldx + c0, d);
-    const float hl0 = 1.f - lh, wl0 = 1.f - lw;
+    load_vec(x0 + (long)w0 * ldx, a);
+    load_vec(x0 + (long)w1 * ldx, b);
+    load_vec(x1 + (long)w0 * ldx, c);
+    load_vec(x1 + (long)w1 * ldx, d);
+    const float hl0 = 1.f - lh;
 #pragma unroll
     for (int e = 0; e < V; ++e) o[e] = hl0 * (wl0 * a[e] + lw * b[e]) + lh * (wl0 * c[e] + lw * d[e]);
-    store_vec(y + ((long)(n * OH + oh) * OW + ow) * ldy + c0, o);
+    store_vec(y + ((long)r * OW + ow) * ldy + c0, o);
   }
 }
 
@@ -585,61 +592,58 @@ __device__ __forceinline__ float up_w(int d, int i, int in, int out, int align) 
   return w;
 }
 
-// gather form of the adjoint: dx[h][w] (+)= sum_{oh,ow} wh(oh,h) ww(ow,w) dy[oh][ow]
+// candidate output range of input index i along one axis (a superset; exact weights decide)
+__device__ __forceinline__ void up_range(int i, int in, int out, int align, int& lo, int& hi) {
+  if (align) {
+    lo = in > 1 ? (int)floorf((float)(i - 1) * (out - 1) / (float)(in - 1)) : 0;
+    hi = in > 1 ? (int)ceilf((float)(i + 1) * (out - 1) / (float)(in - 1)) : out - 1;
+  } else {
+    lo = 2 * i - 2;
+    hi = i == in - 1 ? out - 1 : 2 * i + 2;
+  }
+  lo = max(lo, 0);
+  hi = min(hi, out - 1);
+}
+
+// gather form of the adjoint: dx[h][w] (+)= sum_{oh,ow} wh(oh,h) ww(ow,w) dy[oh][ow]; row-blocked
+// like the forward (row weights wave-uniform, column weights once per lane)
 template <typename T>
 __global__ void upsample_bwd_kernel(const T* dy, int ldy, int N, int H, int W, int C, int align, T* dx, int ldx,
                                     int accumulate) {
   constexpr int V = VE<T>;
   const int cv = C / V, OH = 2 * H, OW = 2 * W;
-  const long total = (long)N * H * W * cv;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    long t = i;
-    const int v = (int)(t % cv); t /= cv;
-    const int w = (int)(t % W); t /= W;
-    const int h = (int)(t % H);
-    const int n = (int)(t / H);
-    const int c0 = v * V;
-    // candidate output ranges (a superset; exact weights decide)
-    int ohl, ohh, owl, owh;
-    if (align) {
-      ohl = H > 1 ? (int)floorf((float)(h - 1) * (OH - 1) / (float)(H - 1)) : 0;
-      ohh = H > 1 ? (int)ceilf((float)(h + 1) * (OH - 1) / (float)(H - 1)) : OH - 1;
-      owl = W > 1 ? (int)floorf((float)(w - 1) * (OW - 1) / (float)(W - 1)) : 0;
-      owh = W > 1 ? (int)ceilf((float)(w + 1) * (OW - 1) / (float)(W - 1)) : OW - 1;
-    } else {
-      ohl = 2 * h - 2; ohh = 2 * h + 2;
-      owl = 2 * w - 2; owh = 2 * w + 2;
-      if (h == H - 1) ohh = OH - 1;
-      if (w == W - 1) owh = OW - 1;
-    }
-    ohl = max(ohl, 0); owl = max(owl, 0);
-    ohh = min(ohh, OH - 1); owh = min(owh, OW - 1);
-    // per-axis weights first (<= 6 candidates each for a x2 resize, most zero), then only the
-    // nonzero pairs load
-    float whv[8], wwv[8];
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= W * cv) return;
+  const int w = idx / cv, c0 = (idx - w * cv) * V;
+  int owl, owh;
+  up_range(w, W, OW, align, owl, owh);
+  float wwv[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      whv[k] = ohl + k <= ohh ? up_w(ohl + k, h, H, OH, align) : 0.f;
-      wwv[k] = owl + k <= owh ? up_w(owl + k, w, W, OW, align) : 0.f;
-    }
+  for (int k = 0; k < 8; ++k) wwv[k] = owl + k <= owh ? up_w(owl + k, w, W, OW, align) : 0.f;
+  const int r0 = blockIdx.y * kUpRowsPB, r1 = min(r0 + kUpRowsPB, N * H);
+  for (int r = r0; r < r1; ++r) {
+    const int n = r / H, h = r - n * H;
+    int ohl, ohh;
+    up_range(h, H, OH, align, ohl, ohh);
     float acc[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) acc[e] = 0.f;
 #pragma unroll
     for (int kh = 0; kh < 8; ++kh) {
-      if (whv[kh] == 0.f) continue;
-      const long rowb = (long)(n * OH + ohl + kh) * OW;
+      const float wh = ohl + kh <= ohh ? up_w(ohl + kh, h, H, OH, align) : 0.f;
+      if (wh == 0.f) continue;
+      const T* row = dy + (long)(n * OH + ohl + kh) * OW * ldy + c0;
 #pragma unroll
       for (int kw = 0; kw < 8; ++kw) {
         if (wwv[kw] == 0.f) continue;
         float g[V];
-        load_vec(dy + (rowb + owl + kw) * ldy + c0, g);
-        const float wt = whv[kh] * wwv[kw];
+        load_vec(row + (long)(owl + kw) * ldy, g);
+        const float wt = wh * wwv[kw];
 #pragma unroll
         for (int e = 0; e < V; ++e) acc[e] += wt * g[e];
       }
     }
-    T* o = dx + ((long)(n * H + h) * W + w) * ldx + c0;
+    T* o = dx + ((long)r * W + w) * ldx + c0;
     if (accumulate) {
       float old[V];
       load_vec(o, old);
@@ -1224,7 +1228,8 @@ UNETSEG_API int unetseg_maxpool_bwd(int dtype, const void* dy, int ldy, const ui
 UNETSEG_API int unetseg_upsample2x_fwd(int dtype, const void* x, int ldx, int n, int h, int w, int c,
                                        int align_corners, void* y, int ldy, void* stream) {
   CHECK_VEC(dtype, c, "upsample_fwd");
-  DISPATCH_T(dtype, hipLaunchKernelGGL(upsample_fwd_kernel<T>, dim3(grid_for((long)n * 4 * h * w * c / VE<T>)),
+  DISPATCH_T(dtype, hipLaunchKernelGGL(upsample_fwd_kernel<T>,
+                                       dim3(ceil_div(2 * w * (c / VE<T>), 256), ceil_div(n * 2 * h, kUpRowsPB)),
                                        dim3(256), 0, (hipStream_t)stream, (const T*)x, ldx, n, h, w, c, align_corners,
                                        (T*)y, ldy));
   US_LAUNCH_CHECK("upsample_fwd");
@@ -1234,9 +1239,10 @@ UNETSEG_API int unetseg_upsample2x_fwd(int dtype, const void* x, int ldx, int n,
 UNETSEG_API int unetseg_upsample2x_bwd(int dtype, const void* dy, int ldy, int n, int h, int w, int c,
                                        int align_corners, void* dx, int ldx, int accumulate, void* stream) {
   CHECK_VEC(dtype, c, "upsample_bwd");
-  DISPATCH_T(dtype, hipLaunchKernelGGL(upsample_bwd_kernel<T>, dim3(grid_for((long)n * h * w * c / VE<T>)), dim3(256),
-                                       0, (hipStream_t)stream, (const T*)dy, ldy, n, h, w, c, align_corners, (T*)dx,
-                                       ldx, accumulate));
+  DISPATCH_T(dtype, hipLaunchKernelGGL(upsample_bwd_kernel<T>,
+                                       dim3(ceil_div(w * (c / VE<T>), 256), ceil_div(n * h, kUpRowsPB)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)dy, ldy, n, h, w, c, align_corners, (T*)dx, ldx,
+                                       accumulate));
   US_LAUNCH_CHECK("upsample_bwd");
   return 0;
 }
