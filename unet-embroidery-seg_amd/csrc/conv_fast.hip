@@ -572,7 +572,11 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
 // ------------------------------------------------------------------------------------------
 constexpr int kWgBK = 32;  // 64 halves the barriers but costs a wave per SIMD: slower here
 
-template <int BM, int BN, int NWM, int NWN>
+// ROW32 (Q % 32 == 0): the 32 pixels of a K step are one run of an output row, so (image, row,
+// first column) is wave-uniform scalar state and each staged row's offset is a scalar base plus a
+// per-lane constant (tap shift, column, channel): a few VALU per row instead of re-deriving the
+// pixel, its bounds and its 32-bit offset every step.
+template <int BM, int BN, int NWM, int NWN, bool ROW32 = false>
 __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArgs a) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int BKW = kWgBK;
@@ -638,7 +642,59 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
   const unsigned a_colb0 = (unsigned)m0 * 2u;
 
   uint4 ra[A_PER], rbv[B_PER];
+  // ---- ROW32 addressing: lane constants and scalar (image, row, column) of the next K step ----
+  unsigned a_off[A_PER], b_l1[B_PER], b_l2[B_PER];
+  int b_lw[B_PER];
+  bool a_ok[A_PER];
+  int s_n = 0, s_p = 0, s_q = 0;
+  if constexpr (ROW32) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      a_ok[i] = (m0 + a_cv[i] * 8) < a.Cout;
+      a_off[i] = (unsigned)a_row[i] * (unsigned)a.ldyb + a_colb0 + a_cv[i] * 16u;
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      b_lw[i] = b_row[i] * a.stride + b_dw[i];
+      const int dpix = b_dh[i] * a.W + b_lw[i];  // relative to the step's (row, first column) pixel
+      b_l1[i] = (unsigned)(dpix * a.ldc1b) + b_cb[i];
+      b_l2[i] = (unsigned)(dpix * a.ldc2b) + b_cb[i];
+    }
+    const long k = kt0 * BKW;
+    s_n = (int)(k / PQ);
+    const int rem = (int)(k - (long)s_n * PQ);
+    s_p = rem / a.Q;
+    s_q = rem - s_p * a.Q;
+  }
+  auto gload_row = [&](long kt) {
+    const unsigned abase = (unsigned)(kt * BKW) * (unsigned)a.ldyb;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) ra[i] = bload(rdy, a_ok[i] ? abase + a_off[i] : kOOB);
+    const int ihb = s_p * a.stride, iwb = s_q * a.stride;
+    const int pixb = (s_n * a.H + ihb) * a.W + iwb;
+    const unsigned base1 = (unsigned)pixb * (unsigned)a.ldc1b, base2 = (unsigned)pixb * (unsigned)a.ldc2b;
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const bool ok = (unsigned)(ihb + b_dh[i]) < (unsigned)a.H && (unsigned)(iwb + b_lw[i]) < (unsigned)a.W;
+      if (b_src[i] == 0)
+        rbv[i] = bload(r1, ok ? base1 + b_l1[i] : kOOB);
+      else
+        rbv[i] = bload(r2, ok ? base2 + b_l2[i] : kOOB);
+    }
+    s_q += BKW;
+    if (s_q == a.Q) {
+      s_q = 0;
+      if (++s_p == a.P) {
+        s_p = 0;
+        ++s_n;
+      }
+    }
+  };
   auto gload = [&](long kt) {
+    if constexpr (ROW32) {
+      gload_row(kt);
+      return;
+    }
     const long k0 = kt * BKW;  // first pixel of the step (uniform)
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
@@ -888,25 +944,32 @@ int wgrad_fast_splits(int Cout, int Ng, long Kpix) {
   return sp;
 }
 
-template <int BM, int BN, int NWM, int NWN>
+template <int BM, int BN, int NWM, int NWN, bool ROW32>
 static void launch_wgrad_cfg(const FastWgradArgs& a, int splits, hipStream_t st) {
   const size_t lds = 2 * (size_t)kWgBK * (BM / 8 + BN / 8) * 16;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_fast_kernel<BM, BN, NWM, NWN>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_fast_kernel<BM, BN, NWM, NWN, ROW32>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   dim3 grid(ceil_div(a.Cout, BM), ceil_div(a.Ng, BN), splits);
-  hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN, NWM, NWN>), grid, dim3(64 * NWM * NWN), lds, st, a);
+  hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN, NWM, NWN, ROW32>), grid, dim3(64 * NWM * NWN), lds, st, a);
 }
 
 int launch_wgrad_fast(FastWgradArgs a, int splits, hipStream_t st) {
   const long nkt = (a.Kpix + kWgBK - 1) / kWgBK;
   a.kt_per_split = (int)((nkt + splits - 1) / splits);
-  if (a.Cout <= 64)
-    launch_wgrad_cfg<64, 256, 1, 4>(a, splits, st);
-  else
-    launch_wgrad_cfg<128, 128, 2, 2>(a, splits, st);
+  static const bool no_row = getenv("UNETSEG_WG_NO_ROW32") != nullptr;
+  // ROW32: every K step is one 32-pixel run of an output row, and the per-lane pixel deltas and
+  // scalar bases fit 32-bit offsets (the caller bounds both tensors below 2^31 bytes)
+  const bool row32 = !no_row && a.Q % kWgBK == 0;
+  if (a.Cout <= 64) {
+    if (row32) launch_wgrad_cfg<64, 256, 1, 4, true>(a, splits, st);
+    else launch_wgrad_cfg<64, 256, 1, 4, false>(a, splits, st);
+  } else {
+    if (row32) launch_wgrad_cfg<128, 128, 2, 2, true>(a, splits, st);
+    else launch_wgrad_cfg<128, 128, 2, 2, false>(a, splits, st);
+  }
   return 0;
 }
