@@ -33,9 +33,19 @@ __device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, unsigned off,
   asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
 }
 
-template <int TH, int NW, int POST>
+// EPI: epilogue flags fixed at compile time (kEpiBias | kEpiRelu | kEpiStats | kEpiAcc), or kEpiDyn
+// to read them from the arguments; with them fixed the tile epilogue has no uniform branches and
+// the bias sits in registers.
+constexpr int kEpiBias = 1, kEpiRelu = 2, kEpiStats = 4, kEpiAcc = 8, kEpiDyn = 16;
+
+template <int TH, int NW, int POST, int EPI>
 __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_w, int tiles_h, int n_sp, int G_per,
                                                         unsigned y_bytes) {
+  constexpr bool kDyn = (EPI & kEpiDyn) != 0;
+  const bool has_bias = kDyn ? a.bias != nullptr : (EPI & kEpiBias) != 0;
+  const bool do_relu = kDyn ? a.relu != 0 : (EPI & kEpiRelu) != 0;
+  const bool do_stats = kDyn ? a.stats != nullptr : (EPI & kEpiStats) != 0;
+  const bool do_acc = kDyn ? a.accumulate != 0 : (EPI & kEpiAcc) != 0;
   // wave w owns output rows [w*TH/NW, (w+1)*TH/NW)
   constexpr int RPW = TH / NW;               // rows per wave
   constexpr int FP = RPW * (HW_TW / 16);     // 16-pixel groups per wave
@@ -64,7 +74,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   const __amdgpu_buffer_rsrc_t ry = srd(a.y, y_bytes);
   (void)ntn;
 
-  if (a.bias && tid < 64) sbias[tid] = a.bias[n0 + tid];
+  if (kDyn && a.bias && tid < 64) sbias[tid] = a.bias[n0 + tid];
   // BN post-op coefficients of this block's 64 channels live in `red` (free in dgrad: no stats)
   float* pco = red;  // [4][64]: sc, sh, mean, inv
   if (POST == 2 && tid < 64) {
@@ -131,6 +141,11 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   // halo tap offsets (uniform): jt -> (dh, dw)
   const int dh0 = a.dh0, dhs = a.dhs, dw0 = a.dw0, dws = a.dws;
   const int j16 = lane & 15, kg = lane >> 4;
+  float breg[FC][4];  // this lane's 16 output channels' bias (compile-time flags only)
+#pragma unroll
+  for (int c = 0; c < FC; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) breg[c][e] = (!kDyn && has_bias) ? a.bias[n0 + c * 16 + kg * 4 + e] : 0.f;
 
   for (int t = 0; t < my_tiles; ++t) {
     const int stage = t & 1;
@@ -209,10 +224,10 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = acc[c][p][e] + (a.bias ? sbias[cb + e] : 0.f);
-          if (a.relu) v[e] = fmaxf(v[e], 0.f);
+          v[e] = acc[c][p][e] + (!has_bias ? 0.f : kDyn ? sbias[cb + e] : breg[c][e]);
+          if (do_relu) v[e] = fmaxf(v[e], 0.f);
         }
-        if (a.accumulate) {
+        if (do_acc) {
           const bf16* ob = reinterpret_cast<const bf16*>((const char*)a.y + outo[p] + cb * 2);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += (float)ob[e];
@@ -249,7 +264,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
         outv[c][p] = *reinterpret_cast<uint2*>(o);
       }
     }
-    if (a.stats) {
+    if (do_stats) {
       // per-tile BN partials over the TH*32 pixels: column sums, then M2 about the tile mean
 #pragma unroll
       for (int c = 0; c < FC; ++c)
@@ -499,7 +514,7 @@ bool halo3_ok(const FastTNArgs& a) {
   return true;
 }
 
-template <int TH, int NW, int POST>
+template <int TH, int NW, int POST, int EPI>
 static int launch_halo3_cfg(const FastTNArgs& a, hipStream_t st) {
   const int tiles_w = a.wc / HW_TW, tiles_h = a.hc / TH;
   const int n_img = a.M / (a.hc * a.wc);
@@ -511,12 +526,12 @@ static int launch_halo3_cfg(const FastTNArgs& a, hipStream_t st) {
   const size_t lds = halo_lds_bytes<TH, NW>();
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_kernel<TH, NW, POST>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_kernel<TH, NW, POST, EPI>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const unsigned y_bytes = (unsigned)((long)a.M * a.ldy * 2);
-  hipLaunchKernelGGL((halo3_kernel<TH, NW, POST>), dim3(ntn * G_per), dim3(64 * NW), lds, st, a, tiles_w, tiles_h, n_sp,
+  hipLaunchKernelGGL((halo3_kernel<TH, NW, POST, EPI>), dim3(ntn * G_per), dim3(64 * NW), lds, st, a, tiles_w, tiles_h, n_sp,
                      G_per, y_bytes);
   return 0;
 }
@@ -534,9 +549,23 @@ int halo3_blocks(const FastTNArgs& a) {
 int launch_halo3(const FastTNArgs& a, hipStream_t st) {
   static const int nw = getenv("UNETSEG_HALO_W4") ? 4 : 8;
   // fused dgrad post-ops are separate instantiations: their registers must not cost the plain path
-  if (a.post == 1) return launch_halo3_cfg<8, 8, 1>(a, st);
-  if (a.post == 2) return launch_halo3_cfg<8, 8, 2>(a, st);
-  return nw == 4 ? launch_halo3_cfg<8, 4, 0>(a, st) : launch_halo3_cfg<8, 8, 0>(a, st);
+  static const bool dyn = getenv("UNETSEG_HALO_EPI_DYN") != nullptr;
+  const int epi = (a.bias ? kEpiBias : 0) | (a.relu ? kEpiRelu : 0) | (a.stats ? kEpiStats : 0) |
+                  (a.accumulate ? kEpiAcc : 0);
+  // fused dgrad post-ops come with a plain epilogue (no bias / ReLU / stats / accumulate)
+  if (a.post == 1) return epi == 0 && !dyn ? launch_halo3_cfg<8, 8, 1, 0>(a, st) : launch_halo3_cfg<8, 8, 1, kEpiDyn>(a, st);
+  if (a.post == 2) return epi == 0 && !dyn ? launch_halo3_cfg<8, 8, 2, 0>(a, st) : launch_halo3_cfg<8, 8, 2, kEpiDyn>(a, st);
+  if (nw == 4) return launch_halo3_cfg<8, 4, 0, kEpiDyn>(a, st);
+  // the epilogues the U-Net runs: conv+bias+ReLU (decoder), conv with BN statistics (encoder),
+  // plain data gradient, accumulated data gradient
+  if (!dyn) switch (epi) {
+      case kEpiBias | kEpiRelu: return launch_halo3_cfg<8, 8, 0, kEpiBias | kEpiRelu>(a, st);
+      case kEpiStats: return launch_halo3_cfg<8, 8, 0, kEpiStats>(a, st);
+      case 0: return launch_halo3_cfg<8, 8, 0, 0>(a, st);
+      case kEpiAcc: return launch_halo3_cfg<8, 8, 0, kEpiAcc>(a, st);
+      default: break;
+    }
+  return launch_halo3_cfg<8, 8, 0, kEpiDyn>(a, st);
 }
 
 bool halo3_wgrad_ok(const HaloWgradArgs& a) {
