@@ -88,8 +88,11 @@ def _run_hip(m, name, x, y, c, mask):
 @pytest.mark.parametrize("name", MODELS)
 def test_model_fp32_parity(name):
     """fp32 mode: logits within 1e-3 of the fp32 oracle; gradients no further from the fp64 oracle
-    than 3x the fp32 oracle's own distance from it (the backward is ill-conditioned at B=2, 64^2:
-    the fp32 oracle itself sits ~3 % from fp64)."""
+    than 2x the fp32 oracle's own distance from it.  The backward is ill-conditioned at B=2, 64^2
+    (BN over a handful of pixels, lovasz sort order): scaling the input by 1 +- 1e-7 (one ulp) moves
+    the fp32 oracle's own median error by ~2x (2.9e-4 -> 5.1e-4 on unet_plain), so the reference
+    distance is the largest over the unperturbed and the two one-ulp-perturbed oracle runs --
+    otherwise a rounding-level change in any HIP kernel flips the verdict."""
     from oracle import ref_cpu
     from unetseg_hip import losses
 
@@ -104,11 +107,15 @@ def test_model_fp32_parity(name):
     assert err < 1e-3, err
     assert abs(loss - l32) < 1e-4 * max(1.0, abs(l32)), (loss, l32)
     scale = float(np.median([v.norm().item() for v in g64.values()]))
-    e_hip, e_cpu = _grad_errors(g, g64, scale), _grad_errors(g32, g64, scale)
-    med_h, med_c = np.median(list(e_hip.values())), np.median(list(e_cpu.values()))
+    e_hip = _grad_errors(g, g64, scale)
+    e_runs = [_grad_errors(g32, g64, scale)]
+    for d in (1e-7, -1e-7):
+        e_runs.append(_grad_errors(_oracle_grads(name, state, x * (1 + d), y, c, mask, torch.float32)[2], g64, scale))
+    med_h = np.median(list(e_hip.values()))
+    med_c = max(np.median(list(e.values())) for e in e_runs)
     assert med_h <= 2.0 * med_c + 1e-4, (med_h, med_c)
-    worst = max(e_hip.values())
-    assert worst <= 3.0 * max(e_cpu.values()) + 1e-3, (worst, max(e_cpu.values()))
+    worst, worst_c = max(e_hip.values()), max(max(e.values()) for e in e_runs)
+    assert worst <= 3.0 * worst_c + 1e-3, (worst, worst_c)
     msd = m.state_dict()
     for k, v in b32.items():
         if k.endswith("running_mean") or k.endswith("running_var"):

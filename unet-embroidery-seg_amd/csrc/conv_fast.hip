@@ -244,7 +244,7 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
   if constexpr (kDMA && TAPS > 0) {
     constexpr int NS = ST - 10, PER = A_PER + B_PER;
     static_assert(NS >= 3 && PER * (NS - 2) <= 63, "vmcnt range");
-    static_assert(A_PER % 2 == 0 && B_PER % 2 == 0, "rows are issued in pairs");
+    static_assert(A_PER % 2 == 0 && (B_PER % 2 == 0 || B_PER == 1), "rows are issued in pairs");
     // (row, tap) -> gather pixel, or pbad: one past every source's last pixel, so pbad * ldcb is
     // out of range for either source (the launcher checks it cannot wrap 32 bits)
     const unsigned pb1 = a.x1_bytes / (unsigned)a.ldc1b;
@@ -280,9 +280,13 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
       for (int i = 0; i < A_PER; i += 2)
         dma16x2<RSTEP * 128>(rx, sb + (unsigned)(RSTEP * i * 128), __umul24(vpix[i][t], ldcb) + kv16,
                              __umul24(vpix[i + 1][t], ldcb) + kv16, soff);
+      if constexpr (B_PER == 1) {
+        dma16s(rwx, sb + (unsigned)(BM * 128), boff[0], wsoff);
+      } else {
 #pragma unroll
-      for (int i = 0; i < B_PER; i += 2)
-        dma16x2<RSTEP * 128>(rwx, sb + (unsigned)((BM + RSTEP * i) * 128), boff[i], boff[i + 1], wsoff);
+        for (int i = 0; i < B_PER; i += 2)
+          dma16x2<RSTEP * 128>(rwx, sb + (unsigned)((BM + RSTEP * i) * 128), boff[i], boff[i + 1], wsoff);
+      }
     };
 #pragma unroll
     for (int s0 = 0; s0 < NS - 1; ++s0) issue(s0 / TAPS, s0 % TAPS, s0);
@@ -860,13 +864,15 @@ static int launch_tn_dma(const FastTNArgs& a, hipStream_t st) {
 static int tn_config(const FastTNArgs& a) {
   if (const char* e = getenv("UNETSEG_TN_CFG")) {  // experiments: force a configuration (1..10)
     const int c = atoi(e);
-    if (c >= 1 && c <= 12) return c;
+    if (c >= 1 && c <= 14) return c;
   }
   static const bool no_dma = getenv("UNETSEG_TN_NO_DMA") != nullptr;
   if (halo3_ok(a)) return 0;
   const int nsteps = a.nr * a.ns * (a.cin >> 6);
   if (nsteps == 1 && a.Ng > 64) return 4;
-  if (a.Ng <= 64) return 6;  // 128x64 (two-step prefetch, 3 blocks/CU): 5-10 % over 256x64
+  // 128x64 (two-step prefetch, 3 blocks/CU): 5-10 % over 256x64; deep 3x3 K on the 3-stage ring
+  // with compile-time taps: ~8 % more (192->64 at 256x256: 390 -> 357 us)
+  if (a.Ng <= 64) return (!no_dma && nsteps >= 18 && tn_taps(a) == 9) ? 13 : 6;
   if (nsteps <= 4) return 3;
   const long tiles_big = (long)ceil_div(a.M, 256) * ceil_div(a.Ng, 128);
   if (tiles_big >= 256) return no_dma ? 2 : 7;
@@ -883,7 +889,7 @@ static int tn_config(const FastTNArgs& a) {
 // row tile (BM) of each TN configuration
 static int tn_cfg_bm(int cfg) {
   switch (cfg) {
-    case 1: case 2: case 7: case 11: return 256;
+    case 1: case 2: case 7: case 11: case 14: return 256;
     case 5: case 9: return 64;
     default: return 128;
   }
@@ -922,6 +928,8 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 10: return launch_tn_dma<128, 128, 2, 2, 15>(a, st);
     case 11: return launch_tn_dma<256, 64, 4, 1, 13>(a, st);
     case 12: return launch_tn_dma<128, 64, 2, 2, 14>(a, st);
+    case 13: return launch_tn_dma<128, 64, 2, 2, 13>(a, st);
+    case 14: return launch_tn_dma<256, 64, 4, 2, 13>(a, st);
     default: return a.post ? launch_tn_cfg<128, 128, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 3>(a, st);
   }
 }

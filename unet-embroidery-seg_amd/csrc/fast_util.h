@@ -42,6 +42,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t srd_u(const void* p, unsigned 
   const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(q >> 32));
   return srd((const void*)(size_t)(((unsigned long long)hi << 32) | lo), __builtin_amdgcn_readfirstlane(bytes));
 }
+// one LDS-DMA row with a scalar offset (see dma16x2)
+__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, unsigned lds_byte, unsigned voff, unsigned soff) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds_byte), "v"(voff), "s"(r), "s"(soff)
+      : "memory");
+}
 // (M0 is set with s_mov only: an s_add would clobber SCC behind the compiler's back)
 template <int STRIDE>
 __device__ __forceinline__ void dma16x2(__amdgpu_buffer_rsrc_t r, unsigned lds_byte, unsigned v0, unsigned v1,
