@@ -326,6 +326,37 @@ def test_upsample_strided_grad(dtname, align, H, C):
     assert _rel(_nchw(xn.grad), xr.grad + g0) < tol
 
 
+@pytest.mark.parametrize("dtname", ["fp32", "bf16"])
+@pytest.mark.parametrize("K", [1, 2])
+@pytest.mark.parametrize("N,H,W", [(2, 37, 50), (1, 64, 64), (3, 5, 7)])
+def test_pw_head(dtname, K, N, H, W):
+    """1x1 head conv (64 -> K, bias) to fp32 NCHW logits, forward and backward"""
+    ops, DT_BF16, DT_F32 = _ops()
+    from unetseg_hip.nn import Conv2d
+    dt = DT_BF16 if dtname == "bf16" else DT_F32
+    g = torch.Generator().manual_seed(13)
+    conv = Conv2d(64, K, 1).to(DEV)
+    conv.weight.grad = torch.zeros_like(conv.weight)
+    conv.bias.grad = torch.zeros_like(conv.bias)
+    x = _round(torch.randn(N, 64, H, W, generator=g), dt)
+    ctx = _ctx(dt)
+    xn = _node(x, dt)
+    y, holder = ops.pw_head(ctx, xn, conv)
+    xr = x.clone().requires_grad_(True)
+    wr = conv.weight.detach().cpu().clone().requires_grad_(True)
+    br = conv.bias.detach().cpu().clone().requires_grad_(True)
+    ref = F.conv2d(xr, wr, br)
+    tol = 2e-2 if dt == DT_BF16 else 1e-5
+    assert _rel(y.cpu(), ref.detach()) < tol
+    dy = torch.randn(ref.shape, generator=g)
+    holder["grad"] = dy.to(DEV)
+    ctx.backward()
+    ref.backward(dy)
+    assert _rel(_nchw(xn.grad), xr.grad) < tol
+    assert _rel(conv.weight.grad.cpu(), wr.grad) < 1e-4
+    assert _rel(conv.bias.grad.cpu(), br.grad) < 1e-4
+
+
 @pytest.mark.parametrize("B,H,W", [(3, 40, 48), (2, 64, 64), (1, 7, 5)])
 def test_lovasz_matches_oracle(B, H, W):
     from oracle import ref_cpu

@@ -679,14 +679,64 @@ __global__ void pw_small_fwd_kernel(const T* x, int ldx, long M, int HW, int C, 
   const int ppw = 64 / cv;  // pixels per wave pass
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int sub = lane / cv, v = lane % cv;
-  const long p0 = (long)blockIdx.x * pix_per_block;
-  const long p1 = min(M, p0 + pix_per_block);
+  const int ppb = pix_per_block < 0 ? -pix_per_block : pix_per_block;
+  const long p0 = (long)blockIdx.x * ppb;
+  const long p1 = min(M, p0 + ppb);
   float wv[K][V];
 #pragma unroll
   for (int k = 0; k < K; ++k)
 #pragma unroll
     for (int e = 0; e < V; ++e) wv[k][e] = w[k * C + v * V + e];
   double lsum = 0.0;
+  if (cv == 8 && !stats && pix_per_block > 0) {
+    // 8 lanes per pixel: four pixel groups per iteration (four 16-B loads in flight per lane),
+    // 8-lane sums by DPP (xor 1, xor 2 within quads, then row_half_mirror: lane 0 of each 8-lane
+    // group adds lane 7, i.e. the other quad's sum) instead of LDS-routed shuffles
+    constexpr int U = 4;
+    for (long pbase = p0 + (long)wid * 8 * U; pbase < p1; pbase += (long)nw * 8 * U) {
+      float acc[U][K];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long p = pbase + u * 8 + sub;
+        float xv[V];
+        if (p < p1) {
+          load_vec(x + p * ldx + v * V, xv);
+        } else {
+#pragma unroll
+          for (int e = 0; e < V; ++e) xv[e] = 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          float a0 = 0.f;
+#pragma unroll
+          for (int e = 0; e < V; ++e) a0 += xv[e] * wv[k][e];
+          acc[u][k] = a0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          float t = acc[u][k];
+          t += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, t), 0xB1, 0xF, 0xF, false));
+          t += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, t), 0x4E, 0xF, 0xF, false));
+          t += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, t), 0x141, 0xF, 0xF, false));
+          acc[u][k] = t;
+        }
+      if (v == 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long p = pbase + u * 8 + sub;
+          if (p < p1) {
+            const long n = p / HW, hw = p - n * HW;
+#pragma unroll
+            for (int k = 0; k < K; ++k) y[(n * K + k) * HW + hw] = acc[u][k] + (b ? b[k] : 0.f);
+          }
+        }
+      }
+    }
+    return;
+  }
   // pass 1: outputs
   for (long pbase = p0 + (long)wid * ppw; pbase < p1; pbase += (long)nw * ppw) {
     const long p = pbase + sub;
@@ -1293,13 +1343,14 @@ UNETSEG_API int unetseg_pw_small_fwd(int dtype, const void* x, int ldx, long M, 
   US_CHECK_ARG(!stats || k == 1, "pw_small_fwd: stats only for k==1");
   const int G = unetseg_pw_small_tiles(M);
   hipStream_t st = (hipStream_t)stream;
+  static const int pw_sign = getenv("UNETSEG_PW_GENERIC") ? -1 : 1;  // A/B: generic shuffle path
   DISPATCH_T(dtype, {
     if (k == 1)
       hipLaunchKernelGGL((pw_small_fwd_kernel<T, 1>), dim3(G), dim3(256), 0, st, (const T*)x, ldx, M, hw, c, w, b, y,
-                         stats, 2048);
+                         stats, 2048 * pw_sign);
     else
       hipLaunchKernelGGL((pw_small_fwd_kernel<T, 2>), dim3(G), dim3(256), 0, st, (const T*)x, ldx, M, hw, c, w, b, y,
-                         stats, 2048);
+                         stats, 2048 * pw_sign);
   });
   US_LAUNCH_CHECK("pw_small_fwd");
   return 0;
