@@ -208,22 +208,24 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
 #pragma unroll
     for (int p = 0; p < FP; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Fragment reads: row = base + p*16 + (lane & 15) and the swizzle depends on (row >> 1) & 7, i.e.
+  // on the lane alone, so each (operand, K half) has one per-lane byte offset and the p / c steps are
+  // immediates (p * 16 rows * 128 B); per step only the stage base is added.
+  unsigned foffA[2], foffB[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int r = lane & 15, sw = ((kk * 4 + (lane >> 4)) ^ ((r >> 1) & 7)) * 16;
+    foffA[kk] = (unsigned)((wm * WTM + r) * 128 + sw);
+    foffB[kk] = (unsigned)((BM + wn * WTN + r) * 128 + sw);
+  }
   auto frags = [&](int buf, int kk, bf16x8 (&pf)[FP], bf16x8 (&wf)[FC]) {
-    const uint4* As = lds + buf * STAGE;
-    const uint4* Bs = As + BM * 8;
-    const int ch = kk * 4 + (lane >> 4);
+    const char* sb = reinterpret_cast<const char*>(lds + buf * STAGE);
+    const char* pa = sb + foffA[kk];
+    const char* pb = sb + foffB[kk];
 #pragma unroll
-    for (int p = 0; p < FP; ++p) {
-      const int row = wm * WTM + p * 16 + (lane & 15);
-      uint4 v = As[row * 8 + swz8(row, ch)];
-      pf[p] = *reinterpret_cast<bf16x8*>(&v);
-    }
+    for (int p = 0; p < FP; ++p) pf[p] = *reinterpret_cast<const bf16x8*>(pa + p * 2048);
 #pragma unroll
-    for (int c = 0; c < FC; ++c) {
-      const int row = wn * WTN + c * 16 + (lane & 15);
-      uint4 v = Bs[row * 8 + swz8(row, ch)];
-      wf[c] = *reinterpret_cast<bf16x8*>(&v);
-    }
+    for (int c = 0; c < FC; ++c) wf[c] = *reinterpret_cast<const bf16x8*>(pb + c * 2048);
   };
   auto mfmas = [&](const bf16x8 (&pf)[FP], const bf16x8 (&wf)[FC]) {
 #pragma unroll
