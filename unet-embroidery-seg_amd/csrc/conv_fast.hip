@@ -762,30 +762,45 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     __syncthreads();
   }
   const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  // per-lane byte offsets of every transposed fragment read (rows 8g+qq and +4 of the K step,
+  // 16-B chunk of the fragment's columns under the row swizzle): the loop adds only the stage base
+  unsigned toffA[FM][2], toffB[FN][2];
+  {
+    const int ra_ = 8 * g + qq, rb_ = ra_ + 4;
+    auto off = [&](int cpr, int col0, int row) -> unsigned {
+      const int chunk = (col0 >> 3) + (pp >> 1);
+      const int sw = cpr >= 16 ? swz_tr16(row) : swz_tr8(row);
+      return (unsigned)(row * (cpr * 16) + ((chunk ^ sw) * 16) + (pp & 1) * 8);
+    };
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      toffA[i][0] = off(CPA, wm * WTM + i * 16, ra_);
+      toffA[i][1] = off(CPA, wm * WTM + i * 16, rb_);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      toffB[j][0] = BKW * CPA * 16 + off(CPB, wn * WTN + j * 16, ra_);
+      toffB[j][1] = BKW * CPA * 16 + off(CPB, wn * WTN + j * 16, rb_);
+    }
+  }
+  static_assert(BKW == 32, "one 32-pixel K half per step");
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nkt) gload(kt0 + kt + 1);
     const char* base = reinterpret_cast<const char*>(lds + cur * STAGE);
-    auto trfrag = [&](int off_bytes, int cpr, int col0, int r0) -> bf16x8 {
-      const int chunk = (col0 >> 3) + (pp >> 1);
-      const int ra_ = r0 + 8 * g + qq, rb_ = r0 + 8 * g + qq + 4;
-      const int swa = cpr >= 16 ? swz_tr16(ra_) : swz_tr8(ra_);
-      const int swb = cpr >= 16 ? swz_tr16(rb_) : swz_tr8(rb_);
-      const char* pa = base + off_bytes + ra_ * (cpr * 16) + ((chunk ^ swa) * 16) + (pp & 1) * 8;
-      const char* pb = base + off_bytes + rb_ * (cpr * 16) + ((chunk ^ swb) * 16) + (pp & 1) * 8;
-      s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(pa));
-      s16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(pb));
+    auto trpair = [&](unsigned o0, unsigned o1) -> bf16x8 {
+      s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + o0));
+      s16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + o1));
       typedef short s16x8 __attribute__((ext_vector_type(8)));
       s16x8 v = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
       return *reinterpret_cast<bf16x8*>(&v);
     };
-#pragma unroll
-    for (int kk = 0; kk < BKW / 32; ++kk) {
+    {
       bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = trfrag(0, CPA, wm * WTM + i * 16, kk * 32);
+      for (int i = 0; i < FM; ++i) af[i] = trpair(toffA[i][0], toffA[i][1]);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = trfrag(BKW * CPA * 16, CPB, wn * WTN + j * 16, kk * 32);
+      for (int j = 0; j < FN; ++j) bfr[j] = trpair(toffB[j][0], toffB[j][1]);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
