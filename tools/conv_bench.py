@@ -2,7 +2,7 @@
 
     python tools/conv_bench.py                      # the U-Net's heaviest shapes
     python tools/conv_bench.py 16,512,512,64,0,64,3,1,1 ...   # N,H,W,C1,C2,K,k,stride,pad
-Env knobs of the library (UNETSEG_NO_HALO, UNETSEG_TN_V3, ...) are read at first use, so compare
+Env knobs of the library (UNETSEG_NO_HALO, UNETSEG_TN_CFG, ...) are read at first use, so compare
 variants in separate processes.
 """
 import os
