@@ -428,3 +428,37 @@ def test_adam_matches_torch():
         lib.adam(pd.data_ptr(), gd.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8, 1e-4, step, 0,
                  torch.cuda.current_stream().cuda_stream)
     torch.testing.assert_close(pd.cpu(), pt.detach(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("dtname", ["fp32", "bf16"])
+def test_pack_conv_weights_batched(dtname):
+    """unetseg_pack_conv_weights (one launch for every conv) == torch permutes of the fp32 weights:
+    wk [K][R][S][Cpad] (zero channels C..Cpad-1) and wt [C][R][S][K]; ragged K/C tiles, tap chunks
+    of a 7x7, K not a multiple of 8 (scalar store path), bit-exact conversion."""
+    ops, DT_BF16, DT_F32 = _ops()
+    dt = DT_BF16 if dtname == "bf16" else DT_F32
+    tdt = torch.bfloat16 if dtname == "bf16" else torch.float32
+    g = torch.Generator().manual_seed(7)
+    shapes = [(64, 64, 3, 3, None, True), (64, 3, 7, 7, 8, False), (40, 24, 3, 3, None, True),
+              (512, 2048, 1, 1, None, True), (36, 20, 3, 3, None, True), (96, 136, 1, 1, None, True),
+              (128, 192, 3, 3, None, True)]
+    convs, pcs, need_t = [], [], []
+    for K, C, R, S, cpad, nt in shapes:
+        conv = torch.nn.Conv2d(C, K, (R, S), bias=False)
+        conv.weight.data = torch.randn(K, C, R, S, generator=g).to(DEV)
+        convs.append(conv)
+        pcs.append(ops.PackedConv(conv, cpad))
+        need_t.append(nt)
+    ctx = _ctx(dt)
+    table = ops.PackTable()
+    table.run(ctx, pcs, need_t)
+    torch.cuda.synchronize()
+    for (K, C, R, S, cpad, nt), conv, pc in zip(shapes, convs, pcs):
+        w = conv.weight.data.cpu()
+        cp = cpad or C
+        ref_k = torch.zeros(K, R, S, cp)
+        ref_k[..., :C] = w.permute(0, 2, 3, 1)
+        assert torch.equal(pc.wk.cpu(), ref_k.to(tdt)), (K, C, R, S)
+        if nt:
+            assert torch.equal(pc.wt.cpu(), w.permute(1, 2, 3, 0).contiguous().to(tdt)), (K, C, R, S)
+

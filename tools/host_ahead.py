@@ -21,6 +21,8 @@ def main():
     from unetseg_hip.losses import binary_segmentation_loss
     from utils.synthetic import make_batch
 
+    if os.environ.get("HA_STREAM", "0") == "1":  # bench.py's default: a created (non-legacy) stream
+        torch.cuda.set_stream(torch.cuda.Stream())
     m = create_model("unet_resnet50", weights="", num_classes=2).cuda().train()
     m.compute_dtype = "bf16"
     opt = FusedAdam(m, lr=1e-4, weight_decay=1e-4)
