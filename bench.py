@@ -197,6 +197,12 @@ def main():
         step(0)
         torch.cuda.synchronize()
         kinds = {}
+        dump = os.environ.get("UNETSEG_PROBE_DUMP")  # per-call table (kind, desc, us, TFLOP/s)
+        if dump:
+            with open(dump, "w") as f:
+                for kind, flops, nl, e0, e1, desc in ops.PROBE:
+                    us = e0.elapsed_time(e1) * 1e3
+                    f.write(f"{kind:9s} {us:9.1f} us {flops / max(us, 1e-3) / 1e6:8.1f} TF/s  {desc}\n")
         for kind, flops, nl, e0, e1, _ in ops.PROBE:
             d = kinds.setdefault(kind, [0.0, 0.0, 0])
             d[0] += flops

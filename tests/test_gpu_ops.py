@@ -71,6 +71,8 @@ CONV_CASES = [
     (2, 64, 64, 256, 0, 512, 1, 2, 0, False, False),
     (1, 96, 32, 64, 128, 64, 3, 1, 1, True, True),
     (3, 33, 64, 192, 0, 32, 1, 1, 0, False, False),
+    # narrow 1x1 output (K % 64 != 0): gradients through dY zero-padded to 64 channels
+    (2, 21, 23, 128, 0, 40, 1, 1, 0, False, False),
     # 3x3 halo kernel (64 input channels, H % 8 == 0, W % 32 == 0): fwd 64->192, dgrad 192<-64
     (2, 16, 64, 64, 0, 192, 3, 1, 1, True, True),
     (1, 24, 32, 192, 0, 64, 3, 1, 1, False, False),
@@ -461,4 +463,5 @@ def test_pack_conv_weights_batched(dtname):
         assert torch.equal(pc.wk.cpu(), ref_k.to(tdt)), (K, C, R, S)
         if nt:
             assert torch.equal(pc.wt.cpu(), w.permute(1, 2, 3, 0).contiguous().to(tdt)), (K, C, R, S)
+
 

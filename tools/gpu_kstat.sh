@@ -1,7 +1,7 @@
 # kernel durations of one bench run (kernel-trace only): KPAT = regex of kernels to print
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ks -o run -- python bench.py --steps 3 --warmup 1 --cpu-baseline 0 --probe 0 > gpurun_out/ks.log 2>&1 || { echo PROF FAILED; tail -20 gpurun_out/ks.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ks -o run -- python bench.py --steps 3 --warmup 1 --cpu-baseline 0 --probe 0 $BENCH_ARGS > gpurun_out/ks.log 2>&1 || { echo PROF FAILED; tail -20 gpurun_out/ks.log; exit 1; }
 python - <<'PY'
 import csv, glob, os, re, collections
 rows = list(csv.DictReader(open(glob.glob("gpurun_out/ks/**/run_kernel_trace.csv", recursive=True)[0])))

@@ -253,6 +253,10 @@ def pack_input(ctx, x, cpad=8):
     return Node(y, need_grad=False)
 
 
+#: narrow 1x1 conv gradients through a 64-channel zero-padded dY (UNETSEG_NO_PADK=1: generic kernels)
+PAD_K = os.environ.get("UNETSEG_NO_PADK", "0") != "1"
+
+
 def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
     """y = conv(cat[x1, x2]) (+bias if the conv has one, ReLU).  Stride/padding come from the
     Conv2d container.  Returns (Node y, BN partials or None)."""
@@ -302,10 +306,19 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
         else:
             assert b is None, "conv with bias and no ReLU is not on the hot path"
             dY = dA
+        # 1x1 convs with a narrow output (the attention gates' theta/phi, K = inter = 32): both
+        # gradient GEMMs reduce over or produce K, below the fast tiles' 64-channel granule, so dY
+        # is zero-padded to Kp channels once and the padded rows of dW / columns of W^T are zero
+        Kp = K
+        if PAD_K and ctx.dt == DT_BF16 and R == 1 and S == 1 and K % 64 != 0 and K % 8 == 0 and x2 is None and stride == 1:
+            Kp = -(-K // 64) * 64
+            dYp = torch.zeros(N, Pq, Qq, Kp, dtype=ctx.tdtype, device=dev)
+            lib.add(ctx.dt, P(dY), ldp(dY), P(dYp), Kp, M, K, ctx.stream)
+            dY = dYp
         # weight gradient: on the side stream when overlapping (it only needs dY and the inputs,
         # and nothing in the data-gradient chain reads its output)
         cin = C1 + C2
-        ws_bytes = lib.conv2d_wgrad_workspace(ctx.dt, N, Pq, Qq, K, cin, R, S)
+        ws_bytes = lib.conv2d_wgrad_workspace(ctx.dt, N, Pq, Qq, Kp, cin, R, S)
         side = ctx.side
         if side is not None:
             lib.stream_wait(side.cuda_stream, ctx.stream)
@@ -318,12 +331,29 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
         else:
             ws = workspace(ws_bytes, dev)
             wst = ctx.stream
-        with _probe("wgrad", flops, 1, ("wgrad",) + desc, stream=side):
-            lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(dY), ldp(dY), K, R, S,
-                             stride, pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, wst)
+        if Kp != K:
+            dwp = torch.empty(Kp, pc.C, dtype=torch.float32, device=dev)
+            if side is not None:
+                dwp.record_stream(side)
+            with _probe("wgrad", flops, 1, ("wgrad",) + desc, stream=side):
+                lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), 0, 0, 0, N, H, W, P(dY), Kp, Kp, 1, 1, 1, 0, P(ws),
+                                 ws.numel(), P(dwp), pc.C, 0, wst)
+                lib.add(DT_F32, P(dwp), pc.C, P(pc.conv.weight.grad), pc.C, K, pc.C, wst)
+        else:
+            with _probe("wgrad", flops, 1, ("wgrad",) + desc, stream=side):
+                lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(dY), ldp(dY), K, R, S,
+                                 stride, pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, wst)
         ctx.param_done(pc.conv.weight, b)
         # data gradient
-        if x2 is None:
+        if Kp != K:
+            if x1.need_grad:
+                wtp = torch.zeros(C1, Kp, dtype=ctx.tdtype, device=dev)
+                lib.add(ctx.dt, P(pc.wt), K, P(wtp), Kp, C1, K, ctx.stream)
+                g, acc = gbuf(ctx, x1)
+                with _probe("igemm_tn", flops, 1, ("dgrad",) + desc):
+                    lib.conv2d_dgrad(ctx.dt, P(dY), Kp, N, Pq, Qq, P(wtp), Kp, C1, 1, 1, 1, 0, P(g), ldp(g), H, W, acc,
+                                     ctx.stream)
+        elif x2 is None:
             if x1.need_grad and not _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
                 g, acc = gbuf(ctx, x1)
                 with _probe("igemm_tn", flops, stride * stride, ("dgrad",) + desc):
