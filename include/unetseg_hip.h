@@ -171,6 +171,8 @@ int unetseg_pw_small_bwd_relu(int dtype, const float* dy, const void* x, int ldx
 /* alpha = sigmoid(BN1(psi)); gated = skip * alpha */
 int unetseg_attn_apply(int dtype, const void* skip, int lds_, const float* psi, const float* sc, const float* sh,
                        float* alpha, void* gated, int ldg, long M, int c, void* stream);
+/* part: [2][G1] (sum dpsibn, sum dpsibn * xhat) per 128-pixel tile, G1 = unetseg_attn_bwd1_tiles(M) */
+int unetseg_attn_bwd1_tiles(long M);
 int unetseg_attn_bwd1(int dtype, const void* dg, int ldg, const void* skip, int lds_, const float* alpha,
                       const float* psi, const float* mean, const float* inv, void* dskip, int ldds, int ds_acc,
                       float* dpsibn, long M, int c, float* part, void* stream);

@@ -936,6 +936,47 @@ __global__ void attn_bwd1_kernel(const T* dg, int ldg, const T* skip, int lds_, 
   const long p0 = (long)blockIdx.x * pix_per_block;
   const long p1 = min(M, p0 + pix_per_block);
   double s0 = 0.0, s1 = 0.0;
+  if (nchunk == 1) {
+    // one vector per lane per pixel: four pixel groups per wave in flight (loads of all four
+    // issued before the first use), the serial form kept one group's latency exposed per step
+    constexpr int U = 4;
+    const int c0 = v * V;
+    const long step = (long)nw * ppw;
+    for (long pb = p0 + (long)wid * ppw; pb < p1; pb += U * step) {
+      float g[U][V], sk[U][V], old[U][V], al[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long p = pb + u * step + sub;
+        al[u] = 0.f;
+#pragma unroll
+        for (int e = 0; e < V; ++e) g[u][e] = sk[u][e] = old[u][e] = 0.f;
+        if (p < p1) {
+          al[u] = alpha[p];
+          load_vec(dg + p * ldg + c0, g[u]);
+          load_vec(skip + p * lds_ + c0, sk[u]);
+          if (ds_acc) load_vec(dskip + p * ldds + c0, old[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long p = pb + u * step + sub;
+        float dot = 0.f, o[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          dot += g[u][e] * sk[u][e];
+          o[e] = g[u][e] * al[u] + old[u][e];
+        }
+        if (p < p1) store_vec(dskip + p * ldds + c0, o);
+        for (int sh = 1; sh < cv; sh <<= 1) dot += __shfl_xor(dot, sh, 64);
+        if (p < p1 && v == 0) {
+          const float d = dot * al[u] * (1.f - al[u]);
+          dpsibn[p] = d;
+          s0 += d;
+          s1 += (double)d * (psi[p] - mean[0]) * inv[0];
+        }
+      }
+    }
+  } else
   for (long pbase = p0 + (long)wid * ppw; pbase < p1; pbase += (long)nw * ppw) {
     const long p = pbase + sub;
     float dot = 0.f;
@@ -1410,16 +1451,20 @@ UNETSEG_API int unetseg_attn_apply(int dtype, const void* skip, int lds_, const 
   return 0;
 }
 
+// 128-pixel tiles: the 64^2 x 512-channel gate has 32 K pixels, 2048-pixel tiles left 16 blocks
+constexpr int kAttnBwd1Tile = 128;
+UNETSEG_API int unetseg_attn_bwd1_tiles(long M) { return ceil_div(M, (long)kAttnBwd1Tile); }
+
 UNETSEG_API int unetseg_attn_bwd1(int dtype, const void* dg, int ldg, const void* skip, int lds_, const float* alpha,
                                   const float* psi, const float* mean, const float* inv, void* dskip, int ldds,
                                   int ds_acc, float* dpsibn, long M, int c, float* part, void* stream) {
   CHECK_VEC(dtype, c, "attn_bwd1");
   const int V = dtype == DT_BF16 ? 8 : 4;
   US_CHECK_ARG(((c / V) & (c / V - 1)) == 0, "attn_bwd1: C/V must be a power of two");
-  const int G = unetseg_pw_small_tiles(M);
+  const int G = unetseg_attn_bwd1_tiles(M);
   DISPATCH_T(dtype, hipLaunchKernelGGL(attn_bwd1_kernel<T>, dim3(G), dim3(256), 0, (hipStream_t)stream, (const T*)dg,
                                        ldg, (const T*)skip, lds_, alpha, psi, mean, inv, (T*)dskip, ldds, ds_acc, dpsibn,
-                                       M, c, 2048, part, G));
+                                       M, c, kAttnBwd1Tile, part, G));
   US_LAUNCH_CHECK("attn_bwd1");
   return 0;
 }

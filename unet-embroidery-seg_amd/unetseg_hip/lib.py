@@ -52,6 +52,7 @@ SIGNATURES = {
     "unetseg_pw_small_bwd": (I, [I, P, P, I, L, I, I, I, P, P, I, I, P, P, P]),
     "unetseg_pw_small_bwd_relu": (I, [I, P, P, I, L, I, I, I, P, P, I, P, P, P, P]),
     "unetseg_attn_apply": (I, [I, P, I, P, P, P, P, P, I, L, I, P]),
+    "unetseg_attn_bwd1_tiles": (I, [L]),
     "unetseg_attn_bwd1": (I, [I, P, I, P, I, P, P, P, P, P, I, I, P, L, I, P, P]),
     "unetseg_attn_bwd2": (I, [I, P, P, P, P, P, P, I, P, P, I, L, I, P, P, P]),
     "unetseg_add": (I, [I, P, I, P, I, L, I, P]),
@@ -122,7 +123,7 @@ class _Caller:
         fn = getattr(load(), "unetseg_" + item)
         if SIGNATURES["unetseg_" + item][0] is I and item not in ("reduce_tiles", "pw_small_tiles", "conv_tile_m",
                                                                     "abi_version", "conv2d_fwd_tile_m",
-                                                                    "conv2d_dgrad_post", "stem_fwd_tile_m"):
+                                                                    "conv2d_dgrad_post", "stem_fwd_tile_m", "attn_bwd1_tiles"):
             def call(*args):
                 rc = fn(*args)
                 if rc != 0:

@@ -674,12 +674,13 @@ def attention_gate(ctx, skip, gate, gm, pth, pph):
         if dg is None:
             return
         dpsibn = ctx.f32(M)
-        part = ctx.f32(3, 1, G)
+        G1 = lib.attn_bwd1_tiles(M)
+        part = ctx.f32(3, 1, G1)
         ds, dsacc = gbuf(ctx, skip)
         lib.attn_bwd1(ctx.dt, P(dg), ldp(dg), P(S_), ldp(S_), P(alpha), P(psi), P(s.mean), P(s.inv), P(ds), ldp(ds),
                       dsacc, P(dpsibn), M, Cs, P(part), ctx.stream)
         coef = ctx.f32(6, 1)
-        lib.bn_bwd_finalize(P(part), 1, G, M, 1, P(psi_bn.weight), P(s.inv), P(psi_bn.weight.grad),
+        lib.bn_bwd_finalize(P(part), 1, G1, M, 1, P(psi_bn.weight), P(s.inv), P(psi_bn.weight.grad),
                             P(psi_bn.bias.grad), 0, 0, 0, 0, P(coef), ctx.stream)
         ctx.param_done(psi_bn.weight, psi_bn.bias)
         dzf, acc = gbuf(ctx, f)
