@@ -9,4 +9,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 D=$(dirname $(find gpurun_out/c4prof -name run_kernel_trace.csv | head -1))
 python tools/prof_summary.py $D 8 40 > gpurun_out/c4_kernel_stats_summary.txt && python tools/trace_streams.py $D 4 > gpurun_out/c4_streams.txt
 head -5 gpurun_out/c4_kernel_stats_summary.txt
+UNETSEG_PROBE_DUMP=gpurun_out/c4_probe.txt timeout -k 10 300 python bench.py --model attention_unet --batch 8 --steps 2 --warmup 1 --cpu-baseline 0 > /dev/null 2>&1 || exit 1
 rm -f $D/run_kernel_trace.csv
