@@ -154,6 +154,7 @@ int unetseg_add(int dtype, const void* x, int ldx, void* out, int ldo, long M, i
 
 /* ---- narrow 1x1 heads (final / outc / seg_head / psi: model/unet_resnet.py:78,
  *      model/unet_plain.py:69, model/unet_multitask.py:69, model/unet_attention.py:24) ------------ */
+int unetseg_pw_small_tile(long M); /* pixels per tile (2048, smaller when M gives < 512 tiles) */
 int unetseg_pw_small_tiles(long M);
 /* y fp32 planar [n][k][hw] (k <= 2); stats (k == 1, may be NULL) [unetseg_pw_small_tiles(M)][2] */
 int unetseg_pw_small_fwd(int dtype, const void* x, int ldx, long M, int hw, int c, int k, const float* w,

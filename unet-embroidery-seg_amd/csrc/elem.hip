@@ -1372,9 +1372,17 @@ UNETSEG_API int unetseg_pack_input_stem(const float* x, int n, int c, int h, int
   return 0;
 }
 
-UNETSEG_API int unetseg_pw_small_tiles(long M) { return ceil_div(M, 2048); }
+// pixel tile of the small-Cout 1x1 / attention-psi kernels: 2048, halved (down to 128) while that
+// leaves fewer than 512 blocks (the 64^2 gate's 32 K pixels had 16 blocks at 2048)
+static long pw_tile(long M) {
+  long t = 2048;
+  while (t > 128 && (M + t - 1) / t < 512) t >>= 1;
+  return t;
+}
+UNETSEG_API int unetseg_pw_small_tile(long M) { return (int)pw_tile(M); }
+UNETSEG_API int unetseg_pw_small_tiles(long M) { return ceil_div(M, pw_tile(M)); }
 
-// y fp32 planar [n][k][hw]; stats (k==1 only, may be NULL): [G][2], G = unetseg_pw_small_tiles(M), tile 2048 px
+// y fp32 planar [n][k][hw]; stats (k==1 only, may be NULL): [G][2], G = unetseg_pw_small_tiles(M), tile unetseg_pw_small_tile(M) px
 UNETSEG_API int unetseg_pw_small_fwd(int dtype, const void* x, int ldx, long M, int hw, int c, int k, const float* w,
                                      const float* b, float* y, float* stats, void* stream) {
   CHECK_VEC(dtype, c, "pw_small_fwd");
@@ -1388,10 +1396,10 @@ UNETSEG_API int unetseg_pw_small_fwd(int dtype, const void* x, int ldx, long M, 
   DISPATCH_T(dtype, {
     if (k == 1)
       hipLaunchKernelGGL((pw_small_fwd_kernel<T, 1>), dim3(G), dim3(256), 0, st, (const T*)x, ldx, M, hw, c, w, b, y,
-                         stats, 2048 * pw_sign);
+                         stats, (int)pw_tile(M) * pw_sign);
     else
       hipLaunchKernelGGL((pw_small_fwd_kernel<T, 2>), dim3(G), dim3(256), 0, st, (const T*)x, ldx, M, hw, c, w, b, y,
-                         stats, 2048 * pw_sign);
+                         stats, (int)pw_tile(M) * pw_sign);
   });
   US_LAUNCH_CHECK("pw_small_fwd");
   return 0;
@@ -1409,10 +1417,10 @@ UNETSEG_API int unetseg_pw_small_bwd(int dtype, const float* dy, const void* x, 
   DISPATCH_T(dtype, {
     if (k == 1)
       hipLaunchKernelGGL((pw_small_bwd_kernel<T, 1>), dim3(G), dim3(256), 0, st, dy, (const T*)x, ldx, M, hw, c, w,
-                         (T*)dx, lddx, dx_acc, part_w, part_b, G, 2048);
+                         (T*)dx, lddx, dx_acc, part_w, part_b, G, (int)pw_tile(M));
     else
       hipLaunchKernelGGL((pw_small_bwd_kernel<T, 2>), dim3(G), dim3(256), 0, st, dy, (const T*)x, ldx, M, hw, c, w,
-                         (T*)dx, lddx, dx_acc, part_w, part_b, G, 2048);
+                         (T*)dx, lddx, dx_acc, part_w, part_b, G, (int)pw_tile(M));
   });
   US_LAUNCH_CHECK("pw_small_bwd");
   return 0;
@@ -1433,10 +1441,10 @@ UNETSEG_API int unetseg_pw_small_bwd_relu(int dtype, const float* dy, const void
   hipStream_t st = (hipStream_t)stream;
   if (k == 1)
     hipLaunchKernelGGL((pw_small_bwd_kernel<bf16, 1, true>), dim3(G), dim3(256), 0, st, dy, (const bf16*)x, ldx, M, hw,
-                       c, w, (bf16*)dx, lddx, 0, part_w, part_b, G, 2048, part_d);
+                       c, w, (bf16*)dx, lddx, 0, part_w, part_b, G, (int)pw_tile(M), part_d);
   else
     hipLaunchKernelGGL((pw_small_bwd_kernel<bf16, 2, true>), dim3(G), dim3(256), 0, st, dy, (const bf16*)x, ldx, M, hw,
-                       c, w, (bf16*)dx, lddx, 0, part_w, part_b, G, 2048, part_d);
+                       c, w, (bf16*)dx, lddx, 0, part_w, part_b, G, (int)pw_tile(M), part_d);
   US_LAUNCH_CHECK("pw_small_bwd_relu");
   return 0;
 }
@@ -1478,7 +1486,7 @@ UNETSEG_API int unetseg_attn_bwd2(int dtype, const float* dpsibn, const float* p
   US_CHECK_ARG(cv <= 256 && 256 % cv == 0, "attn_bwd2: bad C");
   const int G = unetseg_pw_small_tiles(M);
   DISPATCH_T(dtype, hipLaunchKernelGGL(attn_bwd2_kernel<T>, dim3(G), dim3(256), 0, (hipStream_t)stream, dpsibn, psi,
-                                       mean, inv, coef, (const T*)f, ldf, wpsi, (T*)dzf, lddz, M, c, cv, 2048, part_w,
+                                       mean, inv, coef, (const T*)f, ldf, wpsi, (T*)dzf, lddz, M, c, cv, (int)pw_tile(M), part_w,
                                        part_b, G));
   US_LAUNCH_CHECK("attn_bwd2");
   return 0;

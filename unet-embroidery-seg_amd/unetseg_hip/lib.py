@@ -48,6 +48,7 @@ SIGNATURES = {
     "unetseg_upsample2x_bwd": (I, [I, P, I, I, I, I, I, I, P, I, I, P]),
     "unetseg_pack_input": (I, [I, P, I, I, I, I, I, P, P]),
     "unetseg_pw_small_tiles": (I, [L]),
+    "unetseg_pw_small_tile": (I, [L]),
     "unetseg_pw_small_fwd": (I, [I, P, I, L, I, I, I, P, P, P, P, P]),
     "unetseg_pw_small_bwd": (I, [I, P, P, I, L, I, I, I, P, P, I, I, P, P, P]),
     "unetseg_pw_small_bwd_relu": (I, [I, P, P, I, L, I, I, I, P, P, I, P, P, P, P]),
@@ -123,7 +124,7 @@ class _Caller:
         fn = getattr(load(), "unetseg_" + item)
         if SIGNATURES["unetseg_" + item][0] is I and item not in ("reduce_tiles", "pw_small_tiles", "conv_tile_m",
                                                                     "abi_version", "conv2d_fwd_tile_m",
-                                                                    "conv2d_dgrad_post", "stem_fwd_tile_m", "attn_bwd1_tiles"):
+                                                                    "conv2d_dgrad_post", "stem_fwd_tile_m", "attn_bwd1_tiles", "pw_small_tile"):
             def call(*args):
                 rc = fn(*args)
                 if rc != 0:

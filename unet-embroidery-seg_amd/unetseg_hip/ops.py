@@ -18,7 +18,6 @@ import torch
 from .lib import DT_BF16, DT_F32, lib
 
 BN_TILE = 128  # == unetseg_conv_tile_m(): M tile of the conv kernel, hence of its BN partials
-PW_TILE = 2048  # pixel tile of the small-Cout 1x1 kernels
 
 
 def P(t):
@@ -661,7 +660,7 @@ def attention_gate(ctx, skip, gate, gm, pth, pph):
     pst = ctx.f32(G, 2, 1)
     lib.pw_small_fwd(ctx.dt, P(F_), ldp(F_), M, M, Ci, 1, P(psi_conv.weight), P(psi_conv.bias), P(psi),
                      P(pst) if ctx.training else 0, ctx.stream)
-    s = _bn_coeffs(ctx, psi_bn, pst, M, PW_TILE)
+    s = _bn_coeffs(ctx, psi_bn, pst, M, lib.pw_small_tile(M))
     S_ = skip.data
     Cs = S_.shape[-1]
     alpha = ctx.f32(M)
