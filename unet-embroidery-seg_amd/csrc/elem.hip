@@ -1375,7 +1375,9 @@ UNETSEG_API int unetseg_pack_input_stem(const float* x, int n, int c, int h, int
 // pixel tile of the small-Cout 1x1 / attention-psi kernels: 2048, halved (down to 128) while that
 // leaves fewer than 512 blocks (the 64^2 gate's 32 K pixels had 16 blocks at 2048)
 static long pw_tile(long M) {
+  static const bool fixed = getenv("UNETSEG_PW_TILE_FIXED") != nullptr;  // A/B: always 2048
   long t = 2048;
+  if (fixed) return t;
   while (t > 128 && (M + t - 1) / t < 512) t >>= 1;
   return t;
 }
