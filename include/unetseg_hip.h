@@ -64,6 +64,24 @@ int unetseg_conv2d_fwd_tile_m(int dtype, int c1, int ldc1, int c2, int ldc2, int
 int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h,
                        int w, const void* wk, int cout, int r, int s, int stride, int pad, const float* bias, int relu,
                        void* y, int ldy, float* stats, void* stream);
+/* Kernel-configuration queries (host only, nothing is launched; replace no reference operator:
+ * they let the parity tests assert that they exercise every kernel configuration the benchmark
+ * selects).  Codes: 0 = halo3 (64-channel 3x3 kernel), 1..14 = TN tile configuration
+ * (conv_fast.hip tn_config: 1 256x64, 2 256x128, 3 128x128, 4 128x128 one K step, 5 64x128,
+ * 6 128x64, 7 256x128 LDS-DMA ring, 8 128x128 ring, 9 64x128 ring, 10 128x128 5-stage ring,
+ * 11-14 other rings), 100 = generic igemm kernel (fp32 / unaligned channels).  *taps_out = the
+ * compile-time tap count of an LDS-DMA ring (9 or 1; 0 = generic ring or not a ring). */
+int unetseg_conv2d_fwd_config(int dtype, int c1, int ldc1, int c2, int ldc2, int n, int h, int w, int cout, int r,
+                              int s, int stride, int pad, int* taps_out);
+/* per output-parity class of the data gradient: cfg_out/taps_out[ph*stride+pw] (-1: not launched);
+ * returns the number of classes launched */
+int unetseg_conv2d_dgrad_config(int dtype, int ldy, int n, int p, int q, int cout, int cin, int r, int s, int stride,
+                                int pad, int ldx, int h, int w, int* cfg_out, int* taps_out);
+/* weight-gradient kernel: 0 = halo3_wgrad, 1 = wgrad_fast 64x256 row-run, 2 = wgrad_fast 128x128
+ * row-run, 3 / 4 = the same tiles with general pixel walks, 5 = generic; *splits_out = split-K
+ * slabs (reduced by wgrad_reduce<16> from 16 slabs, <4> from 4, else <1>) */
+int unetseg_conv2d_wgrad_config(int dtype, int c1, int ldc1, int c2, int ldc2, int n, int h, int w, int ldy, int cout,
+                                int r, int s, int stride, int pad, int* splits_out);
 /* dx[n,h,w,cin] (+)= conv_transpose(dy[n,p,q,cout], wt) */
 int unetseg_conv2d_dgrad(int dtype, const void* dy, int ldy, int n, int p, int q, const void* wt, int cout, int cin,
                          int r, int s, int stride, int pad, void* dx, int ldx, int h, int w, int accumulate,
@@ -90,6 +108,8 @@ int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1, const void
 int unetseg_pack_input_stem(const float* x, int n, int c, int h, int w, void* xp, void* stream);
 int unetseg_stem_pack_weight(const float* w, int K, int C, void* wk, void* stream);
 int unetseg_stem_fwd_tile_m(int n, int h, int w, int K);
+/* TN configuration of unetseg_stem_fwd (-1: unsupported) and split-K slabs of unetseg_stem_wgrad */
+int unetseg_stem_config(int n, int h, int w, int K, int* splits_out);
 int unetseg_stem_fwd(const void* xp, int n, int h, int w, const void* wk, int K, void* y, int ldy, float* stats,
                      void* stream);
 size_t unetseg_stem_wgrad_workspace(int n, int h, int w, int K);

@@ -1,0 +1,386 @@
+"""GPU: every conv kernel configuration the benchmark step selects, at shapes that select it.
+
+The library picks a kernel configuration per call from the shape (conv_fast.hip tn_config: halo /
+register-staged TN tiles / LDS-DMA rings with compile-time taps; wgrad: halo / fast tiles with
+split-K slabs and a 16- / 4- / 1-lane reduce).  Each case below names the configuration it must
+select -- asserted through the host-only ``unetseg_conv2d_*_config`` queries of the C ABI -- and
+checks the launch against a float64 reference computed on the same bf16-rounded operands
+(im2col + GEMM in torch float64 on the GPU: exact products, so the only error left is the
+kernel's own fp32 accumulation and its single bf16 rounding).
+
+Tolerances (stated here):
+  * bf16 outputs (conv output y, data gradient dx, masked gradient d):
+    |out - ref| <= 2^-8 |ref| + 1e-4 max|ref|   (one round-to-nearest bf16 rounding = half an ulp
+    <= 2^-8 relative, plus fp32 accumulation noise near zero);
+  * fp32 weight gradient: |dw - ref| <= 1e-3 |ref| + 2e-5 max|ref|;
+  * BN partial statistics / fused backward partials: 1e-4 relative after merging the row tiles.
+``test_bench_configs_covered`` runs one real benchmark step (unet_resnet50 512x512 B=16) with the
+probe on and asserts every configuration it launched appears in CASES.
+Shapes follow the reference layers (model/resnet_backbone.py:35-115, model/unet_resnet.py:7-42,70-78).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+RNG = 1234
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from unetseg_hip import load
+    load()
+
+
+# id: (direction, (N, H, W, C1, C2, K, R, stride), expected configuration key(s))
+#   direction: fwd_relu (bias + ReLU epilogue, decoder) | fwd_stats (BN partials, encoder) |
+#              fwd_all (bias + ReLU + stats: every runtime epilogue flag of a TN tile) |
+#              dgrad (plain, then accumulated onto a random gradient) | post1 | post2 | wgrad
+CASES = {
+    # ---- forward ----
+    "fwd_halo3_relu": ("fwd_relu", (2, 64, 256, 64, 0, 64, 3, 1), ["fwd:halo3"]),           # up_conv @512^2 (rows)
+    "fwd_halo3_stats": ("fwd_stats", (2, 128, 128, 64, 0, 64, 3, 1), ["fwd:halo3"]),        # layer1 conv2
+    "fwd_ring256x128_t9": ("fwd_all", (16, 32, 32, 1024, 2048, 512, 3, 1), ["fwd:ring256x128_t9"]),  # up_concat4.conv1
+    "fwd_ring256x128_t9_s2": ("fwd_stats", (16, 128, 128, 128, 0, 128, 3, 2), ["fwd:ring256x128_t9"]),  # layer2 conv2
+    "fwd_ring256x128_t1": ("fwd_stats", (16, 64, 64, 512, 0, 128, 1, 1), ["fwd:ring256x128_t1"]),
+    "fwd_ring128x128_5st_t9": ("fwd_stats", (8, 128, 128, 128, 0, 128, 3, 2), ["fwd:ring128x128_5st_t9"]),
+    "fwd_ring128x128_5st_t1": ("fwd_stats", (16, 32, 32, 1024, 0, 256, 1, 1), ["fwd:ring128x128_5st_t1"]),
+    "fwd_ring128x64_t9": ("fwd_relu", (1, 256, 256, 64, 128, 64, 3, 1), ["fwd:ring128x64_t9"]),  # up_concat1.conv1
+    "fwd_ring64x128_t9": ("fwd_stats", (1, 64, 64, 256, 0, 256, 3, 2), ["fwd:ring64x128_t9"]),
+    "fwd_ring64x128_t1": ("fwd_stats", (1, 16, 16, 2048, 0, 512, 1, 1), ["fwd:ring64x128_t1"]),
+    "fwd_tn128x128": ("fwd_all", (1, 64, 64, 128, 0, 512, 1, 1), ["fwd:tn128x128"]),
+    "fwd_tn128x128_1step": ("fwd_stats", (1, 128, 128, 64, 0, 256, 1, 1), ["fwd:tn128x128_1step"]),
+    "fwd_tn128x64": ("fwd_stats", (1, 128, 128, 64, 0, 64, 1, 1), ["fwd:tn128x64"]),
+    "fwd_tn64x128": ("fwd_all", (1, 64, 64, 512, 0, 128, 1, 1), ["fwd:tn64x128"]),
+    # generic kernel: the first conv of unet_plain / attention_unet (3 input channels padded to 8)
+    "fwd_generic_cin8": ("fwd_stats", (2, 64, 64, 8, 0, 64, 3, 1), ["fwd:generic"]),
+    # ---- data gradient (plain / accumulated) ----
+    "dgrad_halo3": ("dgrad", (1, 128, 128, 64, 0, 64, 3, 1), ["dgrad:halo3"]),
+    "dgrad_ring256x128_t9": ("dgrad", (16, 64, 64, 128, 0, 128, 3, 1), ["dgrad:ring256x128_t9"]),
+    "dgrad_ring256x128_t9_cat": ("dgrad", (16, 32, 32, 1024, 2048, 512, 3, 1), ["dgrad:ring256x128_t9"]),
+    "dgrad_ring256x128_t1": ("dgrad", (16, 64, 64, 128, 0, 512, 1, 1), ["dgrad:ring256x128_t1"]),
+    "dgrad_ring128x128_5st_t9": ("dgrad", (8, 64, 64, 128, 0, 128, 3, 1), ["dgrad:ring128x128_5st_t9"]),
+    "dgrad_ring128x128_5st_t1": ("dgrad", (16, 32, 32, 256, 0, 1024, 1, 1), ["dgrad:ring128x128_5st_t1"]),
+    "dgrad_ring128x64_t9": ("dgrad", (1, 256, 256, 64, 0, 128, 3, 1), ["dgrad:ring128x64_t9"]),  # attention down1
+    "dgrad_ring64x128_t9": ("dgrad", (1, 32, 32, 256, 0, 256, 3, 1), ["dgrad:ring64x128_t9"]),
+    "dgrad_ring64x128_t1": ("dgrad", (1, 16, 16, 512, 0, 2048, 1, 1), ["dgrad:ring64x128_t1"]),
+    "dgrad_tn128x128": ("dgrad", (1, 64, 64, 512, 0, 128, 1, 1), ["dgrad:tn128x128"]),
+    "dgrad_tn128x128_s2": ("dgrad", (2, 64, 64, 256, 0, 512, 1, 2),
+                           ["dgrad:tn64x128", "dgrad:tn128x128", "dgrad:tn128x128", "dgrad:tn128x128"]),
+    "dgrad_tn128x128_1step": ("dgrad", (1, 128, 128, 256, 0, 64, 1, 1), ["dgrad:tn128x128_1step"]),
+    "dgrad_tn128x64": ("dgrad", (1, 128, 128, 64, 0, 64, 1, 1), ["dgrad:tn128x64"]),
+    # ---- data gradient with the producer's ReLU (post 1) / BN-ReLU (post 2) backward fused ----
+    "post1_halo3": ("post1", (2, 64, 256, 64, 0, 64, 3, 1), ["dgrad_post1:halo3"]),
+    "post1_ring256x128_t9": ("post1", (16, 32, 32, 512, 0, 512, 3, 1), ["dgrad_post1:ring256x128_t9"]),
+    "post1_ring128x128_5st_t9": ("post1", (8, 64, 64, 128, 0, 128, 3, 1), ["dgrad_post1:ring128x128_5st_t9"]),
+    "post2_halo3": ("post2", (1, 128, 128, 64, 0, 64, 3, 1), ["dgrad_post2:halo3"]),
+    "post2_tn128x128": ("post2", (1, 64, 64, 512, 0, 128, 1, 1), ["dgrad_post2:tn128x128"]),
+    "post2_tn64x128": ("post2", (1, 64, 64, 128, 0, 512, 1, 1), ["dgrad_post2:tn64x128"]),
+    "post2_tn128x64": ("post2", (1, 128, 128, 64, 0, 64, 1, 1), ["dgrad_post2:tn128x64"]),
+    "post2_ring128x128_5st_t9": ("post2", (8, 64, 64, 128, 0, 128, 3, 1), ["dgrad_post2:ring128x128_5st_t9"]),
+    "post2_ring128x128_5st_t1": ("post2", (16, 32, 32, 256, 0, 1024, 1, 1), ["dgrad_post2:ring128x128_5st_t1"]),
+    # stride-2 3x3: the four parity classes have 4 / 2 / 2 / 1 taps -> generic ring, ring_t1, ...
+    "post2_ring256x128_s2": ("post2", (16, 128, 128, 128, 0, 128, 3, 2), None),
+    "post2_ring256x128_t9": ("post2", (16, 64, 64, 128, 0, 128, 3, 1), ["dgrad_post2:ring256x128_t9"]),
+    "post2_ring256x128_t1": ("post2", (16, 64, 64, 128, 0, 512, 1, 1), ["dgrad_post2:ring256x128_t1"]),
+    "post2_ring64x128_s2": ("post2", (1, 32, 32, 512, 0, 512, 3, 2), None),
+    "post2_ring64x128_t9": ("post2", (1, 32, 32, 256, 0, 256, 3, 1), ["dgrad_post2:ring64x128_t9"]),
+    "post2_ring64x128_t1": ("post2", (1, 16, 16, 512, 0, 2048, 1, 1), ["dgrad_post2:ring64x128_t1"]),
+    # ---- weight gradient (+ split-K reduce) ----
+    "wgrad_halo3": ("wgrad", (2, 64, 256, 64, 0, 64, 3, 1), ["wgrad:halo3_wgrad", None]),
+    "wgrad_halo3_cat": ("wgrad", (16, 32, 32, 1024, 2048, 512, 3, 1), ["wgrad:halo3_wgrad", None]),
+    "wgrad128_row_r16": ("wgrad", (16, 128, 128, 64, 0, 256, 1, 1), ["wgrad:wgrad128_row", "reduce16"]),
+    "wgrad128_row_r4": ("wgrad", (1, 64, 64, 128, 0, 512, 1, 1), ["wgrad:wgrad128_row", "reduce4"]),
+    "wgrad128_row_r1": ("wgrad", (1, 32, 32, 256, 0, 1024, 1, 1), ["wgrad:wgrad128_row", "reduce1"]),
+    "wgrad128_s2": ("wgrad", (16, 32, 32, 512, 0, 512, 3, 2), ["wgrad:wgrad128", None]),
+    "wgrad128_r16_16x16": ("wgrad", (16, 16, 16, 2048, 0, 512, 1, 1), ["wgrad:wgrad128", None]),
+    "wgrad64x256_row": ("wgrad", (16, 128, 128, 256, 0, 64, 1, 1), ["wgrad:wgrad64x256_row", "reduce16"]),
+}
+
+
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+def _nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def _nchw(t):
+    return t.permute(0, 3, 1, 2).double()
+
+
+def _out_hw(H, W, R, stride):
+    pad = R // 2
+    return (H + 2 * pad - R) // stride + 1, (W + 2 * pad - R) // stride + 1
+
+
+def _ref_fwd(x, w, stride, pad):
+    """float64 conv via im2col (x [N,C,H,W] f64, w [K,C,R,S] f64)"""
+    N = x.shape[0]
+    K, C, R, S = w.shape
+    cols = F.unfold(x, (R, S), padding=pad, stride=stride)
+    P, Q = (x.shape[2] + 2 * pad - R) // stride + 1, (x.shape[3] + 2 * pad - S) // stride + 1
+    return (w.reshape(K, -1) @ cols).reshape(N, K, P, Q)
+
+
+def _ref_dgrad(dy, w, H, W, stride, pad):
+    N, K, P, Q = dy.shape
+    _, C, R, S = w.shape
+    cols = w.reshape(K, -1).t() @ dy.reshape(N, K, P * Q)
+    return F.fold(cols, (H, W), (R, S), padding=pad, stride=stride)
+
+
+def _ref_wgrad(x, dy, R, stride, pad):
+    N, K, P, Q = dy.shape
+    cols = F.unfold(x, (R, R), padding=pad, stride=stride)  # [N, C*R*R, L]
+    return torch.einsum("nkl,ncl->kc", dy.reshape(N, K, P * Q), cols).reshape(K, x.shape[1], R, R)
+
+
+def _check_bf16(out, ref, what):
+    out, ref = out.double(), ref.double()
+    m = ref.abs().max().item()
+    err = (out - ref).abs()
+    bound = 2.0 ** -8 * ref.abs() + 1e-4 * m
+    bad = (err > bound).sum().item()
+    assert bad == 0, f"{what}: {bad} elements outside 2^-8|ref| + 1e-4 max|ref| (max err {err.max().item():.3e}, max|ref| {m:.3e})"
+
+
+def _key_list(direction, shape):
+    from unetseg_hip import introspect
+    N, H, W, C1, C2, K, R, s = shape
+    d = {"fwd_relu": "fwd", "fwd_stats": "fwd", "fwd_all": "fwd", "dgrad": "dgrad", "post1": "dgrad_post1",
+         "post2": "dgrad_post2", "wgrad": "wgrad"}[direction]
+    return introspect.call_configs((d, N, H, W, C1, C2, K, R, R, s, R // 2, C1, C2))
+
+
+def covered_keys():
+    keys = set()
+    for direction, shape, _ in CASES.values():
+        keys.update(_key_list(direction, shape))
+    return keys
+
+
+class _Op:
+    """operands of one case: bf16-rounded x (cat of x1, x2), w, dy on the device"""
+
+    def __init__(self, shape, seed):
+        N, H, W, C1, C2, K, R, s = shape
+        g = torch.Generator(device=DEV).manual_seed(seed)
+        self.shape = shape
+        cin = C1 + C2
+        self.pad = R // 2
+        self.P, self.Q = _out_hw(H, W, R, s)
+        self.x = _bf(torch.randn(N, cin, H, W, generator=g, device=DEV))
+        self.w32 = _bf(torch.randn(K, cin, R, R, generator=g, device=DEV) / math.sqrt(cin * R * R)).float()
+        self.dy = _bf(torch.randn(N, K, self.P, self.Q, generator=g, device=DEV))
+        self.bias = torch.randn(K, generator=g, device=DEV) * 0.1
+        self.gen = g
+
+    def x_parts(self):
+        N, H, W, C1, C2, K, R, s = self.shape
+        x1 = _nhwc(self.x[:, :C1])
+        x2 = _nhwc(self.x[:, C1:]) if C2 else None
+        return x1, x2
+
+    def packed(self):
+        from unetseg_hip.lib import DT_BF16, lib
+        K, C, R, S = self.w32.shape
+        wk = torch.empty(K, R, S, C, dtype=torch.bfloat16, device=DEV)
+        wt = torch.empty(C, R, S, K, dtype=torch.bfloat16, device=DEV)
+        lib.pack_conv_weight(DT_BF16, self.w32.data_ptr(), K, C, R, S, C, wk.data_ptr(), wt.data_ptr(), _st())
+        return wk, wt
+
+
+def _st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _P(t):
+    return 0 if t is None else t.data_ptr()
+
+
+@pytest.mark.parametrize("cid", list(CASES))
+def test_config_case(cid):
+    from unetseg_hip.lib import DT_BF16, lib
+    direction, shape, expect = CASES[cid]
+    keys = _key_list(direction, shape)
+    if expect is not None:
+        got = [k for k in keys if k is not None]
+        want = [k for k in expect if k is not None]
+        assert got[:len(want)] == want, f"{cid}: selects {keys}, expected {expect}"
+    N, H, W, C1, C2, K, R, s = shape
+    cin = C1 + C2
+    op = _Op(shape, RNG + sum(map(ord, cid)))
+    pad, P, Q = op.pad, op.P, op.Q
+    x64, w64, dy64 = op.x.double(), op.w32.double(), op.dy.double()
+    wk, wt = op.packed()
+    st = _st()
+    if direction.startswith("fwd"):
+        x1, x2 = op.x_parts()
+        relu = direction in ("fwd_relu", "fwd_all")
+        stats = direction in ("fwd_stats", "fwd_all")
+        bias = op.bias if relu else None
+        M = N * P * Q
+        tile = lib.conv2d_fwd_tile_m(DT_BF16, C1, C1, C2, C2, N, H, W, K, R, R, s, pad)
+        G = -(-M // tile)
+        stt = torch.empty(G, 2, K, dtype=torch.float32, device=DEV) if stats else None
+        y = torch.empty(N, P, Q, K, dtype=torch.bfloat16, device=DEV)
+        lib.conv2d_fwd(DT_BF16, _P(x1), C1, C1, _P(x2), C2, C2, N, H, W, _P(wk), K, R, R, s, pad, _P(bias), int(relu),
+                       _P(y), K, _P(stt), st)
+        ref = _ref_fwd(x64, w64, s, pad)
+        if relu:
+            ref = torch.relu(ref + op.bias.double().view(1, -1, 1, 1))
+        out = _nchw(y)
+        _check_bf16(out, ref, f"{cid} y")
+        if stats:
+            # merge the per-row-tile (sum, M2) partials and compare with the stored outputs' stats
+            st_ = stt.double()
+            cnt = torch.tensor([min(tile, M - g_ * tile) for g_ in range(G)], dtype=torch.float64, device=DEV)
+            tot = st_[:, 0].sum(0)
+            mean = tot / M
+            m2 = (st_[:, 1] + cnt[:, None] * (st_[:, 0] / cnt[:, None] - mean) ** 2).sum(0)
+            o = out.permute(1, 0, 2, 3).reshape(K, -1)
+            torch.testing.assert_close(tot, o.sum(1), rtol=1e-4, atol=1e-4 * o.abs().sum(1).max().item() / M * 10)
+            torch.testing.assert_close(m2 / M, o.var(1, unbiased=False), rtol=1e-4, atol=1e-6)
+        return
+    if direction in ("dgrad", "post1", "post2"):
+        dyh = _nhwc(op.dy)
+        ref = _ref_dgrad(dy64, w64, H, W, s, pad)
+        dx = torch.empty(N, H, W, cin, dtype=torch.bfloat16, device=DEV)
+        if direction == "dgrad":
+            lib.conv2d_dgrad(DT_BF16, _P(dyh), K, N, P, Q, _P(wt), K, cin, R, R, s, pad, _P(dx), cin, H, W, 0, st)
+            _check_bf16(_nchw(dx), ref, f"{cid} dx")
+            # accumulate onto an existing gradient: dx' = bf16(float(dx0) + float(bf16 dgrad))
+            g0 = _bf(torch.randn(N, H, W, cin, generator=op.gen, device=DEV))
+            dx.copy_(g0)
+            lib.conv2d_dgrad(DT_BF16, _P(dyh), K, N, P, Q, _P(wt), K, cin, R, R, s, pad, _P(dx), cin, H, W, 1, st)
+            # either rounding order (the TN epilogue rounds the dgrad first, halo adds the fp32
+            # value): within half an ulp of the dgrad plus half an ulp of the sum
+            acc_ref = _nchw(g0) + ref
+            err = (_nchw(dx) - acc_ref).abs()
+            bound = 2.0 ** -8 * (ref.abs() + acc_ref.abs()) + 1e-4 * ref.abs().max().item()
+            assert int((err > bound).sum()) == 0, f"{cid} dx accumulated: max err {err.max().item():.3e}"
+            return
+        post = 1 if direction == "post1" else 2
+        # aux: the producer's output (post 1: ReLU output >= 0 with zeros; post 2: BN input z)
+        z = _bf(torch.randn(N, H, W, cin, generator=op.gen, device=DEV))
+        aux = torch.relu(z) if post == 1 else z
+        sc = (1 + 0.3 * torch.randn(cin, generator=op.gen, device=DEV)).float()
+        sh = (0.3 * torch.randn(cin, generator=op.gen, device=DEV)).float()
+        mu = (0.1 * torch.randn(cin, generator=op.gen, device=DEV)).float()
+        inv = (1 + 0.2 * torch.rand(cin, generator=op.gen, device=DEV)).float()
+        coeffs = [_P(sc), _P(sh), _P(mu), _P(inv)] if post == 2 else [0, 0, 0, 0]
+        args = [DT_BF16, _P(dyh), K, N, P, Q, _P(wt), K, cin, R, R, s, pad]
+        rows = lib.conv2d_dgrad_post(*args, 0, cin, H, W, post, _P(aux), cin, *coeffs, 0, 0, st)
+        assert rows > 0, f"{cid}: shape has no fused path"
+        part = torch.empty(rows, 2, cin, dtype=torch.float32, device=DEV)
+        rc = lib.conv2d_dgrad_post(*args, _P(dx), cin, H, W, post, _P(aux), cin, *coeffs, _P(part), rows, st)
+        assert rc == 0
+        a64 = _nchw(aux)
+        if post == 1:
+            mask = a64 > 0
+        else:  # sign of fmaf(z, sc, sh): exact in float64 (24x24-bit product)
+            mask = (a64 * sc.double().view(1, -1, 1, 1) + sh.double().view(1, -1, 1, 1)) > 0
+        d = _nchw(dx)
+        _check_bf16(d, torch.where(mask, ref, torch.zeros_like(ref)), f"{cid} d")
+        assert (d[~mask] == 0).all()
+        # fused reduction over the stored (rounded, masked) d
+        q0 = d.sum((0, 2, 3))
+        torch.testing.assert_close(part[:, 0].double().sum(0), q0, rtol=1e-4, atol=1e-4 * d.abs().sum((0, 2, 3)).max().item() / d[:, 0].numel())
+        if post == 2:
+            xhat = (a64 - mu.double().view(1, -1, 1, 1)) * inv.double().view(1, -1, 1, 1)
+            q1 = (d * xhat).sum((0, 2, 3))
+            scale = (d * xhat).abs().sum((0, 2, 3)).max().item() / d[:, 0].numel()
+            torch.testing.assert_close(part[:, 1].double().sum(0), q1, rtol=1e-4, atol=1e-4 * scale)
+        return
+    # weight gradient
+    x1, x2 = op.x_parts()
+    dyh = _nhwc(op.dy)
+    ws_bytes = lib.conv2d_wgrad_workspace(DT_BF16, N, P, Q, K, cin, R, R)
+    ws = torch.empty(max(ws_bytes, 1) // 4 + 1, dtype=torch.float32, device=DEV)
+    dw = torch.empty(K, cin, R, R, dtype=torch.float32, device=DEV)
+    lib.conv2d_wgrad(DT_BF16, _P(x1), C1, C1, _P(x2), C2, C2, N, H, W, _P(dyh), K, K, R, R, s, pad, _P(ws), ws_bytes,
+                     _P(dw), cin, 0, st)
+    ref = _ref_wgrad(x64, dy64, R, s, pad)
+    m = ref.abs().max().item()
+    err = (dw.double() - ref).abs()
+    bad = (err > 1e-3 * ref.abs() + 2e-5 * m).sum().item()
+    assert bad == 0, f"{cid}: {bad} dw elements out of tolerance (max err {err.max().item():.3e}, max|ref| {m:.3e})"
+    # accumulate (deterministic split-K order: the second pass adds exactly the same values)
+    dw1 = dw.clone()
+    lib.conv2d_wgrad(DT_BF16, _P(x1), C1, C1, _P(x2), C2, C2, N, H, W, _P(dyh), K, K, R, R, s, pad, _P(ws), ws_bytes,
+                     _P(dw), cin, 1, st)
+    assert torch.equal(dw, dw1 + dw1), f"{cid}: accumulated wgrad is not 2x the first (non-deterministic reduce?)"
+
+
+@pytest.mark.parametrize("N,H", [(16, 512), (2, 200)])
+def test_stem_bench_size(N, H):
+    """ResNet stem at the benchmark size (model/resnet_backbone.py:126-131): 7x7/s2/p3 3->64 on the
+    width-packed fast kernels (stem_fwd: TN 128x64 tile; stem_wgrad: 64x256 split-K + reduce<16>)."""
+    from unetseg_hip import ops
+    from unetseg_hip.lib import DT_BF16, stem_config
+    from unetseg_hip.nn import Conv2d
+    cfg, splits = stem_config(N, H, H, 64)
+    assert cfg == "tn128x64" and splits >= 16, (cfg, splits)
+    g = torch.Generator(device=DEV).manual_seed(N + H)
+    conv = Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(_bf(torch.randn(64, 3, 7, 7, generator=g, device=DEV) / math.sqrt(147)).float())
+    conv.weight.grad = torch.zeros_like(conv.weight)
+    x = torch.rand(N, 3, H, H, generator=g, device=DEV)
+    ctx = ops.Ctx(DT_BF16, True, True, torch.device(DEV))
+    y, (stt, tile) = ops.stem_conv(ctx, x, conv)
+    xr = _bf(x).double()
+    ref = _ref_fwd(xr, conv.weight.detach().double(), 2, 3)
+    _check_bf16(_nchw(y.data), ref, "stem y")
+    dy = _bf(torch.randn(ref.shape, generator=g, device=DEV))
+    y.grad = _nhwc(dy)
+    ctx.backward()
+    torch.cuda.synchronize()
+    dref = _ref_wgrad(xr, dy.double(), 7, 2, 3)
+    err = (conv.weight.grad.double() - dref).abs()
+    m = dref.abs().max().item()
+    assert (err <= 1e-3 * dref.abs() + 2e-5 * m).all(), err.max().item()
+
+
+def test_bench_configs_covered():
+    """One real benchmark step (unet_resnet50, 512x512, B=16, bf16, Lovasz + Adam) with the probe
+    on: every kernel configuration it launches must be exercised by a case above."""
+    import contextlib
+    import io
+
+    from model.model_factory import create_model
+    from unetseg_hip import introspect, ops
+    from unetseg_hip.arena import FusedAdam
+    from unetseg_hip.losses import binary_segmentation_loss
+    from utils.synthetic import make_batch
+    with contextlib.redirect_stdout(io.StringIO()):
+        model = create_model("unet_resnet50", num_classes=2, weights="").to(DEV).train()
+    model.compute_dtype = "bf16"
+    opt = FusedAdam(model, lr=1e-4)
+    x, y = make_batch(16, 512, seed=7)
+    x, y = x.to(DEV), y.to(DEV)
+    ops.PROBE = []
+    try:
+        opt.zero_grad()
+        loss = binary_segmentation_loss(model(x), y, "lovasz_hinge")
+        loss.backward()
+        opt.step()
+        torch.cuda.synchronize()
+        used = set()
+        for rec in ops.PROBE:
+            used.update(introspect.call_configs(rec[5]))
+    finally:
+        ops.PROBE = None
+    assert np.isfinite(loss.item())
+    stem = {"stem_fwd:tn128x64", "stem_wgrad:wgrad64x256_row"}  # test_stem_bench_size
+    missing = sorted(used - covered_keys() - stem)
+    assert not missing, f"bench configurations without a parity case: {missing}"

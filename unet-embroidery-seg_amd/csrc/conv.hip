@@ -650,6 +650,26 @@ UNETSEG_API int unetseg_conv2d_fwd_tile_m(int dtype, int c1, int ldc1, int c2, i
   return fwd_tile_m(dtype, a);
 }
 
+// ---- kernel-configuration queries (host only, no launch): which kernel a call of this shape
+// runs, so parity tests can assert they exercise every configuration the benchmark selects ----
+// A placeholder address stands in for x2: the dispatch only tests it for NULL.
+static const void* const kSomePtr = reinterpret_cast<const void*>(uintptr_t{256});
+
+static int tn_query(int dtype, const IgemmArgs& a, int* taps_out) {
+  if (taps_out) *taps_out = 0;
+  FastTNArgs f;
+  if (dtype != DT_BF16 || !fast_tn_args(a, f)) return kCfgGeneric;
+  return tn_fast_config(f, taps_out);
+}
+
+UNETSEG_API int unetseg_conv2d_fwd_config(int dtype, int c1, int ldc1, int c2, int ldc2, int n, int h, int w,
+                                          int cout, int r, int s, int stride, int pad, int* taps_out) {
+  IgemmArgs a = fwd_args(kSomePtr, c1, ldc1, c2 ? kSomePtr : nullptr, c2, ldc2, n, h, w, kSomePtr, cout, r, s, stride,
+                         pad);
+  a.ldy = cout;
+  return tn_query(dtype, a, taps_out);
+}
+
 // Forward conv.  x = cat([x1 (c1 ch, pixel stride ldc1), x2 (c2 ch, ldc2)], C) NHWC [n,h,w,*];
 // wk: dtype [cout][r][s][c1+c2]; y: NHWC [n,p,q,*] pixel stride ldy.
 // Epilogue: + bias[cout] (fp32, may be NULL), ReLU if relu, and when stats != NULL the per-row-tile
@@ -769,6 +789,28 @@ UNETSEG_API int unetseg_conv2d_dgrad_post(int dtype, const void* dy, int ldy, in
   }
   US_LAUNCH_CHECK("conv2d_dgrad_post");
   return 0;
+}
+
+// Configuration of each output-parity class of unetseg_conv2d_dgrad / _dgrad_post:
+// cfg_out[ph * stride + pw] (kCfg* codes; -1 = class not launched), taps_out likewise (may be NULL).
+// Returns the number of classes launched.
+UNETSEG_API int unetseg_conv2d_dgrad_config(int dtype, int ldy, int n, int p, int q, int cout, int cin, int r, int s,
+                                            int stride, int pad, int ldx, int h, int w, int* cfg_out, int* taps_out) {
+  US_CHECK_ARG(cfg_out && (stride == 1 || stride == 2), "conv2d_dgrad_config: bad args");
+  int launched = 0;
+  for (int ph = 0; ph < stride; ++ph)
+    for (int pw = 0; pw < stride; ++pw) {
+      const int k = ph * stride + pw;
+      cfg_out[k] = -1;
+      if (taps_out) taps_out[k] = 0;
+      IgemmArgs a;
+      if (!dgrad_classes(kSomePtr, ldy, n, p, q, kSomePtr, cout, cin, r, s, stride, pad, const_cast<void*>(kSomePtr), ldx, h, w, ph, pw, a))
+        continue;
+      if (a.M <= 0) continue;
+      cfg_out[k] = tn_query(dtype, a, taps_out ? taps_out + k : nullptr);
+      ++launched;
+    }
+  return launched;
 }
 
 static int wgrad_splits(int Cout, int Ng, long Kpix, int bkw) {
@@ -891,6 +933,31 @@ UNETSEG_API int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1
   return 0;
 }
 
+// Kernel unetseg_conv2d_wgrad runs for this shape: kWg* code; *splits_out = split-K slabs (the
+// reduce is wgrad_reduce_kernel<16> from 16 slabs, <4> from 4, else <1>).
+UNETSEG_API int unetseg_conv2d_wgrad_config(int dtype, int c1, int ldc1, int c2, int ldc2, int n, int h, int w,
+                                            int ldy, int cout, int r, int s, int stride, int pad, int* splits_out) {
+  const int p = (h + 2 * pad - r) / stride + 1, q = (w + 2 * pad - s) / stride + 1;
+  const int cin = c1 + c2, Ng = r * s * cin;
+  const long kpix = (long)n * p * q, src_pix = (long)n * h * w;
+  const long b1 = src_pix * ldc1 * 2, b2 = c2 ? src_pix * ldc2 * 2 : 0, bdy = kpix * ldy * 2;
+  const bool fit = b1 < (1L << 31) && b2 < (1L << 31) && bdy < (1L << 31);
+  int kind = kWgGeneric, splits = 0;
+  HaloWgradArgs hw{};
+  if (stride == 1 && pad == 1 && fit && halo_wgrad_args(dtype, c1, cin, n, h, w, cout, r, s, p, q, hw)) {
+    kind = kWgHalo;
+    splits = halo3_wgrad_splits(hw);
+  } else if (fit && wgrad_fast_eligible(dtype, q, cin, cout) && c1 % 8 == 0) {
+    const bool row32 = !getenv("UNETSEG_WG_NO_ROW32") && q % 32 == 0;
+    kind = cout <= 64 ? (row32 ? kWgFastRow64x256 : kWgFast64x256) : (row32 ? kWgFastRow128 : kWgFast128);
+    splits = wgrad_fast_splits(cout, Ng, kpix);
+  } else {
+    splits = wgrad_splits(cout, Ng, kpix, dtype == DT_BF16 ? 32 : 16);
+  }
+  if (splits_out) *splits_out = splits;
+  return kind;
+}
+
 // All of a model's conv weights in one launch.  desc: DEVICE array of n UnetsegPackDesc with
 // ascending `start` = first tile (desc[0].start == 0; a conv has ceil(K/32)*ceil(Cpad/64) tiles);
 // total = number of tiles.
@@ -993,6 +1060,20 @@ UNETSEG_API int unetseg_stem_fwd_tile_m(int n, int h, int w, int K) {
   FastTNArgs f;
   if (!fast_tn_args(a, f)) return -1;
   return tn_fast_tile_m(f);
+}
+
+// TN configuration of unetseg_stem_fwd (-1: shape unsupported) and the split-K slabs of
+// unetseg_stem_wgrad (*splits_out, may be NULL)
+UNETSEG_API int unetseg_stem_config(int n, int h, int w, int K, int* splits_out) {
+  IgemmArgs a = stem_args(kSomePtr, n, h, w, kSomePtr, K);
+  a.ldy = K;
+  FastTNArgs f;
+  if (splits_out) {
+    FastWgradArgs g = stem_wgrad_args(kSomePtr, n, h, w, kSomePtr, K, K);
+    *splits_out = wgrad_fast_splits(K, g.Ng, g.Kpix);
+  }
+  if (!fast_tn_args(a, f)) return -1;
+  return tn_fast_config(f, nullptr);
 }
 
 UNETSEG_API int unetseg_stem_fwd(const void* xp, int n, int h, int w, const void* wk, int K, void* y, int ldy,

@@ -69,7 +69,12 @@ struct HaloWgradArgs {
   float* ws;
 };
 
+// kernel-configuration codes reported by the unetseg_conv2d_*_config queries (include/unetseg_hip.h)
+enum { kCfgHalo = 0, kCfgGeneric = 100 };  // 1..14: TN tile configurations of tn_config (conv_fast.hip)
+enum { kWgHalo = 0, kWgFastRow64x256 = 1, kWgFastRow128 = 2, kWgFast64x256 = 3, kWgFast128 = 4, kWgGeneric = 5 };
+
 bool tn_fast_ok(const FastTNArgs& a);
+int tn_fast_config(const FastTNArgs& a, int* taps_out);  // kCfgHalo or a TN configuration 1..14
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st);
 int tn_fast_tile_m(const FastTNArgs& a);
 int tn_fast_post_rows(const FastTNArgs& a);  // partial rows (ppart) a launch_tn_fast call writes

@@ -929,6 +929,12 @@ int tn_fast_post_rows(const FastTNArgs& a) {
   return cfg == 0 ? halo3_blocks(a) : ceil_div(a.M, tn_cfg_bm(cfg));
 }
 
+int tn_fast_config(const FastTNArgs& a, int* taps_out) {
+  const int cfg = tn_config(a);
+  if (taps_out) *taps_out = (cfg >= 7 && cfg <= 14) ? tn_taps(a) : 0;
+  return cfg;
+}
+
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
   if (a.M <= 0 || a.Ng <= 0) return 0;
   switch (tn_config(a)) {

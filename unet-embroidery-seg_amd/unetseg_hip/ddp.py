@@ -52,8 +52,24 @@ class GradBuckets:
     @torch.no_grad()
     def broadcast_state(self):
         dist.broadcast(self.model._flat, 0, group=self.group)
-        for b in self.model.buffers():
-            dist.broadcast(b, 0, group=self.group)
+        self.sync_buffers()
+
+    @torch.no_grad()
+    def sync_buffers(self):
+        """Re-broadcast rank 0's BN running statistics (one coalesced collective).  Between syncs
+        they are rank-local (each rank's batch statistics; DDP without SyncBN).  torch DDP's default
+        broadcast_buffers=True does this before every forward; here the train loop calls it before
+        evaluation and checkpointing, where the running statistics are read."""
+        bufs = [b for b in self.model.buffers()]
+        if not bufs:
+            return
+        flat = torch.cat([b.detach().double().reshape(-1) for b in bufs])  # int64 counters survive fp64
+        dist.broadcast(flat, 0, group=self.group)
+        off = 0
+        for b in bufs:
+            n = b.numel()
+            b.copy_(flat[off:off + n].view(b.shape).to(b.dtype))
+            off += n
 
     def _reset(self):
         self._left = [b[2] for b in self.buckets]

@@ -82,7 +82,16 @@ SIGNATURES = {
     "unetseg_stem_wgrad_workspace": (SZ, [I, I, I, I]),
     "unetseg_stem_wgrad": (I, [P, I, I, I, P, I, I, P, SZ, P, I, I, P]),
     "unetseg_adam_dev": (I, [P, P, P, P, L, P, P, F, F, F, F, P, P]),
+    "unetseg_conv2d_fwd_config": (I, [I, I, I, I, I, I, I, I, I, I, I, I, I, P]),
+    "unetseg_conv2d_dgrad_config": (I, [I, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P]),
+    "unetseg_conv2d_wgrad_config": (I, [I, I, I, I, I, I, I, I, I, I, I, I, I, I, P]),
+    "unetseg_stem_config": (I, [I, I, I, I, P]),
 }
+
+#: functions returning a value rather than a status (no RuntimeError on non-zero)
+VALUE_FUNCS = {"reduce_tiles", "pw_small_tiles", "conv_tile_m", "abi_version", "conv2d_fwd_tile_m",
+               "conv2d_dgrad_post", "stem_fwd_tile_m", "attn_bwd1_tiles", "pw_small_tile", "conv2d_fwd_config",
+               "conv2d_dgrad_config", "conv2d_wgrad_config", "stem_config"}
 
 _lib = None
 
@@ -122,9 +131,7 @@ class _Caller:
 
     def __getattr__(self, item):
         fn = getattr(load(), "unetseg_" + item)
-        if SIGNATURES["unetseg_" + item][0] is I and item not in ("reduce_tiles", "pw_small_tiles", "conv_tile_m",
-                                                                    "abi_version", "conv2d_fwd_tile_m",
-                                                                    "conv2d_dgrad_post", "stem_fwd_tile_m", "attn_bwd1_tiles", "pw_small_tile"):
+        if SIGNATURES["unetseg_" + item][0] is I and item not in VALUE_FUNCS:
             def call(*args):
                 rc = fn(*args)
                 if rc != 0:
@@ -135,3 +142,49 @@ class _Caller:
 
 
 lib = _Caller()
+
+
+# ------------------------------------------------------------------------------------------------
+# kernel-configuration queries (host only; used by the parity tests and the bench's config table)
+# ------------------------------------------------------------------------------------------------
+CFG_NAMES = {0: "halo3", 1: "tn256x64", 2: "tn256x128", 3: "tn128x128", 4: "tn128x128_1step", 5: "tn64x128",
+             6: "tn128x64", 7: "ring256x128", 8: "ring128x128", 9: "ring64x128", 10: "ring128x128_5st",
+             11: "ring256x64", 12: "ring128x64_4st", 13: "ring128x64", 14: "ring256x64_8w", 100: "generic"}
+WG_NAMES = {0: "halo3_wgrad", 1: "wgrad64x256_row", 2: "wgrad128_row", 3: "wgrad64x256", 4: "wgrad128",
+            5: "wgrad_generic"}
+
+
+def _cfg_name(cfg, taps):
+    n = CFG_NAMES.get(cfg, str(cfg))
+    return f"{n}_t{taps}" if taps else n
+
+
+def fwd_config(dtype, c1, ldc1, c2, ldc2, n, h, w, cout, r, s, stride, pad):
+    taps = ctypes.c_int(0)
+    cfg = load().unetseg_conv2d_fwd_config(dtype, c1, ldc1, c2, ldc2, n, h, w, cout, r, s, stride, pad,
+                                           ctypes.byref(taps))
+    return _cfg_name(cfg, taps.value)
+
+
+def dgrad_config(dtype, ldy, n, p, q, cout, cin, r, s, stride, pad, ldx, h, w):
+    """list of configuration names, one per launched output-parity class"""
+    cfg = (ctypes.c_int * 4)()
+    taps = (ctypes.c_int * 4)()
+    load().unetseg_conv2d_dgrad_config(dtype, ldy, n, p, q, cout, cin, r, s, stride, pad, ldx, h, w, cfg, taps)
+    return [_cfg_name(cfg[i], taps[i]) for i in range(stride * stride) if cfg[i] >= 0]
+
+
+def wgrad_config(dtype, c1, ldc1, c2, ldc2, n, h, w, ldy, cout, r, s, stride, pad):
+    """(kernel name, split-K slabs, reduce kernel name)"""
+    sp = ctypes.c_int(0)
+    kind = load().unetseg_conv2d_wgrad_config(dtype, c1, ldc1, c2, ldc2, n, h, w, ldy, cout, r, s, stride, pad,
+                                              ctypes.byref(sp))
+    red = 16 if sp.value >= 16 else 4 if sp.value >= 4 else 1
+    return WG_NAMES.get(kind, str(kind)), sp.value, f"reduce{red}"
+
+
+def stem_config(n, h, w, K):
+    sp = ctypes.c_int(0)
+    cfg = load().unetseg_stem_config(n, h, w, K, ctypes.byref(sp))
+    red = 16 if sp.value >= 16 else 4 if sp.value >= 4 else 1
+    return CFG_NAMES.get(cfg, str(cfg)), sp.value

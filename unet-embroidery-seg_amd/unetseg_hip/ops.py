@@ -276,7 +276,9 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
         st = (ctx.f32(math.ceil(M / tile), 2, K), tile)  # [row tiles][sum, M2][K]
     b = pc.conv.bias
     flops = 2.0 * M * K * pc.C * R * S  # algorithmic (unpadded Cin)
-    desc = (N, H, W, C1, C2, K, R, S, stride)
+    # probe descriptor: (N, H, W, C1, C2, K, R, S, stride, pad, ld1, ld2); bench/tools map it to the
+    # kernel configuration through the unetseg_conv2d_*_config queries
+    desc = (N, H, W, C1, C2, K, R, S, stride, pad, ldp(X1), ldp(X2))
     with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
         lib.conv2d_fwd(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride, pad,
                        P(b), int(relu), P(y), K, P(st[0] if st else None), ctx.stream)
@@ -334,7 +336,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
             dwp = torch.empty(Kp, pc.C, dtype=torch.float32, device=dev)
             if side is not None:
                 dwp.record_stream(side)
-            with _probe("wgrad", flops, 1, ("wgrad",) + desc, stream=side):
+            with _probe("wgrad", flops, 1, ("wgrad_padk",) + desc, stream=side):
                 lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), 0, 0, 0, N, H, W, P(dY), Kp, Kp, 1, 1, 1, 0, P(ws),
                                  ws.numel(), P(dwp), pc.C, 0, wst)
                 lib.add(DT_F32, P(dwp), pc.C, P(pc.conv.weight.grad), pc.C, K, pc.C, wst)
@@ -349,7 +351,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
                 wtp = torch.zeros(C1, Kp, dtype=ctx.tdtype, device=dev)
                 lib.add(ctx.dt, P(pc.wt), K, P(wtp), Kp, C1, K, ctx.stream)
                 g, acc = gbuf(ctx, x1)
-                with _probe("igemm_tn", flops, 1, ("dgrad",) + desc):
+                with _probe("igemm_tn", flops, 1, ("dgrad_padk",) + desc):
                     lib.conv2d_dgrad(ctx.dt, P(dY), Kp, N, Pq, Qq, P(wtp), Kp, C1, 1, 1, 1, 0, P(g), ldp(g), H, W, acc,
                                      ctx.stream)
         elif x2 is None:
@@ -386,7 +388,7 @@ def _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
         return False
     g = ctx.empty(N, H, W, C1)
     part = ctx.f32(rows, 2, C1)
-    with _probe("igemm_tn", flops, stride * stride, ("dgrad",) + desc):
+    with _probe("igemm_tn", flops, stride * stride, (f"dgrad_post{kind}",) + desc):
         rc = lib.conv2d_dgrad_post(*args, P(g), C1, H, W, kind, P(aux), ldp(aux), *coeffs, P(part), rows, ctx.stream)
     if rc != 0:
         raise RuntimeError(f"unetseg_conv2d_dgrad_post failed ({rc}): {lib_last_error()}")
@@ -424,8 +426,8 @@ def stem_conv(ctx, x, conv_mod):
     tile = lib.stem_fwd_tile_m(N, H, W, K)
     st = (ctx.f32(math.ceil(M / tile), 2, K), tile)
     flops = 2.0 * M * K * C * 49
-    desc = (N, H, W, C, 0, K, 7, 7, 2)
-    with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
+    desc = (N, H, W, C, 0, K, 7, 7, 2, 3, 8, 0)
+    with _probe("igemm_tn", flops, 1, ("stem_fwd",) + desc):
         lib.stem_fwd(P(xp), N, H, W, P(wk), K, P(y), K, P(st[0]), ctx.stream)
     out = Node(y)
 
@@ -444,7 +446,7 @@ def stem_conv(ctx, x, conv_mod):
         else:
             ws = workspace(ws_bytes, ctx.device)
             wst = ctx.stream
-        with _probe("wgrad", flops, 1, ("wgrad",) + desc, stream=side):
+        with _probe("wgrad", flops, 1, ("stem_wgrad",) + desc, stream=side):
             lib.stem_wgrad(P(xp), N, H, W, P(dY), ldp(dY), K, P(ws), ws.numel(), P(conv_mod.weight.grad), C, 1, wst)
         ctx.param_done(conv_mod.weight)
 
