@@ -47,29 +47,75 @@ def parse():
     return ap.parse_args()
 
 
+def _cpu_share():
+    """(threads to use, host CPU model, CPUs visible, CPU share) -- os.cpu_count() is the whole
+    machine on the GPU box; the process's affinity mask and cgroup quota give its share."""
+    visible = os.cpu_count() or 1
+    try:
+        share = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        share = visible
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            share = min(share, max(1, int(-(-int(q) // int(per)))))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return share, model, visible
+
+
 def cpu_baseline(model_name, size, batch):
-    """The oracle's fp32 train step (fwd + loss + bwd + Adam) on host cores; bounded sample."""
+    """The oracle's train step (fwd + loss + bwd + Adam) on this host's cores, bounded sample, in the
+    reference's CPU precision for the task: binary loops run under bf16 autocast
+    on CPU (train.py:170 always builds a GradScaler object, utils/train_and_eval.py:218), the
+    multitask loop in fp32 (train.py:243).  fp32 is timed for the binary models too."""
     from oracle import ref_cpu
     from oracle.weights import make_torch_state
     from utils.synthetic import make_batch
 
-    threads = min(16, os.cpu_count() or 1)
+    threads, cpu_model, visible = _cpu_share()
     torch.set_num_threads(threads)
-    kw = dict(num_classes=1) if model_name == "multitask_unet" else dict(num_classes=2)
+    multitask = model_name == "multitask_unet"
+    kw = dict(num_classes=1) if multitask else dict(num_classes=2)
     params, buffers = ref_cpu.split_state(make_torch_state(ref_cpu.model_spec(model_name, **kw)))
     m1 = {k: torch.zeros_like(v) for k, v in params.items()}
     m2 = {k: torch.zeros_like(v) for k, v in params.items()}
-    x, y = make_batch(batch, size, seed=99)
-    times = []
-    for i in range(3):  # 1 warmup + 2 timed
-        t0 = time.perf_counter()
-        _, _, grads = ref_cpu.train_step(model_name, params, buffers, x, y, "lovasz_hinge")
-        ref_cpu.adam_step(params, grads, m1, m2, i + 1, 1e-4)
-        times.append(time.perf_counter() - t0)
-    t = min(times[1:])
-    return {"value": round(batch / t, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"oracle fp32 {model_name} {size}x{size} batch {batch}, 1 warmup + 2 timed train steps "
-                      f"(fwd+lovasz+bwd+Adam), best step {t:.2f} s, torch {torch.__version__} CPU"}
+    x, y, c = make_batch(batch, size, seed=99, with_cls=True)
+    mask = (torch.rand(batch, 512, generator=torch.Generator().manual_seed(5)) >= 0.5).float()
+
+    def timed(autocast):
+        times = []
+        for i in range(3):  # 1 warmup + 2 timed
+            t0 = time.perf_counter()
+            if multitask:
+                _, _, grads = ref_cpu.train_step_multitask(params, buffers, x, y, c, mask, 1.0, "bce")
+            else:
+                _, _, grads = ref_cpu.train_step(model_name, params, buffers, x, y, "lovasz_hinge",
+                                                 autocast_bf16=autocast)
+            ref_cpu.adam_step(params, grads, m1, m2, i + 1, 1e-4)
+            times.append(time.perf_counter() - t0)
+        return min(times[1:])
+
+    t_main = timed(not multitask)
+    out = {"value": round(batch / t_main, 4), "unit": "images/s", "cores": threads, "kind": "port",
+           "precision": "fp32" if multitask else "bf16 autocast (reference CPU default)",
+           "host_cpu": cpu_model, "host_cpus_visible": visible}
+    if not multitask:
+        t32 = timed(False)
+        out["fp32_value"] = round(batch / t32, 4)
+    out["sample"] = (f"oracle {model_name} {size}x{size} batch {batch}, 1 warmup + 2 timed train steps "
+                     f"(fwd+{'bce+ce' if multitask else 'lovasz'}+bwd+Adam) per precision, best step "
+                     f"{t_main:.2f} s, {threads} threads (this process's CPU share of {visible}), "
+                     f"torch {torch.__version__} CPU")
+    return out
 
 
 def pmc_traffic(workload, kind):
@@ -86,6 +132,23 @@ def pmc_traffic(workload, kind):
             continue
         if d.get("workload") == workload and kind in d.get("groups", {}):
             best = (round(d["groups"][kind]["traffic_bytes_per_launch"]), os.path.relpath(f, REPO))
+    return best
+
+
+def pmc_mfma(workload, kind):
+    """MFMA busy fraction of `kind` from the committed PMC summary (tools/pmc_mfma.py) for this exact
+    workload: SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) over the group's kernels."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_mfma.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        g = d.get("groups", {}).get(kind)
+        if d.get("workload") == workload and g and g.get("mfma_busy") is not None:
+            best = (round(g["mfma_busy"], 4), os.path.relpath(f, REPO))
     return best
 
 
@@ -213,9 +276,11 @@ def main():
         fl, sec, n = kinds[dom]
         ach = fl / sec / 1e12
         tr = pmc_traffic(workload, dom)
+        mb = pmc_mfma(workload, dom)
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": tr[0] if tr else None,
                 "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": tr[1] if tr else None,
+                "mfma_busy": mb[0] if mb else None, "mfma_busy_source": mb[1] if mb else None,
                 "launches_per_step": n, "avg_launch_us": round(1e6 * sec / n, 2),
                 "algorithmic_gflop_per_step": round(fl / 1e9, 1),
                 "kernels": {k: {"tflops": round(v[0] / v[1] / 1e12, 2), "ms_per_step": round(1e3 * v[1], 3),
@@ -231,7 +296,7 @@ def main():
         in_sync = bool(float(hi.item()) == float(lo.item()))
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_baseline and not multitask:
+    if rank == 0 and world == 1 and args.cpu_baseline:
         cpu = cpu_baseline(args.model, args.size, args.cpu_batch)
 
     if rank == 0:

@@ -44,12 +44,12 @@ def main():
                             "traffic_bytes_per_launch": (f2 + w) / nl}
     per = {}
     for n, v in fetch:
-        k = n.split("(")[0].replace("void (anonymous namespace)::", "")[:80]
+        k = n.replace("void (anonymous namespace)::", "").replace("(anonymous namespace)::", "").split("(")[0][:80]
         e = per.setdefault(k, [0, 0.0, 0.0])
         e[0] += 1
         e[1] += 2.0 * v
     for n, v in write:
-        k = n.split("(")[0].replace("void (anonymous namespace)::", "")[:80]
+        k = n.replace("void (anonymous namespace)::", "").replace("(anonymous namespace)::", "").split("(")[0][:80]
         if k in per:
             per[k][2] += v
     top = sorted(per.items(), key=lambda kv: -(kv[1][1] + kv[1][2]))[:25]

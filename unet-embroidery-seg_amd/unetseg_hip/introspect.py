@@ -47,12 +47,15 @@ def call_configs(desc, dt=DT_BF16):
 
 
 def probe_table(records, dt=DT_BF16):
-    """{config key: [calls, seconds]} over ops.PROBE records (event times summed per call)"""
+    """{config key: [calls, seconds]} over ops.PROBE records (event times summed per call; a
+    call's whole bracket -- every parity class, the split-K reduce -- is charged to its first key,
+    the reduce key only counts calls)"""
     out = {}
     for kind, flops, nl, e0, e1, desc in records:
         t = e0.elapsed_time(e1) * 1e-3
-        for key in call_configs(desc, dt):
+        for i, key in enumerate(call_configs(desc, dt)):
             v = out.setdefault(key, [0, 0.0])
             v[0] += 1
-            v[1] += t
+            if i == 0:
+                v[1] += t
     return out
