@@ -126,6 +126,10 @@ int unetseg_pack_input(int dtype, const float* x, int n, int c, int h, int w, in
 int unetseg_bn_finalize(const float* part, int C, int G, long M, int tile, const float* gamma, const float* beta,
                         float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* mean,
                         float* invstd, float* scale, float* shift, void* stream);
+/* BN partials of an NHWC view no conv produced (model/unet_dualdense.py:9-10: BatchNorm over a dense
+ * block's concatenation): part [ceil(M/tile)][2][C] = (sum, M2 about the tile mean), for bn_finalize */
+int unetseg_channel_stats_tiles(long M, int tile);
+int unetseg_channel_stats(int dtype, const void* x, int ldx, long M, int c, int tile, float* part, void* stream);
 int unetseg_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar,
                            float eps, float* scale, float* shift, void* stream);
 /* out = [relu](y*sc + sh [+ r | + r*sc2 + sh2])   res_mode 0 none, 1 identity add, 2 BN'd add */
@@ -171,6 +175,19 @@ int unetseg_upsample2x_fwd(int dtype, const void* x, int ldx, int n, int h, int 
 int unetseg_upsample2x_bwd(int dtype, const void* dy, int ldy, int n, int h, int w, int c, int align_corners,
                            void* dx, int ldx, int accumulate, void* stream);
 int unetseg_add(int dtype, const void* x, int ldx, void* out, int ldo, long M, int c, void* stream);
+/* general bilinear resize to (oh, ow) with ATen's source-index rule (F.interpolate(size=...):
+ * model/unet_attention.py:31-33,52-53, model/unet_dualdense.py:57-58; align_corners=True for the
+ * multiclass losses' logit resize, model/unet_training.py:14-15); backward is a deterministic gather */
+int unetseg_resize_bilinear_fwd(int dtype, const void* x, int ldx, int n, int h, int w, int c, int oh, int ow,
+                                int align_corners, void* y, int ldy, void* stream);
+int unetseg_resize_bilinear_bwd(int dtype, const void* dy, int ldy, int n, int h, int w, int c, int oh, int ow,
+                                int align_corners, void* dx, int ldx, int accumulate, void* stream);
+/* zero padding x [n][h][w] into y [n][oh][ow] at (top, left) (F.pad, model/unet_plain.py:42-45) and its
+ * backward dx (+)= the (top, left) window of dy */
+int unetseg_pad2d_fwd(int dtype, const void* x, int ldx, int n, int h, int w, int c, int top, int left, int oh,
+                      int ow, void* y, int ldy, void* stream);
+int unetseg_pad2d_bwd(int dtype, const void* dy, int ldy, int n, int h, int w, int c, int top, int left, int oh,
+                      int ow, void* dx, int ldx, int accumulate, void* stream);
 
 /* ---- narrow 1x1 heads (final / outc / seg_head / psi: model/unet_resnet.py:78,
  *      model/unet_plain.py:69, model/unet_multitask.py:69, model/unet_attention.py:24) ------------ */
@@ -207,6 +224,9 @@ int unetseg_attn_bwd2(int dtype, const float* dpsibn, const float* psi, const fl
 size_t unetseg_lovasz_workspace(int B, long P);
 int unetseg_lovasz_fwd(const float* out, int nch, const int64_t* tgt, int B, long P, void* ws, size_t ws_bytes,
                        float* gz, float* loss, void* stream);
+/* per-image Lovasz over the pixels whose target is not ignore_index (model/unet_training.py:268-274) */
+int unetseg_lovasz_fwd_masked(const float* out, int nch, const int64_t* tgt, int B, long P, long ignore_index, void* ws,
+                              size_t ws_bytes, float* gz, float* loss, void* stream);
 /* BCE-with-logits mean with optional scalar pos_weight (model/unet_training.py:205-216) */
 size_t unetseg_bce_workspace(int B, long P);
 int unetseg_bce_fwd(const float* out, int nch, const int64_t* tgt, int B, long P, const float* pos_weight, void* ws,
@@ -217,10 +237,47 @@ int unetseg_dz_to_dout(const float* gz, int B, long P, int nch, const float* s1,
 /* global tp/fp/fn/tn (argmax, tie -> class 0) of utils/train_and_eval.py:116-138,293 */
 int unetseg_confusion(const float* out, int nch, const int64_t* tgt, int B, long P, unsigned long long* conf,
                       void* stream);
+/* the same with ignore_index (utils/train_and_eval.py:125-126,172-176): pixels whose target equals
+ * ignore_index are skipped by the counts and the losses.  masked loss kind 0 = BCE over the valid
+ * pixels, 1 = the reference's Lovasz on the flattened valid pixels (a per-pixel hinge mean, since
+ * lovasz_hinge_loss then loops over single elements: model/unet_training.py:267-276) */
+int unetseg_confusion_masked(const float* out, int nch, const int64_t* tgt, int B, long P, long ignore_index,
+                             unsigned long long* conf, void* stream);
+size_t unetseg_masked_loss_workspace(int B, long P);
+int unetseg_masked_loss_fwd(const float* out, int nch, const int64_t* tgt, int B, long P, long ignore_index, int kind,
+                            const float* pos_weight, void* ws, size_t ws_bytes, float* gz, float* loss, void* stream);
 /* cross entropy, mean over the batch (MultiTaskLoss: model/unet_multitask.py:119-139) */
 int unetseg_ce_fwd(const float* logits, const int64_t* tgt, int B, int K, float* loss, float* dlog, void* stream);
 int unetseg_scale_grad(const float* g, long n, const float* s1, float a1, const float* s2, float a2, float* out,
                        void* stream);
+
+/* ---- multiclass task (model/unet_training.py:9-91 CE_Loss / Focal_Loss / Dice_loss;
+ *      utils/train_and_eval.py:20-103 metrics; model/*.py outc/final with num_classes > 2;
+ *      predict.py:79-93 post-processing).  Logits fp32 planar [B][C][P], C <= 32. ----------------- */
+/* 1x1 head with 1 <= k <= 32 outputs: y fp32 [n][k][hw] = x . W^T + b (W fp32 [k][c]) */
+int unetseg_pw_head_fwd(int dtype, const void* x, int ldx, long M, int hw, int c, int k, const float* w,
+                        const float* b, float* y, void* stream);
+int unetseg_pw_head_tiles(long M);
+/* dx (may be NULL) (+)= dy . W; part_w [k][c][G], part_b [k][G] (G = unetseg_pw_head_tiles(M)); c divides 256 */
+int unetseg_pw_head_bwd(int dtype, const float* dy, const void* x, int ldx, long M, int hw, int c, int k,
+                        const float* w, void* dx, int lddx, int dx_acc, float* part_w, float* part_b, void* stream);
+size_t unetseg_mc_loss_workspace(int B, int C, long P);
+/* loss fp32[3] = (total, main, dice).  focal: main term 0 = CE (class weights cls_w or NULL, ignore_index),
+ * 1 = Focal (alpha < 0: None, gamma), 2 = none; dice_t float [B][P][ct] one-hot (NULL: no Dice term) */
+int unetseg_mc_loss_fwd(const float* out, const int64_t* tgt, int B, int C, long P, const float* cls_w,
+                        long ignore_index, int focal, float alpha, float gamma, const float* dice_t, int ct,
+                        float beta, float smooth, void* ws, size_t ws_bytes, float* loss, void* stream);
+/* dout fp32 [B][C][P] = gscale[0] * d total / d out (same arguments and workspace as the forward) */
+int unetseg_mc_loss_bwd(const float* out, const int64_t* tgt, int B, int C, long P, const float* cls_w,
+                        long ignore_index, int focal, float alpha, float gamma, const float* dice_t, int ct,
+                        float beta, float smooth, const void* ws, const float* gscale, float* dout, void* stream);
+/* hist u64 [(C+1)][C] += (target row, argmax column); targets outside [0, C) count in row C */
+int unetseg_mc_confusion(const float* out, const int64_t* tgt, int B, int C, long P, unsigned long long* hist,
+                         void* stream);
+/* one image: labels int32 [OH][OW] = argmax_c bilinear(align_corners=False)-resized softmax of the
+ * logits [C][H][W] cropped to rows y0..y0+ch, cols x0..x0+cw */
+int unetseg_softmax_resize_argmax(const float* logits, int C, int H, int W, int y0, int x0, int ch, int cw, int OH,
+                                  int OW, int32_t* labels, void* stream);
 
 /* ---- streams ---------------------------------------------------------------------------------- */
 /* `waiter` waits for everything enqueued so far on `signaler` (device-scope release event; no

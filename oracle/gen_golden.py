@@ -186,5 +186,184 @@ def main():
     print("golden fixtures written to", OUT)
 
 
+def gen_init():
+    """init_seed11.npz: the reference's create_model init (train.py:48-59 = build_model +
+    weights_init, model/unet_training.py:94-113) under torch.manual_seed(11) (train.py seeds 11 via
+    seed_everything, utils/utils.py:50-57).  Per state_dict entry: sha256 of the float32/int64
+    bytes (bit-exact pin without shipping 176 MB) plus the first 8 values."""
+    import hashlib
+
+    sys.path.insert(0, REF)
+    sys.dont_write_bytecode = True
+    from model.model_factory import build_model
+    from model.unet_training import weights_init
+
+    rec = {}
+    for name, kw in [("unet_plain", dict(num_classes=2)), ("unet_resnet50", dict(num_classes=2)),
+                     ("attention_unet", dict(num_classes=2)),
+                     ("multitask_unet", dict(num_classes=1, num_seg_classes=1, num_cls_classes=3)),
+                     ("dualdense_unet", dict(num_classes=2)), ("dualdense_unet", dict(num_classes=5))]:
+        torch.manual_seed(11)
+        m = build_model(name, **kw)
+        weights_init(m)
+        tag = f"{name}_c{kw['num_classes']}"
+        keys, digests, heads = [], [], []
+        for k, v in m.state_dict().items():
+            a = v.detach().contiguous().numpy()
+            keys.append(k)
+            digests.append(hashlib.sha256(a.tobytes()).hexdigest())
+            h = np.zeros(8, dtype=np.float64)
+            flat = a.reshape(-1)[:8].astype(np.float64)
+            h[:flat.size] = flat
+            heads.append(h)
+        rec[tag + "::keys"] = np.array(keys)
+        rec[tag + "::sha256"] = np.array(digests)
+        rec[tag + "::head"] = np.stack(heads)
+    np.savez_compressed(os.path.join(OUT, "init_seed11.npz"), **rec)
+    print("wrote init_seed11.npz")
+
+
+def gen_loop():
+    """loop_unet_plain.npz: the reference's own train_one_epoch_binary (utils/train_and_eval.py:185-263,
+    fp32: scaler None) for 3 epochs of 2 batches with the warm-cos LR (set_optimizer_lr per epoch) and
+    Adam (train.py:62-78), then evaluate_binary (:266-305) on a validation list."""
+    sys.path.insert(0, REF)
+    sys.dont_write_bytecode = True
+    import contextlib
+    import io
+
+    from model.unet_training import get_lr_scheduler, set_optimizer_lr
+    from utils.train_and_eval import evaluate_binary, train_one_epoch_binary
+
+    torch.set_num_threads(8)
+    torch.manual_seed(0)
+    m = ref_model("unet_plain", num_classes=2)
+    load_hash(m)
+    batches = []
+    for i in range(2):
+        x, y = synth(2, 64, seed=700 + i)
+        batches.append((x, y, torch.zeros(1)))
+    vx, vy = synth(2, 64, seed=777)
+    val = [(vx, vy, torch.zeros(1))]
+    opt = torch.optim.Adam(m.parameters(), 1e-4, betas=(0.9, 0.999), weight_decay=1e-4)
+    sched = get_lr_scheduler("cos", 1e-4, 1e-6, 3)
+    losses_ep = []
+    dev = torch.device("cpu")
+    with contextlib.redirect_stdout(io.StringIO()):
+        for ep in range(3):
+            set_optimizer_lr(opt, sched, ep)
+            losses_ep.append(train_one_epoch_binary(m, opt, batches, dev, "lovasz_hinge", None, 0.0, None, ep, 3))
+        met = evaluate_binary(m, val, dev, "lovasz_hinge", None)
+    fin = {k: v.numpy() for k, v in m.state_dict().items() if k in ("outc.weight", "outc.bias", "up4.conv.net.3.weight")}
+    rec = {"x%d" % i: b[0].numpy() for i, b in enumerate(batches)}
+    rec.update({"y%d" % i: b[1].numpy() for i, b in enumerate(batches)})
+    rec.update(vx=vx.numpy(), vy=vy.numpy(), epoch_loss=np.array(losses_ep),
+               metrics=np.array([met[k] for k in ("Dice", "IoU", "Precision", "Recall", "Accuracy", "Loss")]))
+    rec.update({"final::" + k: v for k, v in fin.items()})
+    np.savez_compressed(os.path.join(OUT, "loop_unet_plain.npz"), **rec)
+    print("wrote loop_unet_plain.npz", losses_ep, met)
+
+
+def gen_multiclass():
+    """multiclass.npz: the reference's CE_Loss / Focal_Loss / Dice_loss (values + logit gradients;
+    class weights, the ignore label num_classes, a non-matching size that triggers their logit
+    interpolation) and the four multiclass metrics (utils/train_and_eval.py:20-103)."""
+    sys.path.insert(0, REF)
+    sys.dont_write_bytecode = True
+    from model.unet_training import CE_Loss, Dice_loss, Focal_Loss
+    from utils.train_and_eval import frequency_weighted_iou, mean_accuracy, mean_iou, pixel_accuracy
+
+    g = torch.Generator().manual_seed(21)
+    rec = {}
+    for tag, (n, c, h, w, ht, wt) in {"a": (2, 5, 24, 20, 24, 20), "b": (3, 21, 16, 16, 16, 16),
+                                      "r": (2, 4, 12, 10, 24, 20)}.items():
+        logits = torch.randn(n, c, h, w, generator=g) * 2
+        tgt = torch.randint(0, c + 1, (n, ht, wt), generator=g)  # c = ignore label (num_classes)
+        onehot = torch.eye(c + 1)[tgt.reshape(-1)].reshape(n, ht, wt, c + 1)
+        cw = (0.5 + torch.rand(c, generator=g)).float()
+        rec[f"{tag}_logits"], rec[f"{tag}_tgt"], rec[f"{tag}_onehot"], rec[f"{tag}_cw"] = (
+            logits.numpy(), tgt.numpy(), onehot.numpy(), cw.numpy())
+        for name, fn in {"ce": lambda x: CE_Loss(x, tgt, cw, num_classes=c),
+                         "ce1": lambda x: CE_Loss(x, tgt, torch.ones(c), num_classes=c),
+                         "focal": lambda x: Focal_Loss(x, tgt, cw, num_classes=c),
+                         "dice": lambda x: Dice_loss(x, onehot)}.items():
+            x = logits.clone().requires_grad_(True)
+            v = fn(x)
+            v.backward()
+            rec[f"{tag}_{name}"] = np.array([v.item()])
+            rec[f"{tag}_{name}_grad"] = x.grad.numpy()
+        if (h, w) == (ht, wt):
+            rec[f"{tag}_metrics"] = np.array([pixel_accuracy(logits, tgt), mean_accuracy(logits, tgt, c),
+                                              mean_iou(logits, tgt, c), frequency_weighted_iou(logits, tgt, c)])
+    np.savez_compressed(os.path.join(OUT, "multiclass.npz"), **rec)
+    print("wrote multiclass.npz")
+
+
+def gen_ignore():
+    """ignore.npz: binary_segmentation_loss / lovasz_hinge_loss / confusion with ignore_index (255)
+    (utils/train_and_eval.py:116-182, model/unet_training.py:253-280)."""
+    sys.path.insert(0, REF)
+    sys.dont_write_bytecode = True
+    from model.unet_training import lovasz_hinge_loss
+    from utils.train_and_eval import _binary_confusion_from_pred, binary_segmentation_loss
+
+    g = torch.Generator().manual_seed(31)
+    two = torch.randn(3, 2, 20, 24, generator=g) * 2
+    tgt = (torch.rand(3, 20, 24, generator=g) < 0.4).long()
+    tgt[torch.rand(3, 20, 24, generator=g) < 0.2] = 255
+    tgt[2] = 255  # one image entirely ignored
+    rec = {"two": two.numpy(), "tgt": tgt.numpy()}
+    for name in ("bce", "lovasz_hinge"):
+        x = two.clone().requires_grad_(True)
+        v = binary_segmentation_loss(x, tgt, name, pos_weight=torch.tensor([1.3]) if name == "bce" else None,
+                                     ignore_index=255)
+        v.backward()
+        rec[f"{name}"] = np.array([v.item()])
+        rec[f"{name}_grad"] = x.grad.numpy()
+    z = (two[:, 1] - two[:, 0]).clone().requires_grad_(True)
+    v = lovasz_hinge_loss(z, tgt, ignore_index=255)
+    v.backward()
+    rec["lovasz_direct"] = np.array([v.item()])
+    rec["lovasz_direct_grad"] = z.grad.numpy()
+    rec["conf"] = np.array(_binary_confusion_from_pred(two.argmax(1), tgt, ignore_index=255), dtype=np.int64)
+    np.savez_compressed(os.path.join(OUT, "ignore.npz"), **rec)
+    print("wrote ignore.npz", rec["bce"], rec["lovasz_hinge"], rec["lovasz_direct"], rec["conf"])
+
+
+def gen_models2():
+    """model_dualdense_unet.npz and odd-size fixtures (unet_plain / attention_unet / dualdense at 72x88:
+    the pad-then-cat and interpolate branches), hash weights, train mode fp32: logits, loss, grad norms."""
+    sys.path.insert(0, REF)
+    sys.dont_write_bytecode = True
+    from utils.train_and_eval import binary_segmentation_loss
+
+    torch.set_num_threads(8)
+    for name, s, b, tag in [("dualdense_unet", 64, 2, "model_dualdense_unet"),
+                            ("unet_plain", (72, 88), 2, "odd_unet_plain"),
+                            ("attention_unet", (72, 88), 2, "odd_attention_unet"),
+                            ("dualdense_unet", (72, 88), 1, "odd_dualdense_unet")]:
+        torch.manual_seed(0)
+        m = ref_model(name, num_classes=2)
+        spec = load_hash(m)
+        hh, ww = (s, s) if isinstance(s, int) else s
+        x, y = synth(b, max(hh, ww), seed=2000 + hh)
+        x, y = x[:, :, :hh, :ww].contiguous(), y[:, :hh, :ww].contiguous()
+        m.train()
+        out = m(x)
+        loss = binary_segmentation_loss(out, y, "lovasz_hinge")
+        loss.backward()
+        rec = {"x": x.numpy(), "y": y.numpy(), "out": out.detach().numpy(), "loss": np.array([loss.item()]),
+               "grad_names": np.array([k for k, _ in m.named_parameters()]),
+               "grad_norms": np.array([float(p.grad.double().norm()) for _, p in m.named_parameters()])}
+        m.eval()
+        with torch.no_grad():
+            rec["eval_out"] = m(x).numpy()
+        np.savez_compressed(os.path.join(OUT, f"{tag}.npz"), **rec)
+        print("wrote", tag, loss.item())
+
+
 if __name__ == "__main__":
-    main()
+    which = sys.argv[1:] or ["main"]
+    for w in which:
+        {"main": main, "init": gen_init, "loop": gen_loop, "multiclass": gen_multiclass, "ignore": gen_ignore,
+         "models2": gen_models2}[w]()

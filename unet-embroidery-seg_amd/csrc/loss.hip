@@ -33,15 +33,19 @@ __device__ __forceinline__ float load_z(const float* out, int nch, int b, long P
   return nch == 2 ? base[P + i] - base[i] : base[i];
 }
 
+// has_ignore: pixels whose target is `ignore` get error -inf and label 0, so they sort after every
+// valid pixel and contribute to neither the loss, the gradient nor the Jaccard counts of the valid
+// prefix: the per-image Lovasz over the valid pixels (model/unet_training.py:268-274)
 __global__ void lovasz_keygen_kernel(const float* out, int nch, const int64_t* tgt, int B, long P, uint32_t* keys,
-                                     uint32_t* vals) {
+                                     uint32_t* vals, int has_ignore, long ignore) {
   const long total = (long)B * P;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int b = (int)(i / P);
     const long px = i - (long)b * P;
     const float z = load_z(out, nch, b, P, px);
-    const uint32_t y = tgt[i] == 1 ? 1u : 0u;
-    const float e = 1.0f - z * (2.0f * (float)y - 1.0f);
+    const bool ign = has_ignore && tgt[i] == ignore;
+    const uint32_t y = (!ign && tgt[i] == 1) ? 1u : 0u;
+    const float e = ign ? -INFINITY : 1.0f - z * (2.0f * (float)y - 1.0f);
     keys[i] = desc_key(e);
     vals[i] = (uint32_t)px | (y << 31);
   }
@@ -279,13 +283,78 @@ __global__ void sum_kernel(const float* x, int n, float* out) {
   if (threadIdx.x == 0) out[0] = (float)s;
 }
 
-// confusion counts: mode 2 -> pred = o1 > o0 (argmax, tie -> 0); mode 1 -> pred = sigmoid(o0) > 0.5
+// Binary loss over the pixels whose target is not ignore_index (utils/train_and_eval.py:169-176):
+// kind 0 = BCE-with-logits (pos_weight); kind 1 = the reference's Lovasz on the FLATTENED valid
+// pixels: lovasz_hinge_loss then iterates over single pixels (model/unet_training.py:267-276), so its
+// value is the mean hinge relu(1 - z(2y-1)) with gradient -(2y-1)[e > 0].  gz gets the per-pixel
+// gradient numerator (0 on ignored pixels); part [2][G] = (loss sum, valid count) per block.
+__global__ void masked_loss_kernel(const float* out, int nch, const int64_t* tgt, int B, long P, long ignore, int kind,
+                                   const float* pos_weight, float* gz, float* part) {
+  __shared__ double sred[16];
+  const long total = (long)B * P;
+  const float pw = pos_weight ? pos_weight[0] : 1.0f;
+  double s = 0.0, n = 0.0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / P);
+    const long px = i - (long)b * P;
+    const int64_t t = tgt[i];
+    float g = 0.f;
+    if (t != ignore) {
+      const float z = load_z(out, nch, b, P, px);
+      const float y = t == 1 ? 1.f : 0.f;
+      if (kind == 0) {
+        const float lw = (pw - 1.f) * y + 1.f;
+        const float sp = log1pf(expf(-fabsf(z))) + fmaxf(-z, 0.f);
+        s += (double)((1.f - y) * z + lw * sp);
+        g = (1.f - y) - lw / (1.f + expf(z));
+      } else {
+        const float sg = 2.f * y - 1.f, e = 1.f - z * sg;
+        s += (double)fmaxf(e, 0.f);
+        g = e > 0.f ? -sg : 0.f;
+      }
+      n += 1.0;
+    }
+    gz[i] = g;
+  }
+  s = block_sum(s, sred);
+  n = block_sum(n, sred);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = (float)s;
+    part[gridDim.x + blockIdx.x] = (float)n;
+  }
+}
+
+// loss = sum / count (count 0: NaN for BCE, as a mean over nothing; 0 for the Lovasz branch, whose
+// empty loss list returns logits.sum() * 0); inv = 1 / count (0 if none)
+__global__ void masked_finalize_kernel(const float* part, int G, int kind, float* loss, float* inv) {
+  __shared__ double sred[16];
+  double s = 0.0, n = 0.0;
+  for (int i = threadIdx.x; i < G; i += blockDim.x) {
+    s += part[i];
+    n += part[G + i];
+  }
+  s = block_sum(s, sred);
+  n = block_sum(n, sred);
+  if (threadIdx.x == 0) {
+    loss[0] = n > 0.0 ? (float)(s / n) : (kind == 0 ? __builtin_nanf("") : 0.f);
+    inv[0] = n > 0.0 ? (float)(1.0 / n) : 0.f;
+  }
+}
+
+__global__ void scale_by_kernel(float* x, long n, const float* s) {
+  const float f = s[0];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) x[i] *= f;
+}
+
+// confusion counts: mode 2 -> pred = o1 > o0 (argmax, tie -> 0); mode 1 -> pred = sigmoid(o0) > 0.5;
+// pixels whose target equals `ignore` are skipped when has_ignore (utils/train_and_eval.py:125-126)
 __global__ void confusion_kernel(const float* out, int nch, const int64_t* tgt, int B, long P,
-                                 unsigned long long* conf) {
+                                 unsigned long long* conf, int has_ignore, long ignore) {
   __shared__ unsigned long long sc[4][16];
   const long total = (long)B * P;
   unsigned long long c[4] = {0, 0, 0, 0};
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    if (has_ignore && tgt[i] == ignore) continue;
     const int b = (int)(i / P);
     const long px = i - (long)b * P;
     bool pred;
@@ -507,8 +576,23 @@ UNETSEG_API size_t unetseg_lovasz_workspace(int B, long P) {
 
 // Lovasz hinge (per-image mean).  out: planar fp32 [B][nch][P] logits (nch 2 -> z = o1-o0);
 // tgt int64 [B][P] (==1 is foreground).  Writes loss[0] and gz [B][P] = dloss/dz (already /B).
+static int lovasz_impl(const float* out, int nch, const int64_t* tgt, int B, long P, int has_ignore, long ignore,
+                       void* ws, size_t ws_bytes, float* gz, float* loss, void* stream);
+
 UNETSEG_API int unetseg_lovasz_fwd(const float* out, int nch, const int64_t* tgt, int B, long P, void* ws,
                                    size_t ws_bytes, float* gz, float* loss, void* stream) {
+  return lovasz_impl(out, nch, tgt, B, P, 0, 0L, ws, ws_bytes, gz, loss, stream);
+}
+
+// per-image Lovasz over the pixels whose target is not ignore_index (lovasz_hinge_loss(..., ignore_index))
+UNETSEG_API int unetseg_lovasz_fwd_masked(const float* out, int nch, const int64_t* tgt, int B, long P,
+                                          long ignore_index, void* ws, size_t ws_bytes, float* gz, float* loss,
+                                          void* stream) {
+  return lovasz_impl(out, nch, tgt, B, P, 1, ignore_index, ws, ws_bytes, gz, loss, stream);
+}
+
+static int lovasz_impl(const float* out, int nch, const int64_t* tgt, int B, long P, int has_ignore, long ignore,
+                       void* ws, size_t ws_bytes, float* gz, float* loss, void* stream) {
   US_CHECK_ARG(out && tgt && ws && gz && loss, "lovasz_fwd: null pointer");
   US_CHECK_ARG(nch == 1 || nch == 2, "lovasz_fwd: nch must be 1 or 2");
   US_CHECK_ARG(P < 0x80000000L, "lovasz_fwd: too many pixels per image");
@@ -526,7 +610,8 @@ UNETSEG_API int unetseg_lovasz_fwd(const float* out, int nch, const int64_t* tgt
   uint32_t* hist = v1 + (long)B * P;
   uint32_t* cnt = hist + (long)B * 256 * T;
   float* part = (float*)(cnt + (long)B * T);
-  hipLaunchKernelGGL(lovasz_keygen_kernel, dim3(grid_for((long)B * P)), dim3(256), 0, st, out, nch, tgt, B, P, k0, v0);
+  hipLaunchKernelGGL(lovasz_keygen_kernel, dim3(grid_for((long)B * P)), dim3(256), 0, st, out, nch, tgt, B, P, k0, v0,
+                     has_ignore, ignore);
   for (int pass = 0; pass < 4; ++pass) {
     const int shift = pass * 8;
     hipLaunchKernelGGL(radix_hist_kernel, dim3(T, B), dim3(256), 0, st, k0, P, T, shift, hist);
@@ -573,7 +658,7 @@ UNETSEG_API int unetseg_dz_to_dout(const float* gz, int B, long P, int nch, cons
 UNETSEG_API int unetseg_confusion(const float* out, int nch, const int64_t* tgt, int B, long P, unsigned long long* conf,
                                   void* stream) {
   hipLaunchKernelGGL(confusion_kernel, dim3(grid_for((long)B * P, 2048)), dim3(256), 0, (hipStream_t)stream, out, nch,
-                     tgt, B, P, conf);
+                     tgt, B, P, conf, 0, 0L);
   US_LAUNCH_CHECK("confusion");
   return 0;
 }
@@ -659,5 +744,38 @@ UNETSEG_API int unetseg_scale_grad(const float* g, long n, const float* s1, floa
                                    float* out, void* stream) {
   hipLaunchKernelGGL(scale_grad_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, g, n, s1, a1, s2, a2, out);
   US_LAUNCH_CHECK("scale_grad");
+  return 0;
+}
+
+// confusion counts over the pixels whose target is not ignore_index
+UNETSEG_API int unetseg_confusion_masked(const float* out, int nch, const int64_t* tgt, int B, long P, long ignore_index,
+                                         unsigned long long* conf, void* stream) {
+  US_CHECK_ARG(out && tgt && conf && (nch == 1 || nch == 2), "confusion_masked: bad args");
+  hipLaunchKernelGGL(confusion_kernel, dim3(grid_for((long)B * P, 2048)), dim3(256), 0, (hipStream_t)stream, out, nch,
+                     tgt, B, P, conf, 1, ignore_index);
+  US_LAUNCH_CHECK("confusion_masked");
+  return 0;
+}
+
+UNETSEG_API size_t unetseg_masked_loss_workspace(int B, long P) {
+  return (size_t)2 * grid_for((long)B * P) * sizeof(float) + 256;
+}
+
+// binary loss over the non-ignored pixels; kind 0 BCE (pos_weight may be NULL), 1 Lovasz (flattened,
+// see masked_loss_kernel).  gz [B][P] = dloss/dz (already / count); loss fp32 scalar
+UNETSEG_API int unetseg_masked_loss_fwd(const float* out, int nch, const int64_t* tgt, int B, long P, long ignore_index,
+                                        int kind, const float* pos_weight, void* ws, size_t ws_bytes, float* gz,
+                                        float* loss, void* stream) {
+  US_CHECK_ARG(out && tgt && gz && loss && ws && (kind == 0 || kind == 1), "masked_loss_fwd: bad args");
+  US_CHECK_ARG(ws_bytes >= unetseg_masked_loss_workspace(B, P), "masked_loss_fwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int G = grid_for((long)B * P);
+  float* part = (float*)ws;
+  float* inv = part + 2 * G;
+  hipLaunchKernelGGL(masked_loss_kernel, dim3(G), dim3(256), 0, st, out, nch, tgt, B, P, ignore_index, kind, pos_weight,
+                     gz, part);
+  hipLaunchKernelGGL(masked_finalize_kernel, dim3(1), dim3(256), 0, st, part, G, kind, loss, inv);
+  hipLaunchKernelGGL(scale_by_kernel, dim3(G), dim3(256), 0, st, gz, (long)B * P, inv);
+  US_LAUNCH_CHECK("masked_loss_fwd");
   return 0;
 }

@@ -5,6 +5,7 @@ import numpy as np
 import torch
 
 from model.unet_attention import AttentionUNet
+from model.unet_dualdense import DualDenseUNet
 from model.unet_multitask import MultiTaskUNet
 from model.unet_plain import UNetPlain
 from model.unet_resnet import Unet as UNetResNet50
@@ -13,9 +14,9 @@ SUPPORTED_MODELS = {
     "unet_plain": UNetPlain,
     "unet_resnet50": UNetResNet50,
     "attention_unet": AttentionUNet,
+    "dualdense_unet": DualDenseUNet,
     "multitask_unet": MultiTaskUNet,
 }
-# ``dualdense_unet`` (model/unet_dualdense.py) is outside the hot-path scope.
 
 
 def build_model(model_name: str, num_classes: int, num_seg_classes: int = 1, num_cls_classes: int = 3):

@@ -5,7 +5,7 @@ import torch.nn as nn
 from unetseg_hip import ops
 from unetseg_hip.nn import BatchNorm2d, Conv2d, HipModel, MaxPool2d, ReLU, Seq, Sigmoid, Upsample
 
-from .unet_plain import DoubleConv, check_same_hw, run_double_conv
+from .unet_plain import DoubleConv, run_double_conv
 
 
 class AttentionGate(nn.Module):
@@ -63,9 +63,9 @@ class AttentionUNet(HipModel):
         h = xs[4]
         for up, skip in ((self.up1, xs[3]), (self.up2, xs[2]), (self.up3, xs[1]), (self.up4, xs[0])):
             u = ops.upsample2x(ctx, h, align_corners=False)
-            check_same_hw(u, skip)
             a = up.attn
             g = ops.attention_gate(ctx, skip, u, a, a.theta[0]._pc, a.phi[0]._pc)
+            u = ops.match_hw(ctx, u, skip, "interpolate")  # unet_attention.py:52-53 (odd sizes)
             h = run_double_conv(ctx, up.conv, g, x2=u)
         logits, holder = ops.pw_head(ctx, h, self.outc)
         ctx.out_holders = [holder]

@@ -49,12 +49,6 @@ class Up(nn.Module):
         raise RuntimeError("Up is part of a HIP model; call the top-level model")
 
 
-def check_same_hw(x, skip):
-    if tuple(x.data.shape[1:3]) != tuple(skip.data.shape[1:3]):
-        raise NotImplementedError("input sizes whose pyramid is not exact (pad-then-cat branch, unet_plain.py:42-45) "
-                                  "are not supported by the HIP path: use H, W divisible by 16")
-
-
 class UNetPlain(HipModel):
     """unet_plain.py:50-82"""
 
@@ -82,7 +76,7 @@ class UNetPlain(HipModel):
         h = xs[4]
         for up, skip in ((self.up1, xs[3]), (self.up2, xs[2]), (self.up3, xs[1]), (self.up4, xs[0])):
             u = ops.upsample2x(ctx, h, align_corners=False)
-            check_same_hw(u, skip)
+            u = ops.match_hw(ctx, u, skip, "pad")  # unet_plain.py:42-45 (odd sizes)
             h = run_double_conv(ctx, up.conv, skip, x2=u)
         logits, holder = ops.pw_head(ctx, h, self.outc)
         ctx.out_holders = [holder]

@@ -66,8 +66,6 @@ class Unet(HipModel):
         self._finalize()
 
     def _run(self, ctx, x):
-        if self.num_classes > 2:
-            raise NotImplementedError("HIP head supports num_classes <= 2 (binary task)")
         self._pack_weights(ctx, ctx.tape is not None)
         feats = run_resnet(ctx, self.resnet, x)
         u = run_resnet_decoder(ctx, self, feats)

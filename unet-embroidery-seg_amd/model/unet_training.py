@@ -80,19 +80,33 @@ def bce_with_logits_loss(logits, targets, pos_weight=None):
 
 
 def lovasz_hinge_loss(logits, labels, ignore_index=None, per_image=False):
-    """unet_training.py:253-280 (always the per-image mean) on the fused HIP kernel."""
-    if ignore_index is not None:
-        raise NotImplementedError("ignore_index is not on the hot path")
+    """unet_training.py:253-280 (always the per-image mean) on the fused HIP kernel; with
+    ignore_index each image's loss runs over its valid pixels only (unet_training.py:268-274).
+    A 1-D input is what binary_segmentation_loss hands over after masking (utils/train_and_eval.py:
+    172-180): the reference then loops over single pixels, i.e. a per-pixel hinge mean."""
     lg = logits
+    if lg.dim() == 1:
+        return losses._SegLossFn.apply(lg.view(1, 1, 1, -1), labels.view(1, 1, -1), "lovasz_hinge", None,
+                                       2 ** 62)  # no pixel is ignored: the masked kernel's flat path
     if lg.dim() == 2:
         lg, labels = lg.unsqueeze(0), labels.unsqueeze(0)
     if lg.dim() == 3:
         lg = lg.unsqueeze(1)
+    if ignore_index is not None:
+        return losses._SegLossFn.apply(lg, labels, "lovasz_image_masked", None, int(ignore_index))
     return losses._SegLossFn.apply(lg, labels, "lovasz_hinge", None)
 
 
-def _out_of_scope(*_a, **_k):
-    raise NotImplementedError("the multiclass task (CE/Focal/Dice) is outside the hot-path scope (SURVEY.md §2.1)")
+def CE_Loss(inputs, target, cls_weights, num_classes=21):  # noqa: N802 - reference name
+    """unet_training.py:9-24: weighted cross entropy, ignore_index = num_classes (fused HIP kernel)"""
+    return losses.ce_loss(inputs, target, cls_weights, num_classes)
 
 
-CE_Loss = Focal_Loss = Dice_loss = _out_of_scope
+def Focal_Loss(inputs, target, cls_weights, num_classes=21, alpha=0.5, gamma=2):  # noqa: N802
+    """unet_training.py:32-59: -(1-pt)^gamma * alpha * log pt over every pixel (fused HIP kernel)"""
+    return losses.focal_loss(inputs, target, cls_weights, num_classes, alpha, gamma)
+
+
+def Dice_loss(inputs, target, beta=1, smooth=1e-5):  # noqa: N802
+    """unet_training.py:67-91: 1 - mean_c F-beta score of softmax vs the one-hot target (fused HIP kernel)"""
+    return losses.dice_loss(inputs, target, beta, smooth)

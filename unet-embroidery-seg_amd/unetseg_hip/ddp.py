@@ -93,7 +93,9 @@ class GradBuckets:
     def _on_grad(self, p):
         if self._left is None:
             self._reset()
-        i = self.owner[id(p)]
+        i = self.owner.get(id(p))
+        if i is None:  # a stand-in tensor (e.g. a re-laid-out weight), not a model parameter
+            return
         self._left[i] -= 1
         if self._left[i] == 0 and not self._issued[i]:
             self._issue(i)

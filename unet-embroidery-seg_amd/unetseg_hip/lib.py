@@ -86,12 +86,30 @@ SIGNATURES = {
     "unetseg_conv2d_dgrad_config": (I, [I, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P]),
     "unetseg_conv2d_wgrad_config": (I, [I, I, I, I, I, I, I, I, I, I, I, I, I, I, P]),
     "unetseg_stem_config": (I, [I, I, I, I, P]),
+    "unetseg_pw_head_fwd": (I, [I, P, I, L, I, I, I, P, P, P, P]),
+    "unetseg_pw_head_tiles": (I, [L]),
+    "unetseg_pw_head_bwd": (I, [I, P, P, I, L, I, I, I, P, P, I, I, P, P, P]),
+    "unetseg_mc_loss_workspace": (SZ, [I, I, L]),
+    "unetseg_mc_loss_fwd": (I, [P, P, I, I, L, P, L, I, F, F, P, I, F, F, P, SZ, P, P]),
+    "unetseg_mc_loss_bwd": (I, [P, P, I, I, L, P, L, I, F, F, P, I, F, F, P, P, P, P]),
+    "unetseg_mc_confusion": (I, [P, P, I, I, L, P, P]),
+    "unetseg_softmax_resize_argmax": (I, [P, I, I, I, I, I, I, I, I, I, P, P]),
+    "unetseg_resize_bilinear_fwd": (I, [I, P, I, I, I, I, I, I, I, I, P, I, P]),
+    "unetseg_resize_bilinear_bwd": (I, [I, P, I, I, I, I, I, I, I, I, P, I, I, P]),
+    "unetseg_pad2d_fwd": (I, [I, P, I, I, I, I, I, I, I, I, I, P, I, P]),
+    "unetseg_pad2d_bwd": (I, [I, P, I, I, I, I, I, I, I, I, I, P, I, I, P]),
+    "unetseg_confusion_masked": (I, [P, I, P, I, L, L, P, P]),
+    "unetseg_masked_loss_workspace": (SZ, [I, L]),
+    "unetseg_masked_loss_fwd": (I, [P, I, P, I, L, L, I, P, P, SZ, P, P, P]),
+    "unetseg_lovasz_fwd_masked": (I, [P, I, P, I, L, L, P, SZ, P, P, P]),
+    "unetseg_channel_stats_tiles": (I, [L, I]),
+    "unetseg_channel_stats": (I, [I, P, I, L, I, I, P, P]),
 }
 
 #: functions returning a value rather than a status (no RuntimeError on non-zero)
 VALUE_FUNCS = {"reduce_tiles", "pw_small_tiles", "conv_tile_m", "abi_version", "conv2d_fwd_tile_m",
                "conv2d_dgrad_post", "stem_fwd_tile_m", "attn_bwd1_tiles", "pw_small_tile", "conv2d_fwd_config",
-               "conv2d_dgrad_config", "conv2d_wgrad_config", "stem_config"}
+               "conv2d_dgrad_config", "conv2d_wgrad_config", "stem_config", "pw_head_tiles", "channel_stats_tiles"}
 
 _lib = None
 

@@ -26,15 +26,32 @@ def _prep(outputs, targets):
     return out, tgt
 
 
-def _seg_forward(kind, out, nch, tgt, B, Pn, pos_weight, need_grad):
+def _seg_forward(kind, out, nch, tgt, B, Pn, pos_weight, need_grad, ignore_index=None):
     dev = out.device
     st = _stream(dev)
     loss = torch.empty((), dtype=torch.float32, device=dev)
-    gz = torch.empty((B, Pn), dtype=torch.float32, device=dev) if (need_grad or kind == "lovasz_hinge") else None
-    if kind == "lovasz_hinge":
+    gz = (torch.empty((B, Pn), dtype=torch.float32, device=dev)
+          if (need_grad or kind in ("lovasz_hinge", "lovasz_image_masked")) else None)
+    if ignore_index is not None and kind != "lovasz_image_masked":
+        if kind not in ("bce", "lovasz_hinge"):
+            raise ValueError(f"Unsupported loss_name: {kind}")
+        if gz is None:
+            gz = torch.empty((B, Pn), dtype=torch.float32, device=dev)
+        pw = None
+        if pos_weight is not None and kind == "bce":
+            pw = torch.as_tensor(pos_weight, dtype=torch.float32, device=dev).reshape(-1)[:1].contiguous()
+        nb = lib.masked_loss_workspace(B, Pn)
+        ws = workspace(nb, dev)
+        lib.masked_loss_fwd(P(out), nch, P(tgt), B, Pn, int(ignore_index), 0 if kind == "bce" else 1, P(pw), P(ws),
+                            ws.numel(), P(gz), P(loss), st)
+    elif kind == "lovasz_hinge":
         nb = lib.lovasz_workspace(B, Pn)
         ws = workspace(nb, dev)
         lib.lovasz_fwd(P(out), nch, P(tgt), B, Pn, P(ws), ws.numel(), P(gz), P(loss), st)
+    elif kind == "lovasz_image_masked":  # lovasz_hinge_loss(..., ignore_index): per image, valid pixels
+        nb = lib.lovasz_workspace(B, Pn)
+        ws = workspace(nb, dev)
+        lib.lovasz_fwd_masked(P(out), nch, P(tgt), B, Pn, int(ignore_index), P(ws), ws.numel(), P(gz), P(loss), st)
     elif kind == "bce":
         pw = None
         if pos_weight is not None:
@@ -49,11 +66,11 @@ def _seg_forward(kind, out, nch, tgt, B, Pn, pos_weight, need_grad):
 
 class _SegLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(fctx, outputs, targets, kind, pos_weight):
+    def forward(fctx, outputs, targets, kind, pos_weight, ignore_index=None):
         out, tgt = _prep(outputs, targets)
         B, nch = out.shape[0], out.shape[1]
         Pn = out[0, 0].numel()
-        loss, gz = _seg_forward(kind, out, nch, tgt, B, Pn, pos_weight, outputs.requires_grad)
+        loss, gz = _seg_forward(kind, out, nch, tgt, B, Pn, pos_weight, outputs.requires_grad, ignore_index)
         fctx.save_for_backward(gz)
         fctx.meta = (B, nch, Pn, outputs.shape, outputs.dtype)
         return loss
@@ -66,18 +83,17 @@ class _SegLossFn(torch.autograd.Function):
         dout = torch.empty(shape, dtype=torch.float32, device=gz.device)
         scratch = torch.empty_like(gz)
         lib.dz_to_dout(P(gz), B, Pn, nch, P(g), 1.0, 0, 0.0, P(scratch), P(dout), _stream(gz.device))
-        return dout.to(dtype), None, None, None
+        return dout.to(dtype), None, None, None, None
 
 
 def binary_segmentation_loss(outputs, targets, loss_name, pos_weight=None, ignore_index=None):
-    """utils/train_and_eval.py:155-182 on the HIP path (ignore_index must be None)."""
+    """utils/train_and_eval.py:155-182 on the HIP path.  With ignore_index the valid pixels are
+    flattened across the batch (BCE: their mean; Lovasz: see unetseg_masked_loss_fwd)."""
     if outputs.dim() != 4 or outputs.size(1) != 2:
         raise ValueError(f"Expected output shape (N,2,H,W), got {tuple(outputs.shape)}")
-    if ignore_index is not None:
-        raise NotImplementedError("ignore_index is not on the hot path (train.py always passes None)")
     if loss_name not in ("bce", "lovasz_hinge"):
         raise ValueError(f"Unsupported loss_name: {loss_name}")
-    return _SegLossFn.apply(outputs, targets, loss_name, pos_weight)
+    return _SegLossFn.apply(outputs, targets, loss_name, pos_weight, ignore_index)
 
 
 def seg_loss_1ch(logits, targets, kind):
@@ -134,13 +150,144 @@ def multitask_loss(seg_logits, cls_logits, seg_targets, cls_targets, cls_loss_we
     return _MultiTaskFn.apply(seg_logits, cls_logits, seg_targets, cls_targets, cls_loss_weight, kind)
 
 
-def binary_confusion(outputs, targets, conf=None):
+def binary_confusion(outputs, targets, conf=None, ignore_index=None):
     """device uint64[4] (+)= (tp, fp, fn, tn).  outputs [B,2,H,W] (argmax, tie -> 0) or [B,1,H,W]
-    (sigmoid > 0.5).  No host sync: callers read the counters once per split."""
+    (sigmoid > 0.5); pixels whose target is ignore_index are skipped.  No host sync: callers read
+    the counters once per split."""
     out, tgt = _prep(outputs, targets)
     B, nch = out.shape[0], out.shape[1]
     Pn = out[0, 0].numel()
     if conf is None:
         conf = torch.zeros(4, dtype=torch.int64, device=out.device)
-    lib.confusion(P(out), nch, P(tgt), B, Pn, P(conf), _stream(out.device))
+    if ignore_index is None:
+        lib.confusion(P(out), nch, P(tgt), B, Pn, P(conf), _stream(out.device))
+    else:
+        lib.confusion_masked(P(out), nch, P(tgt), B, Pn, int(ignore_index), P(conf), _stream(out.device))
     return conf
+
+
+# ------------------------------------------------------------------------------------------------
+# multiclass task (model/unet_training.py:9-91, utils/train_and_eval.py:20-103)
+# ------------------------------------------------------------------------------------------------
+MC_CE, MC_FOCAL, MC_NONE = 0, 1, 2
+
+
+class _McLossFn(torch.autograd.Function):
+    """One fused kernel pair (unetseg_mc_loss_fwd / _bwd): CE or Focal over argmax targets and/or
+    Dice over a one-hot target, on fp32 planar logits [B][C][H][W]."""
+
+    @staticmethod
+    def forward(fctx, outputs, target, cls_w, kind, alpha, gamma, dice_t, beta, smooth, ignore_index):
+        if not outputs.is_cuda:
+            raise RuntimeError("HIP losses need device tensors")
+        out = outputs.detach().float().contiguous()
+        B, C = out.shape[0], out.shape[1]
+        Pn = out[0, 0].numel()
+        dev = out.device
+        tgt = target.detach().to(device=dev, dtype=torch.int64).contiguous() if target is not None else None
+        w = cls_w.detach().to(device=dev, dtype=torch.float32).contiguous() if cls_w is not None else None
+        dt = dice_t.detach().to(device=dev, dtype=torch.float32).contiguous() if dice_t is not None else None
+        ct = dt.shape[-1] if dt is not None else 0
+        nb = lib.mc_loss_workspace(B, C, Pn)
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+        loss = torch.empty(3, dtype=torch.float32, device=dev)
+        args = (P(out), P(tgt), B, C, Pn, P(w), int(ignore_index), int(kind), float(alpha), float(gamma), P(dt), ct,
+                float(beta), float(smooth))
+        lib.mc_loss_fwd(*args, P(ws), nb, P(loss), _stream(dev))
+        fctx.keep = (out, tgt, w, dt, ws, args, outputs.shape, outputs.dtype)
+        return loss[0]
+
+    @staticmethod
+    def backward(fctx, g):
+        out, tgt, w, dt, ws, args, shape, dtype = fctx.keep
+        g = g.detach().float().reshape(1).contiguous()
+        dout = torch.empty(shape, dtype=torch.float32, device=out.device)
+        lib.mc_loss_bwd(*args, P(ws), P(g), P(dout), _stream(out.device))
+        fctx.keep = None
+        return dout.to(dtype), None, None, None, None, None, None, None, None, None
+
+
+def _check_mc(inputs, target_hw):
+    n, c, h, w = inputs.size()
+    ht, wt = target_hw
+    if h != ht and w != wt:
+        # the reference interpolates the logits (align_corners=True) to the label size first
+        inputs = _ResizeLogitsFn.apply(inputs, int(ht), int(wt), True)
+    return inputs
+
+
+class _ResizeLogitsFn(torch.autograd.Function):
+    """F.interpolate(bilinear) of fp32 planar logits [N][C][H][W] on the HIP resize kernels (the
+    planes are N*C single-channel NHWC images)"""
+
+    @staticmethod
+    def forward(fctx, x, oh, ow, align):
+        from .lib import DT_F32
+        xc = x.detach().float().contiguous()
+        N, C, H, W = xc.shape
+        y = torch.empty((N, C, oh, ow), dtype=torch.float32, device=xc.device)
+        lib.resize_bilinear_fwd(DT_F32, P(xc), 1, N * C, H, W, 1, oh, ow, int(align), P(y), 1, _stream(xc.device))
+        fctx.meta = (N, C, H, W, oh, ow, align)
+        return y
+
+    @staticmethod
+    def backward(fctx, g):
+        from .lib import DT_F32
+        N, C, H, W, oh, ow, align = fctx.meta
+        gc = g.detach().float().contiguous()
+        dx = torch.empty((N, C, H, W), dtype=torch.float32, device=gc.device)
+        lib.resize_bilinear_bwd(DT_F32, P(gc), 1, N * C, H, W, 1, oh, ow, int(align), P(dx), 1, 0, _stream(gc.device))
+        return dx, None, None, None
+
+
+def ce_loss(inputs, target, cls_weights, num_classes=21):
+    """CE_Loss (model/unet_training.py:9-24): weighted mean cross entropy, ignore_index=num_classes"""
+    inputs = _check_mc(inputs, target.shape[-2:])
+    return _McLossFn.apply(inputs, target, cls_weights, MC_CE, -1.0, 0.0, None, 1.0, 0.0, num_classes)
+
+
+def focal_loss(inputs, target, cls_weights, num_classes=21, alpha=0.5, gamma=2):
+    """Focal_Loss (model/unet_training.py:32-59): -(1-pt)^gamma * alpha * log pt, mean over all pixels"""
+    inputs = _check_mc(inputs, target.shape[-2:])
+    return _McLossFn.apply(inputs, target, cls_weights, MC_FOCAL, -1.0 if alpha is None else alpha, gamma, None, 1.0,
+                           0.0, num_classes)
+
+
+def dice_loss(inputs, target, beta=1, smooth=1e-5):
+    """Dice_loss (model/unet_training.py:67-91) on a one-hot target [N,H,W,ct] (first C channels)"""
+    inputs = _check_mc(inputs, target.shape[1:3])
+    return _McLossFn.apply(inputs, None, None, MC_NONE, -1.0, 0.0, target, beta, smooth, -1)
+
+
+def mc_confusion(outputs, target, hist=None):
+    """device u64 [(C+1), C] (+)= (target class, argmax class); targets outside [0, C) -> row C"""
+    out = outputs.detach().float().contiguous()
+    B, C = out.shape[0], out.shape[1]
+    tgt = target.detach().to(device=out.device, dtype=torch.int64).contiguous()
+    if hist is None:
+        hist = torch.zeros(C + 1, C, dtype=torch.int64, device=out.device)
+    lib.mc_confusion(P(out), P(tgt), B, C, out[0, 0].numel(), P(hist), _stream(out.device))
+    return hist
+
+
+def mc_metrics_from_hist(hist):
+    """pixel_accuracy / mean_accuracy / mean_iou / frequency_weighted_iou of utils/train_and_eval.py:20-103
+    from one batch's histogram (host, float64; classes absent from the target are skipped as there)"""
+    import numpy as np
+    h = np.asarray(hist, dtype=np.float64)
+    C = h.shape[1]
+    total = h.sum()
+    inter = np.array([h[i, i] for i in range(C)])
+    tcount = h[:C].sum(1)
+    pcount = h.sum(0)
+    union = tcount + pcount - inter
+    pixel_acc = float(inter.sum() / total) if total > 0 else 0.0
+    present = tcount > 0
+    accs = [inter[i] / tcount[i] for i in range(C) if present[i]]
+    mean_acc = float(sum(accs) / len(accs)) if accs else 0.0
+    ious = [(inter[i] / union[i]) if union[i] > 0 else 0.0 for i in range(C) if present[i]]
+    miou = float(sum(ious) / len(ious)) if ious else 0.0
+    iou_all = [(inter[i] / union[i]) if union[i] > 0 else 0.0 for i in range(C)]
+    ft = tcount.sum()
+    fw = float(sum(f * i for f, i in zip(tcount, iou_all)) / ft) if ft > 0 else 0.0
+    return {"Pixel Accuracy": pixel_acc, "Mean Accuracy": mean_acc, "Mean IoU": miou, "Frequency Weighted IoU": fw}

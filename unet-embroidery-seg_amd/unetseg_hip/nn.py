@@ -248,7 +248,10 @@ class HipModel(nn.Module):
             return
         if getattr(self, "_pack_table", None) is None:
             self._pack_table = ops.PackTable()
-        self._pack_table.run(ctx, self._packed, [need_t and pc.conv.in_channels >= 8 for pc in self._packed])
+        # convs on the (padded) image need no data gradient -- unless an input op with parameters
+        # sits in front of them (dualdense's BN-ReLU on the image: force_t)
+        self._pack_table.run(ctx, self._packed, [need_t and (pc.conv.in_channels >= 8 or getattr(pc, "force_t", False))
+                                                 for pc in self._packed])
 
     def forward(self, x):
         if not x.is_cuda:

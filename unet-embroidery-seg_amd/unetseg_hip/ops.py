@@ -150,6 +150,8 @@ class Ctx:
                 self.side = None
 
     def param_done(self, *params):
+        """report parameters whose gradient is final (DDP bucketing; stand-in tensors that are not
+        model parameters, e.g. a re-laid-out weight, are ignored by the hook)"""
         if self.grad_hook is not None:
             for p in params:
                 if p is not None:
@@ -194,10 +196,12 @@ class PackedConv:
         K, C, R, S = self.K, self.C, self.R, self.S
         if self.wk is None or self.dt != ctx.dt or self.wk.device != ctx.device:
             self.wk = ctx.empty(K, R, S, self.cpad)
-            self.wt = ctx.empty(C, R, S, K) if need_t else None
+            self.wt = None
             self.dt = ctx.dt
         if need_t and self.wt is None:
-            self.wt = ctx.empty(C, R, S, K)
+            # [Cpad][R][S][K]: the padded input channels' rows stay zero (the pack writes C rows), so a
+            # data gradient over all Cpad channels of a padded input is well defined
+            self.wt = torch.zeros((self.cpad, R, S, K), dtype=ctx.tdtype, device=ctx.device)
 
     def pack(self, ctx, need_t):
         K, C, R, S = self.K, self.C, self.R, self.S
@@ -256,9 +260,10 @@ def pack_input(ctx, x, cpad=8):
 PAD_K = os.environ.get("UNETSEG_NO_PADK", "0") != "1"
 
 
-def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
+def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None):
     """y = conv(cat[x1, x2]) (+bias if the conv has one, ReLU).  Stride/padding come from the
-    Conv2d container.  Returns (Node y, BN partials or None)."""
+    Conv2d container.  out: an NHWC view (pixel stride >= K) to write y into, e.g. a channel slice
+    of a dense block's concatenation buffer.  Returns (Node y, BN partials or None)."""
     stride, pad = pc.conv.stride, pc.conv.padding
     use(x1, x2)
     X1 = x1.data
@@ -269,7 +274,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
     Pq = (H + 2 * pad - R) // stride + 1
     Qq = (W + 2 * pad - S) // stride + 1
     M = N * Pq * Qq
-    y = ctx.empty(N, Pq, Qq, K)
+    y = ctx.empty(N, Pq, Qq, K) if out is None else out
     st = None
     if stats:
         tile = lib.conv2d_fwd_tile_m(ctx.dt, C1, ldp(X1), C2, ldp(X2), N, H, W, K, R, S, stride, pad)
@@ -281,7 +286,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
     desc = (N, H, W, C1, C2, K, R, S, stride, pad, ldp(X1), ldp(X2))
     with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
         lib.conv2d_fwd(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride, pad,
-                       P(b), int(relu), P(y), K, P(st[0] if st else None), ctx.stream)
+                       P(b), int(relu), P(y), ldp(y), P(st[0] if st else None), ctx.stream)
     out = Node(y)
     if relu:
         out.fuse = (1, y, None)
@@ -301,7 +306,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False):
             Gr = lib.reduce_tiles(ctx.dt, M, K, None, None)
             part = ctx.f32(K, Gr)
             dY = ctx.empty(N, Pq, Qq, K)
-            lib.relu_bwd_bias(ctx.dt, P(dA), ldp(dA), P(y), K, P(dY), K, M, K, P(part), Gr, ctx.stream)
+            lib.relu_bwd_bias(ctx.dt, P(dA), ldp(dA), P(y), ldp(y), P(dY), K, M, K, P(part), Gr, ctx.stream)
             if b is not None:
                 lib.colsum_finalize(P(part), K, Gr, P(b.grad), 1, ctx.stream)
         else:
@@ -605,16 +610,77 @@ def upsample2x(ctx, x, align_corners):
     return out
 
 
+def resize_bilinear(ctx, x, oh, ow, align_corners):
+    """F.interpolate(x, size=(oh, ow), mode="bilinear") for sizes that are not an exact x2
+    (model/unet_attention.py:31-33,52-53, model/unet_dualdense.py:57-58)"""
+    use(x)
+    X = x.data
+    N, H, W, C = X.shape
+    y = ctx.empty(N, oh, ow, C)
+    lib.resize_bilinear_fwd(ctx.dt, P(X), ldp(X), N, H, W, C, oh, ow, int(align_corners), P(y), C, ctx.stream)
+    out = Node(y)
+
+    def bwd():
+        if out.grad is None or not x.need_grad:
+            return
+        g, acc = gbuf(ctx, x)
+        lib.resize_bilinear_bwd(ctx.dt, P(out.grad), ldp(out.grad), N, H, W, C, oh, ow, int(align_corners), P(g),
+                                ldp(g), acc, ctx.stream)
+
+    ctx.push(bwd)
+    return out
+
+
+def pad2d(ctx, x, top, left, oh, ow):
+    """F.pad(x, [left, right, top, bottom]) with zeros (model/unet_plain.py:42-45)"""
+    use(x)
+    X = x.data
+    N, H, W, C = X.shape
+    y = ctx.empty(N, oh, ow, C)
+    lib.pad2d_fwd(ctx.dt, P(X), ldp(X), N, H, W, C, top, left, oh, ow, P(y), C, ctx.stream)
+    out = Node(y)
+
+    def bwd():
+        if out.grad is None or not x.need_grad:
+            return
+        g, acc = gbuf(ctx, x)
+        lib.pad2d_bwd(ctx.dt, P(out.grad), ldp(out.grad), N, H, W, C, top, left, oh, ow, P(g), ldp(g), acc,
+                      ctx.stream)
+
+    ctx.push(bwd)
+    return out
+
+
+def match_hw(ctx, x, skip, mode):
+    """x resized ("interpolate", align_corners=False) or zero-padded ("pad", centred as the
+    reference's F.pad) to skip's spatial size; x itself when the sizes already agree"""
+    h, w = x.data.shape[1:3]
+    sh, sw = skip.data.shape[1:3]
+    if (h, w) == (sh, sw):
+        return x
+    if mode == "pad":
+        dh, dw = sh - h, sw - w
+        if dh < 0 or dw < 0:
+            raise RuntimeError(f"pad-then-cat needs the upsampled map ({h}x{w}) no larger than the skip ({sh}x{sw})")
+        return pad2d(ctx, x, dh // 2, dw // 2, sh, sw)
+    return resize_bilinear(ctx, x, sh, sw, False)
+
+
 def pw_head(ctx, x, conv_mod):
-    """1x1 conv with Cout in {1,2} -> fp32 NCHW logits (the reference's output layout)"""
+    """1x1 conv head -> fp32 NCHW logits (the reference's output layout): Cout in {1, 2} on the
+    vectorised pw_small kernels (binary / multitask heads), 3..32 classes (the multiclass task's
+    outc / final, model/unet_resnet.py:78, model/unet_plain.py:69) on pw_head"""
     use(x)
     X = x.data
     N, H, W, C = X.shape
     K = conv_mod.weight.shape[0]
     M = N * H * W
     y = torch.empty((N, K, H, W), dtype=torch.float32, device=ctx.device)
-    lib.pw_small_fwd(ctx.dt, P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(conv_mod.bias), P(y), 0,
-                     ctx.stream)
+    if K > 2:
+        lib.pw_head_fwd(ctx.dt, P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(conv_mod.bias), P(y), ctx.stream)
+    else:
+        lib.pw_small_fwd(ctx.dt, P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(conv_mod.bias), P(y), 0,
+                         ctx.stream)
     holder = {}
 
     def bwd():
@@ -622,6 +688,16 @@ def pw_head(ctx, x, conv_mod):
         if dy is None:
             return
         dy = dy.contiguous().float()
+        if K > 2:
+            G = lib.pw_head_tiles(M)
+            pw, pb = ctx.f32(K, C, G), ctx.f32(K, G)
+            dx, acc = (gbuf(ctx, x) if x.need_grad else (None, 0))
+            lib.pw_head_bwd(ctx.dt, P(dy), P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(dx), ldp(dx), acc,
+                            P(pw), P(pb), ctx.stream)
+            lib.colsum_finalize(P(pw), K * C, G, P(conv_mod.weight.grad), 1, ctx.stream)
+            lib.colsum_finalize(P(pb), K, G, P(conv_mod.bias.grad), 1, ctx.stream)
+            ctx.param_done(conv_mod.weight, conv_mod.bias)
+            return
         G = lib.pw_small_tiles(M)
         pw, pb = ctx.f32(K, C, G), ctx.f32(K, G)
         if (FUSE and x.need_grad and x.fuse is not None and x.fuse[0] == 1 and x.fuse[1] is X
@@ -648,7 +724,9 @@ def pw_head(ctx, x, conv_mod):
 
 def attention_gate(ctx, skip, gate, gm, pth, pph):
     """model/unet_attention.py:30-35.  gm: AttentionGate container; pth/pph: packed theta/phi convs.
-    Returns the gated skip Node (skip * alpha)."""
+    Returns the gated skip Node (skip * alpha).  A gate of another size is first resized to the
+    skip's (bilinear, align_corners=False, unet_attention.py:31-33)."""
+    gate = match_hw(ctx, gate, skip, "interpolate")
     use(skip)  # read again by attn_apply
     th, st_t = conv(ctx, skip, pth, stats=True)
     ph, st_p = conv(ctx, gate, pph, stats=True)
@@ -735,3 +813,109 @@ def cls_head(ctx, feat, head, dropout_mask=None, seed=0):
 
     ctx.push(bwd)
     return y, holder, mask
+
+
+# ------------------------------------------------------------------------------------------------
+# dense blocks (model/unet_dualdense.py): concatenation buffer, BN-ReLU over its channel prefix
+# ------------------------------------------------------------------------------------------------
+def copy_into(ctx, src, block, c0):
+    """block.data[..., c0:c0+C] = src.data (the block buffer starts zeroed); backward hands the
+    matching channel slice of block.grad to src"""
+    use(src)
+    S_ = src.data
+    N, H, W, C = S_.shape
+    B_ = block.data
+    lib.add(ctx.dt, P(S_), ldp(S_), P(B_[..., c0:]), ldp(B_), N * H * W, C, ctx.stream)
+
+    def bwd():
+        if block.grad is None or not src.need_grad:
+            return
+        give_grad(ctx, src, block.grad[..., c0:c0 + C])
+
+    ctx.push(bwd)
+
+
+def link_grad(ctx, node, block, c0):
+    """at backward time, node.grad := the channel slice of block.grad that node's data occupies
+    (node was written into the block buffer by its producer)"""
+    C = node.data.shape[-1]
+
+    def bwd():
+        if block.grad is not None:
+            node.grad = block.grad[..., c0:c0 + C]
+
+    ctx.push(bwd)
+
+
+STATS_TILE = 256
+
+
+def bn_relu_prefix(ctx, block, width, bnm, idx=None):
+    """a = ReLU(BN(block.data[..., :width])) (model/unet_dualdense.py:9-11: BatchNorm2d + ReLU over the
+    dense concatenation) -> new contiguous Node.  idx (LongTensor, device): physical channel of each of
+    the BN's logical channels when the buffer holds padding channels (the 3-channel image padded to
+    8); padding channels get gamma = beta = 0, i.e. output 0.  Backward adds into block.grad."""
+    use(block)
+    Y = block.data[..., :width]
+    N, H, W, _ = Y.shape
+    M = N * H * W
+    C = width
+    dev = ctx.device
+    if idx is None:
+        g, b, rm, rv = bnm.weight, bnm.bias, bnm.running_mean, bnm.running_var
+    else:
+        def phys(v):
+            t = torch.zeros(C, dtype=torch.float32, device=dev)
+            return t.index_copy_(0, idx, v.detach())
+        g, b, rm, rv = phys(bnm.weight), phys(bnm.bias), phys(bnm.running_mean), phys(bnm.running_var)
+    s = BNState()
+    s.sc, s.sh = ctx.f32(C), ctx.f32(C)
+    if ctx.training:
+        G = lib.channel_stats_tiles(M, STATS_TILE)
+        part = ctx.f32(G, 2, C)
+        lib.channel_stats(ctx.dt, P(Y), ldp(Y), M, C, STATS_TILE, P(part), ctx.stream)
+        s.mean, s.inv = ctx.f32(C), ctx.f32(C)
+        lib.bn_finalize(P(part), C, G, M, STATS_TILE, P(g), P(b), P(rm), P(rv), P(bnm.num_batches_tracked),
+                        bnm.momentum, bnm.eps, P(s.mean), P(s.inv), P(s.sc), P(s.sh), ctx.stream)
+        if idx is not None:
+            with torch.no_grad():
+                bnm.running_mean.copy_(rm.index_select(0, idx))
+                bnm.running_var.copy_(rv.index_select(0, idx))
+    else:
+        s.mean = s.inv = None
+        lib.bn_eval_coeffs(C, P(g), P(b), P(rm), P(rv), bnm.eps, P(s.sc), P(s.sh), ctx.stream)
+    a = ctx.empty(N, H, W, C)
+    lib.bn_apply(ctx.dt, P(Y), ldp(Y), P(s.sc), P(s.sh), 0, 0, 0, 0, 0, 1, P(a), C, M, C, ctx.stream)
+    out = Node(a)
+
+    def bwd():
+        dA = out.grad
+        if dA is None:
+            return
+        if not ctx.training:
+            raise NotImplementedError("backward through eval-mode BatchNorm is not on the hot path")
+        Gr = lib.reduce_tiles(ctx.dt, M, C, None, None)
+        part = ctx.f32(3, C, Gr)
+        lib.bn_bwd_reduce(ctx.dt, P(dA), ldp(dA), 0, C, P(s.sc), P(s.sh), P(Y), ldp(Y), P(s.mean), P(s.inv), 0, 0,
+                          0, 0, M, C, P(part), Gr, ctx.stream)
+        coef = ctx.f32(6, C)
+        dg, db = (bnm.weight.grad, bnm.bias.grad) if idx is None else (ctx.f32(C), ctx.f32(C))
+        if idx is not None:
+            dg.zero_()
+            db.zero_()
+        lib.bn_bwd_finalize(P(part), C, Gr, M, 1, P(g), P(s.inv), P(dg), P(db), 0, 0, 0, 0, P(coef), ctx.stream)
+        if idx is not None:
+            with torch.no_grad():
+                bnm.weight.grad.add_(dg.index_select(0, idx))
+                bnm.bias.grad.add_(db.index_select(0, idx))
+        ctx.param_done(bnm.weight, bnm.bias)
+        dy = ctx.empty(N, H, W, C)
+        lib.bn_bwd_apply(ctx.dt, P(dA), ldp(dA), 0, C, P(s.sc), P(s.sh), P(Y), ldp(Y), P(s.mean), P(s.inv),
+                         P(dy), C, 0, 0, 0, 0, 0, 0, P(coef), 0, 0, 0, M, C, ctx.stream)
+        if block.grad is None:
+            block.grad = torch.zeros_like(block.data)
+        G_ = block.grad
+        lib.add(ctx.dt, P(dy), C, P(G_), ldp(G_), M, C, ctx.stream)
+
+    ctx.push(bwd)
+    return out

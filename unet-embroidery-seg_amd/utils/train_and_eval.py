@@ -109,7 +109,7 @@ def evaluate_binary(model, val_loader, device, loss_name: str, pos_weight, ignor
             outputs = model_eval(imgs)
             loss = binary_segmentation_loss(outputs, pngs, loss_name, pos_weight, ignore_index)
             total_loss += loss
-            losses.binary_confusion(outputs, pngs, conf)
+            losses.binary_confusion(outputs, pngs, conf, ignore_index)
             seen_batches += 1
             if max_batches is not None and seen_batches >= max_batches:
                 break
@@ -182,8 +182,99 @@ def evaluate_multitask(model, loader, device, criterion, max_batches=None):
             "Dice": 2 * tp / ((tp + fp) + (tp + fn) + 1e-6), "Cls Acc": 100.0 * float(correct.item()) / max(total, 1)}
 
 
-def _out_of_scope(*_a, **_k):
-    raise NotImplementedError("the multiclass task is outside the hot-path scope (SURVEY.md §2.1)")
+# ------------------------------------------------------------------------------------------------
+# multiclass task (train_and_eval.py:20-103, 308-513): metrics from one fused confusion histogram
+# per batch (device, u64), losses on the fused CE / Focal / Dice kernels
+# ------------------------------------------------------------------------------------------------
+def _mc_hist(output, target):
+    return losses.mc_confusion(output, target).cpu().numpy()
 
 
-train_one_epoch = evaluate = pixel_accuracy = mean_accuracy = mean_iou = frequency_weighted_iou = _out_of_scope
+def pixel_accuracy(output, target):
+    """train_and_eval.py:20-26 (correct / all pixels)"""
+    return losses.mc_metrics_from_hist(_mc_hist(output, target))["Pixel Accuracy"]
+
+
+def mean_accuracy(output, target, num_classes):
+    """train_and_eval.py:28-59 (classes present in the target)"""
+    return losses.mc_metrics_from_hist(_mc_hist(output, target))["Mean Accuracy"]
+
+
+def mean_iou(output, target, num_classes):
+    """train_and_eval.py:63-81 (classes present in the target)"""
+    return losses.mc_metrics_from_hist(_mc_hist(output, target))["Mean IoU"]
+
+
+def frequency_weighted_iou(output, target, num_classes):
+    """train_and_eval.py:85-103"""
+    return losses.mc_metrics_from_hist(_mc_hist(output, target))["Frequency Weighted IoU"]
+
+
+def _mc_loss(outputs, pngs, labels, weights, num_classes, dice_loss, focal_loss):
+    from model.unet_training import CE_Loss, Dice_loss, Focal_Loss
+    if focal_loss:
+        loss = Focal_Loss(outputs, pngs, weights, num_classes=num_classes)
+    else:
+        loss = CE_Loss(outputs, pngs, weights, num_classes=num_classes)
+    if dice_loss:
+        loss = loss + Dice_loss(outputs, labels)
+    return loss
+
+
+def train_one_epoch(model, optimizer, train_loader, device, dice_loss, focal_loss, gpu_used, num_classes, scaler,
+                    epoch, train_epoch):
+    """train_and_eval.py:308-409: CE or Focal (+ Dice) with unit class weights; returns the mean loss"""
+    import numpy as np
+    cls_weights = np.ones([num_classes], np.float32)
+    epoch_loss = torch.zeros((), dtype=torch.float64, device=device)
+    model_train = model.train().to(device)
+    weights = torch.tensor(cls_weights).to(device)
+    n_batches = len(train_loader)
+    for iteration, batch in enumerate(train_loader):
+        imgs, pngs, labels = batch[0].to(device), batch[1].to(device), batch[2].to(device)
+        optimizer.zero_grad()
+        if scaler is None:
+            outputs = model_train(imgs)
+            loss = _mc_loss(outputs, pngs, labels, weights, num_classes, dice_loss, focal_loss)
+            loss.backward()
+            optimizer.step()
+        else:
+            with autocast(device_type=device.type, enabled=True):
+                outputs = model_train(imgs)
+                loss = _mc_loss(outputs, pngs, labels, weights, num_classes, dice_loss, focal_loss)
+            scaler.scale(loss).backward()
+            scaler.step(optimizer)
+            scaler.update()
+        epoch_loss += loss.detach().double()
+        if iteration == 0:
+            print(f"{LogColor.GREEN}Epoch{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}data_num{LogColor.RESET}{' ' * 12}"
+                  f"{LogColor.YELLOW}GPU Mem{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}Loss{LogColor.RESET}{' ' * 12}"
+                  f"{LogColor.YELLOW}LR{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}Image_size{LogColor.RESET}{' ' * 12}")
+        print(f"\r{epoch + 1}/{train_epoch}    {iteration + 1}/{n_batches}    {gpu_used:.2f} MB    "
+              f"{get_lr(optimizer):.8f}    {imgs.shape[2]}", end="", flush=True)
+    print(f"{LogColor.GREEN}")
+    return float(epoch_loss.item()) / max(n_batches, 1)
+
+
+def evaluate(model, val_loader, device, dice_loss, focal_loss, num_classes):
+    """train_and_eval.py:411-513: per-batch metrics averaged over batches, as the reference does"""
+    import numpy as np
+    weights = torch.tensor(np.ones([num_classes], np.float32)).to(device)
+    model_eval = model.eval().to(device)
+    hists, loss_sum = [], torch.zeros((), dtype=torch.float64, device=device)
+    with torch.no_grad():
+        for batch in val_loader:
+            imgs, pngs, labels = batch[0].to(device), batch[1].to(device), batch[2].to(device)
+            outputs = model_eval(imgs)
+            loss_sum += _mc_loss(outputs, pngs, labels, weights, num_classes, dice_loss, focal_loss).double()
+            hists.append(losses.mc_confusion(outputs, pngs))
+    n = max(len(val_loader), 1)
+    keys = ("Pixel Accuracy", "Mean Accuracy", "Mean IoU", "Frequency Weighted IoU")
+    tot = dict.fromkeys(keys, 0.0)
+    for h in hists:  # one device->host copy per batch histogram, after the loop
+        m = losses.mc_metrics_from_hist(h.cpu().numpy())
+        for k in keys:
+            tot[k] += m[k]
+    metrics = {k: tot[k] / n for k in keys}
+    metrics["Loss"] = float(loss_sum.item()) / n
+    return metrics
