@@ -279,6 +279,21 @@ int unetseg_mc_confusion(const float* out, const int64_t* tgt, int B, int C, lon
 int unetseg_softmax_resize_argmax(const float* logits, int C, int H, int W, int y0, int x0, int ch, int cw, int OH,
                                   int OW, int32_t* labels, void* stream);
 
+/* ---- device augmentation of the loader (utils/hf_dataloader.py:67-105, 111-180, 183-213) -------
+ * Replaces HFUnetDataset.get_random_data + preprocess + hf_unet_dataset_collate for one batch:
+ * PIL BICUBIC image / NEAREST mask resize (bit-exact), flip, paste on the grey / zero canvas,
+ * OpenCV-style HSV jitter (hsv flag), /255, label binarise / clamp, one-hot.
+ * desc: int64 [B][20] per-sample descriptors (host copy for validation + device copy), tables:
+ * int32 per-sample resize / nearest / LUT tables (host + device), src / msk: packed uint8 RGB images
+ * and L masks, tmp / rsz: uint8 scratch.  Outputs: img fp32 [B][3][H][W], png int64 [B][H][W],
+ * onehot fp32 [B][H][W][num_classes+1] (may be NULL). */
+int unetseg_augment_tables_len(long long nw, long long nh, long long ksh, long long ksv, long long hsv);
+int unetseg_augment_batch(const long long* desc_host, const long long* desc, int B, const int* tables_host,
+                          const int* tables, long long n_tables, const uint8_t* src, long long src_bytes,
+                          const uint8_t* msk, long long msk_bytes, uint8_t* tmp, long long tmp_bytes, uint8_t* rsz,
+                          long long rsz_bytes, int H, int W, int num_classes, int binary, float* img, long long* png,
+                          float* onehot, void* stream);
+
 /* ---- streams ---------------------------------------------------------------------------------- */
 /* `waiter` waits for everything enqueued so far on `signaler` (device-scope release event; no
    reference counterpart: orders the weight-gradient stream against the compute stream) */

@@ -1,0 +1,139 @@
+"""GPU: the device augmentation (csrc/augment.hip via utils/hf_dataloader.py) against the CPU
+restatement of the reference's get_random_data + preprocessing + collate (oracle/augment_ref.py).
+
+The geometric part (PIL BICUBIC / NEAREST, flip, paste) and everything after it is compared
+bit-exactly: fp32 images, int64 labels, one-hot.  The HSV jitter is compared bit-exactly with the
+oracle's OpenCV restatement, which is itself parity unpinned (cv2 is absent here).
+"""
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from augment_data import make_dataset
+from oracle import augment_ref
+from utils.hf_dataloader import DeviceLoader, HFUnetDataset, make_collate
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_batch(ds, samples):
+    h, w = ds.input_shape
+    imgs, pngs, segs = [], [], []
+    for s in samples:
+        p = dict(nw=s.nw, nh=s.nh, dx=s.dx, dy=s.dy, flip=s.flip, r=s.r)
+        arr, lab = augment_ref.augment(Image.fromarray(s.image), Image.fromarray(s.mask), w, h, p)
+        jpg, png, oh = augment_ref.to_sample(arr, lab, ds.num_classes, ds.task)
+        imgs.append(jpg)
+        pngs.append(png)
+        segs.append(oh)
+    return np.stack(imgs), np.stack(pngs), np.stack(segs)
+
+
+def _check(ds, samples, out):
+    ri, rp, rs = _oracle_batch(ds, samples)
+    torch.cuda.synchronize()
+    gi, gp, gs = (t.cpu().numpy() for t in out[:3])
+    assert gi.dtype == np.float32 and gp.dtype == np.int64 and gs.dtype == np.float32
+    for b in range(len(samples)):
+        bad = np.argwhere(gi[b] != ri[b])
+        assert bad.size == 0, (b, bad[:5], gi[b][tuple(bad[0])], ri[b][tuple(bad[0])])
+    np.testing.assert_array_equal(gp, rp)
+    np.testing.assert_array_equal(gs, rs)
+
+
+@pytest.mark.parametrize("task,nc,train,shape", [("binary", 2, True, (64, 64)), ("multiclass", 4, True, (48, 80)),
+                                                  ("binary", 2, False, (64, 64)), ("multiclass", 4, False, (40, 56))])
+def test_augment_matches_oracle(tmp_path, task, nc, train, shape):
+    make_dataset(str(tmp_path), "full", "train", n=10, seed=11)
+    ds = HFUnetDataset(str(tmp_path), list(shape), nc, augmentation=train, split="train", config="full", task=task,
+                       return_cls_label=True)
+    np.random.seed(7)
+    samples = [ds[i] for i in range(len(ds))]
+    out = make_collate(ds)(samples).to_device("cuda")
+    _check(ds, samples, out)
+    assert out[3].tolist() == [s.cls_label for s in samples]
+
+
+def test_augment_edge_geometry(tmp_path):
+    """flip at both edges, negative / overhanging paste offsets, mask size != image size, 1-pixel
+    resize targets, an identity resize"""
+    make_dataset(str(tmp_path), "full", "train", n=6, seed=3, sizes=[(50, 30)] * 6,
+                 mask_sizes=[(50, 30), (25, 15), (60, 45), (50, 30), (7, 90), (50, 30)])
+    ds = HFUnetDataset(str(tmp_path), [32, 32], 4, split="train", config="full", task="multiclass")
+    np.random.seed(0)
+    samples = [ds[i] for i in range(6)]
+    geo = [(60, 36, -10, -2, True), (1, 1, 5, 7, False), (50, 30, -9, 1, True), (70, 9, -30, 20, False),
+           (3, 64, 31, -16, True), (50, 30, 0, 0, False)]
+    for s, (nw, nh, dx, dy, fl) in zip(samples, geo):
+        s.nw, s.nh, s.dx, s.dy, s.flip = nw, nh, dx, dy, fl
+    samples[1].r = None  # one sample without the HSV jitter inside a training batch
+    _check(ds, samples, make_collate(ds)(samples).to_device("cuda"))
+
+
+def test_augment_bench_size(tmp_path):
+    """the 512x512 B=16 shape of the headline workload from 640x480-class sources"""
+    sizes = [(640, 480), (480, 640), (800, 600), (512, 512)] * 4
+    make_dataset(str(tmp_path), "full", "train", n=16, seed=5, sizes=sizes)
+    ds = HFUnetDataset(str(tmp_path), [512, 512], 2, split="train", config="full", task="binary")
+    np.random.seed(11)
+    samples = [ds[i] for i in range(16)]
+    _check(ds, samples, make_collate(ds)(samples).to_device("cuda"))
+
+
+@pytest.mark.parametrize("workers", [0, 2])
+def test_device_loader(tmp_path, workers):
+    """DataLoader (CPU workers: decode + draws) -> DeviceLoader (upload + kernels one batch ahead)"""
+    make_dataset(str(tmp_path), "full", "validation", n=7, seed=9)
+    ds = HFUnetDataset(str(tmp_path), [64, 64], 2, augmentation=False, split="validation", config="full",
+                       task="binary")
+    loader = torch.utils.data.DataLoader(ds, batch_size=3, shuffle=False, num_workers=workers,
+                                         collate_fn=make_collate(ds))
+    seen = 0
+    for imgs, pngs, segs in DeviceLoader(loader, "cuda"):
+        samples = [ds[i] for i in range(seen, seen + imgs.shape[0])]
+        _check(ds, samples, (imgs, pngs, segs))
+        seen += imgs.shape[0]
+    assert seen == 7
+
+
+def test_single_item_matches_reference_item(tmp_path):
+    make_dataset(str(tmp_path), "full", "validation", n=2, seed=4)
+    ds = HFUnetDataset(str(tmp_path), [48, 48], 4, augmentation=False, split="validation", config="full",
+                       task="multiclass", return_cls_label=True)
+    jpg, png, seg, cls = ds.get(1)
+    s = ds[1]
+    arr, lab = augment_ref.augment(Image.fromarray(s.image), Image.fromarray(s.mask), 48, 48,
+                                   dict(nw=s.nw, nh=s.nh, dx=s.dx, dy=s.dy, flip=False, r=None))
+    rj, rp, rs = augment_ref.to_sample(arr, lab, 4, "multiclass")
+    np.testing.assert_array_equal(jpg, rj)
+    np.testing.assert_array_equal(png, rp)
+    np.testing.assert_array_equal(seg, rs)
+    assert cls == ds.cls_label_of(1)
+
+
+@pytest.mark.parametrize("task,model,loss", [("binary", "unet_plain", "bce"), ("multiclass", "unet_plain", "ce"),
+                                             ("multitask", "multitask_unet", "lovasz_hinge")])
+def test_train_val_on_parquet(tmp_path, task, model, loss):
+    """train.py / val.py on an HF-layout dataset (train / validation / test splits) through the
+    device loader, DataLoader workers decoding"""
+    import json
+    import os
+
+    import train
+    import val
+
+    data = tmp_path / "hf"
+    for split, n, seed in (("train", 6, 1), ("validation", 3, 2), ("test", 2, 3)):
+        make_dataset(str(data), "no-ai", split, n=n, seed=seed)
+    common = ["--task", task, "--model", model, "--input-size", "64", "--data-path", str(data), "--num-classes", "3"]
+    args = train.parse_args(common + ["--loss", loss, "--batch-size", "2", "--epochs", "2", "--workers", "2",
+                                      "--pos-weight", "auto", "--out-dir", str(tmp_path / "logs")])
+    exp = train.train(args)
+    summ = json.load(open(os.path.join(exp, "summary.json")))
+    assert len(summ["train_losses"]) == 2 and all(v == v and v > 0 for v in summ["train_losses"])
+    assert summ["test_metrics"] is not None
+    vloss = [] if task == "multiclass" else ["--loss", loss if loss != "ce" else "bce"]
+    m = val.val(val.parse_args(common + vloss + ["--weights", os.path.join(exp, "weights", "best.pth")]))
+    key = "Mean IoU" if task == "multiclass" else "IoU"
+    assert 0.0 <= float(m[key]) <= 1.0

@@ -3,11 +3,13 @@
 Same command line, same `create_model` / `get_optimizer_and_lr` helpers and the same per-epoch
 flow: set the warm-cos LR, train (binary: utils.train_and_eval.train_one_epoch_binary; multitask:
 the fused seg+cls loop), validate, keep best/last `state_dict`s, write the metric history and a
-summary.  Differences, all deliberate:
+summary.  Tasks: binary, multiclass (CE / Focal (+ Dice), Mean-IoU model selection) and
+multitask.  Differences, all deliberate:
   * the model, losses, metrics and Adam run on hand-written HIP kernels (no CPU fallback);
-  * `--data-path synthetic` (the default here) trains on the seeded synthetic embroidery-like
-    generator; the HF parquet pipeline (utils/hf_dataloader.py) is the next scope row and a real
-    path raises NotImplementedError;
+  * a real `--data-path` reads the HF parquet layout with utils/hf_dataloader.py: DataLoader
+    workers decode and draw the augmentation, the pixel work runs on the GPU (DeviceLoader);
+    `--data-path synthetic` (the default here: no dataset ships offline) uses the seeded
+    synthetic embroidery-like generator;
   * launched under torchrun (WORLD_SIZE > 1) it trains data-parallel over RCCL: rank r takes every
     W-th image, gradients are bucket-averaged during backward (unetseg_hip.ddp.GradBuckets);
   * plots / visual exports (matplotlib, cv2) are out of scope.
@@ -36,10 +38,13 @@ from model.unet_multitask import MultiTaskLoss  # noqa: E402
 from model.unet_training import get_lr_scheduler, lovasz_hinge_loss, set_optimizer_lr, weights_init  # noqa: E402
 from unetseg_hip.arena import FusedAdam  # noqa: E402
 from unetseg_hip.ddp import GradBuckets, init_from_env, local_device  # noqa: E402
+from utils.hf_dataloader import DeviceLoader, HFUnetDataset, make_collate  # noqa: E402
 from utils.synthetic import SyntheticSegDataset, collate  # noqa: E402
 from utils.train_and_eval import (  # noqa: E402
+    evaluate,
     evaluate_binary,
     evaluate_multitask,
+    train_one_epoch,
     train_one_epoch_binary,
     train_one_epoch_multitask,
 )
@@ -71,32 +76,60 @@ def get_optimizer_and_lr(model, batch_size, train_epoch, momentum, weight_decay)
 
 
 def _datasets(args, num_classes, rank, world):
-    if args.data_path != "synthetic":
-        raise NotImplementedError(
-            "the HF parquet data pipeline (utils/hf_dataloader.py) is outside this build's scope; "
-            "use --data-path synthetic")
     size = [args.input_size, args.input_size]
     cls = args.task == "multitask"
+    if args.data_path != "synthetic":  # train.py:115-137
+        task = "binary" if args.task == "multitask" else args.task
+        mk = lambda split, aug: HFUnetDataset(args.data_path, size, num_classes, augmentation=aug,  # noqa: E731
+                                              split=split, config=args.data_config, task=task,
+                                              cache_dir=args.cache_dir, return_cls_label=cls)
+        return mk("train", True), mk("validation", False), lambda: mk("test", False)
+    if args.task == "multiclass":
+        raise ValueError("the synthetic set is binary; the multiclass task needs a real --data-path")
     mk = lambda n, seed: SyntheticSegDataset(n, size, num_classes, seed=seed, return_cls_label=cls)  # noqa: E731
-    return mk(args.synthetic_train, 1234), mk(args.synthetic_val, 777_000), mk(args.synthetic_val, 888_000)
+    return mk(args.synthetic_train, 1234), mk(args.synthetic_val, 777_000), lambda: mk(args.synthetic_val, 888_000)
 
 
-def _loader(ds, args, shuffle, rank, world):
+class _SeededWorkerInit:
+    """worker_init_fn(worker_id, seed) as a picklable callable (train.py:149)"""
+
+    def __init__(self, seed):
+        self.seed = seed
+
+    def __call__(self, worker_id):
+        worker_init_fn(worker_id, self.seed)
+
+
+def _loader(ds, args, shuffle, rank, world, device, workers=None):
     sampler = None
     if world > 1:
         sampler = torch.utils.data.distributed.DistributedSampler(ds, world, rank, shuffle=shuffle, seed=args.seed)
         shuffle = False
-    return DataLoader(ds, batch_size=args.batch_size, shuffle=shuffle, sampler=sampler, num_workers=args.workers,
-                      pin_memory=True, drop_last=False, collate_fn=collate,
-                      worker_init_fn=(lambda w: worker_init_fn(w, args.seed)) if args.workers else None)
+    workers = args.workers if workers is None else workers
+    hf = isinstance(ds, HFUnetDataset)
+    dl = DataLoader(ds, batch_size=args.batch_size, shuffle=shuffle, sampler=sampler, num_workers=workers,
+                    pin_memory=not hf, drop_last=False, collate_fn=make_collate(ds) if hf else collate,
+                    worker_init_fn=_SeededWorkerInit(args.seed) if workers else None)
+    return DeviceLoader(dl, device) if hf else dl
+
+
+def _pos_weight_auto(train_ds, args, device):
+    """train.py:190-203: neg/pos over evenly spaced training samples (labels of the augmented items)"""
+    n = min(args.pos_weight_samples, len(train_ds))
+    pos = neg = 0
+    for i in np.linspace(0, len(train_ds) - 1, n, dtype=int):
+        png = train_ds.get(int(i), device)[1] if isinstance(train_ds, HFUnetDataset) else train_ds[int(i)][1]
+        pos += int((png == 1).sum())
+        neg += int((png == 0).sum())
+    if pos > 0:
+        return torch.tensor([neg / pos], dtype=torch.float32, device=device)
+    return None
 
 
 def train(args):
     rank, world, local = init_from_env("nccl")
     seed_everything(args.seed)
-    if args.task == "multiclass":
-        raise NotImplementedError("the multiclass task is outside the hot-path scope (SURVEY.md §2.1)")
-    num_classes = 2
+    num_classes = args.num_classes + 1 if args.task == "multiclass" else 2  # train.py:83-92
     device = torch.device("cuda", local_device(local)) if world > 1 else torch.device(args.device)
     if device.type != "cuda" or not torch.cuda.is_available():
         raise RuntimeError("the HIP training path needs a GPU (no CPU fallback)")
@@ -110,9 +143,9 @@ def train(args):
         with open(os.path.join(exp_folder, "config.json"), "w", encoding="utf-8") as f:
             json.dump(vars(args), f, ensure_ascii=False, indent=2)
 
-    train_ds, val_ds, test_ds = _datasets(args, num_classes, rank, world)
-    train_loader = _loader(train_ds, args, True, rank, world)
-    val_loader = _loader(val_ds, args, False, 0, 1)
+    train_ds, val_ds, make_test_ds = _datasets(args, num_classes, rank, world)
+    train_loader = _loader(train_ds, args, True, rank, world, device)
+    val_loader = _loader(val_ds, args, False, 0, 1, device)
 
     if args.task == "multitask":
         model = create_model(args.model, num_classes=1, weights=args.weights, num_seg_classes=1, num_cls_classes=3)
@@ -126,14 +159,7 @@ def train(args):
     pos_weight = None
     if args.task == "binary" and args.loss == "bce" and args.pos_weight:
         if args.pos_weight == "auto":
-            n = min(args.pos_weight_samples, len(train_ds))
-            pos = neg = 0
-            for i in np.linspace(0, len(train_ds) - 1, n, dtype=int):
-                png = train_ds[int(i)][1]
-                pos += int((png == 1).sum())
-                neg += int((png == 0).sum())
-            if pos > 0:
-                pos_weight = torch.tensor([neg / pos], dtype=torch.float32, device=device)
+            pos_weight = _pos_weight_auto(train_ds, args, device)
         else:
             pos_weight = torch.tensor([float(args.pos_weight)], dtype=torch.float32, device=device)
 
@@ -158,21 +184,31 @@ def train(args):
             if rank == 0:
                 print(f"Epoch {epoch + 1}/{args.epochs} - Loss: {loss:.4f} (Seg: {sl:.4f}, Cls: {cl:.4f}), "
                       f"Cls Acc: {acc:.2f}%")
-        else:
+        elif args.task == "binary":
             loss = train_one_epoch_binary(model, optimizer, train_loader, device, loss_name=args.loss,
                                           pos_weight=pos_weight, gpu_used=torch.cuda.memory_allocated() / 2**20,
                                           scaler=scaler if args.amp else None, epoch=epoch, train_epoch=args.epochs,
                                           ignore_index=None, max_batches=mtb)
+        else:  # train.py:285-294
+            loss = train_one_epoch(model, optimizer, train_loader, device, args.use_dice, args.loss == "focal",
+                                   torch.cuda.memory_allocated() / 2**20, num_classes,
+                                   scaler if args.amp else None, epoch, args.epochs)
         train_losses.append(loss)
+        if buckets is not None:
+            buckets.sync_buffers()  # BN running statistics: rank 0's (DDP broadcast_buffers semantics)
         if rank != 0:
             continue
         if args.task == "multitask":
             metrics = evaluate_multitask(model, val_loader, device, criterion, mvb)
             print(f"Val - IoU: {metrics['IoU']:.4f}, Dice: {metrics['Dice']:.4f}, Cls Acc: {metrics['Cls Acc']:.2f}%")
-        else:
+            score = float(metrics["IoU"])
+        elif args.task == "binary":
             metrics = evaluate_binary(model, val_loader, device, loss_name=args.loss, pos_weight=pos_weight,
                                       ignore_index=None, max_batches=mvb)
-        score = float(metrics["IoU"])
+            score = float(metrics["IoU"])
+        else:
+            metrics = evaluate(model, val_loader, device, args.use_dice, args.loss == "focal", num_classes)
+            score = float(metrics["Mean IoU"])
         val_losses.append(metrics["Loss"])
         history.append(metrics)
         if score > best_score:
@@ -186,10 +222,20 @@ def train(args):
         test_metrics = None
         if os.path.exists(best_path):
             model.load_state_dict(torch.load(best_path, map_location=device, weights_only=True))
-            test_loader = _loader(test_ds, args, False, 0, 1)
+            try:
+                test_ds = make_test_ds()
+            except FileNotFoundError as e:  # the reference skips the test pass when the split is absent
+                print(f"[test] skipped: {e}")
+                test_ds = None
+            test_loader = _loader(test_ds, args, False, 0, 1, device, max(0, args.workers // 2)) \
+                if test_ds is not None else None
             mtest = args.max_test_batches or None
-            if args.task == "multitask":
+            if test_loader is None:
+                pass
+            elif args.task == "multitask":
                 test_metrics = evaluate_multitask(model, test_loader, device, criterion, mtest)
+            elif args.task == "multiclass":
+                test_metrics = evaluate(model, test_loader, device, True, False, num_classes)
             else:
                 test_metrics = evaluate_binary(model, test_loader, device, loss_name=args.loss, pos_weight=pos_weight,
                                                ignore_index=None, max_batches=mtest)

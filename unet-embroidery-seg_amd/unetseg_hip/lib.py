@@ -19,6 +19,7 @@ L = ctypes.c_long
 F = ctypes.c_float
 SZ = ctypes.c_size_t
 ULL = ctypes.c_ulonglong
+LL = ctypes.c_longlong
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -104,12 +105,15 @@ SIGNATURES = {
     "unetseg_lovasz_fwd_masked": (I, [P, I, P, I, L, L, P, SZ, P, P, P]),
     "unetseg_channel_stats_tiles": (I, [L, I]),
     "unetseg_channel_stats": (I, [I, P, I, L, I, I, P, P]),
+    "unetseg_augment_tables_len": (I, [LL, LL, LL, LL, LL]),
+    "unetseg_augment_batch": (I, [P, P, I, P, P, LL, P, LL, P, LL, P, LL, P, LL, I, I, I, I, P, P, P, P]),
 }
 
 #: functions returning a value rather than a status (no RuntimeError on non-zero)
 VALUE_FUNCS = {"reduce_tiles", "pw_small_tiles", "conv_tile_m", "abi_version", "conv2d_fwd_tile_m",
                "conv2d_dgrad_post", "stem_fwd_tile_m", "attn_bwd1_tiles", "pw_small_tile", "conv2d_fwd_config",
-               "conv2d_dgrad_config", "conv2d_wgrad_config", "stem_config", "pw_head_tiles", "channel_stats_tiles"}
+               "conv2d_dgrad_config", "conv2d_wgrad_config", "stem_config", "pw_head_tiles", "channel_stats_tiles",
+               "augment_tables_len"}
 
 _lib = None
 

@@ -1,0 +1,326 @@
+"""HF parquet dataset with device augmentation (reference: utils/hf_dataloader.py:17-213).
+
+Reference flow per sample, on CPU workers: decode -> get_random_data (PIL BICUBIC/NEAREST resize,
+flip, paste, cv2 HSV jitter) -> /255, binarise / clamp the label, one-hot -> collate to tensors.
+
+Here the split is at the pixel work:
+  * ``HFUnetDataset.__getitem__`` (CPU, DataLoader workers) reads one parquet row, decodes the
+    image / mask with PIL exactly as the reference (``.convert("RGB")`` / ``.convert("L")``) and
+    draws the augmentation parameters with ``np.random`` in the reference's order
+    (hf_dataloader.py:135-166), so a seeded run makes the same draws.  It returns a ``RawSample``.
+  * ``hf_unet_dataset_collate`` packs a list of ``RawSample`` into one ``RawBatch``: the uint8
+    pixels back to back plus the per-sample descriptors and tables (utils/augment_tables.py).
+  * ``RawBatch.to_device`` (main process) uploads the bytes and runs ``unetseg_augment_batch``
+    (csrc/augment.hip): resize, flip, paste, HSV jitter, /255, label handling and one-hot for the
+    whole batch, writing the collated ``(images, pngs, seg_labels[, cls_labels])`` the reference's
+    collate returns, already on the GPU.  ``DeviceLoader`` wraps a DataLoader and does this one
+    batch ahead on a side stream.
+The geometric part is bit-exact with Pillow; the HSV jitter follows OpenCV's 8-bit algorithm
+(parity unpinned: cv2 is not installed here, see oracle/augment_ref.py).
+
+Dataset layout (convert_and_upload.py:60-90): ``{data_dir}/{config}/{split}/data.parquet`` with
+columns image / mask (HF Image structs: bytes + path), label, filename, subset.
+"""
+from __future__ import annotations
+
+import glob
+import io
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+from PIL import Image
+
+from utils.augment_tables import bicubic_coeffs, hsv_luts, nearest_index
+
+AUG_DESC = 20  # csrc/augment.hip descriptor width (int64)
+(D_SRC, D_MSK, D_TMP, D_RSZ, D_IW, D_IH, D_NW, D_NH, D_DX, D_DY, D_FLIP, D_Y0, D_ROWS, D_KSH, D_KSV, D_TAB, D_HSV,
+ D_MIW, D_MIH) = range(19)
+
+_SPLIT_ALIASES = {"validation": ("validation", "val", "valid", "dev"), "train": ("train", "training"),
+                  "test": ("test", "testing", "eval")}
+
+
+def find_split_files(data_dir, config, split):
+    """the parquet files ``load_dataset(f"{data_dir}/{config}", split=split)`` reads for a local
+    directory (HF's default patterns: ``{split}/*.parquet``, ``{split}-*.parquet``,
+    ``data/{split}-*.parquet``)"""
+    root = os.path.join(data_dir, config)
+    for name in _SPLIT_ALIASES.get(split, (split,)):
+        for pat in (os.path.join(root, name, "*.parquet"), os.path.join(root, f"{name}-*.parquet"),
+                    os.path.join(root, "data", f"{name}-*.parquet"), os.path.join(root, f"{name}.parquet")):
+            files = sorted(glob.glob(pat))
+            if files:
+                return files
+    raise FileNotFoundError(f"no parquet files for split '{split}' under {root}")
+
+
+def _open_image(cell, base_dir):
+    """an HF Image cell: {'bytes': ..., 'path': ...} (bytes win; else the path, relative to the data)"""
+    if isinstance(cell, dict):
+        data, path = cell.get("bytes"), cell.get("path")
+    else:
+        data, path = None, cell
+    if data is not None:
+        return Image.open(io.BytesIO(data))
+    if path is None:
+        raise ValueError("image cell has neither bytes nor path")
+    if not os.path.isabs(path) and not os.path.exists(path):
+        path = os.path.join(base_dir, path)
+    return Image.open(path)
+
+
+@dataclass
+class RawSample:
+    """one decoded sample and its drawn augmentation (picklable: crosses DataLoader workers)"""
+    image: np.ndarray  # uint8 [ih][iw][3]
+    mask: np.ndarray  # uint8 [mh][mw]
+    nw: int
+    nh: int
+    dx: int
+    dy: int
+    flip: bool
+    r: np.ndarray | None  # HSV factors (training) or None (validation letterbox)
+    cls_label: int | None = None
+
+
+class HFUnetDataset(torch.utils.data.Dataset):
+    """hf_dataloader.py:17-105 (same constructor, same CLASS_TO_IDX, same draws)"""
+
+    CLASS_TO_IDX = {"动物类": 0, "植物类": 1, "复合类": 2}
+
+    def __init__(self, data_dir, input_shape, num_classes, augmentation=True, split="train", config="full",
+                 task: str = "multiclass", cache_dir: str | None = None, return_cls_label: bool = False):
+        import pyarrow.parquet as pq
+
+        self.input_shape = input_shape
+        self.num_classes = num_classes
+        self.augmentation = augmentation
+        self.task = task
+        self.return_cls_label = return_cls_label
+        self.files = find_split_files(data_dir, config, split)
+        self.base_dir = os.path.join(data_dir, config)
+        tables = [pq.read_table(f) for f in self.files]
+        cols = set(tables[0].column_names)
+        missing = {"image", "mask"} - cols
+        if missing:
+            raise ValueError(f"{self.files[0]}: missing columns {sorted(missing)}")
+        self.images, self.masks, self.labels = [], [], []
+        for t in tables:
+            self.images += t.column("image").to_pylist()
+            self.masks += t.column("mask").to_pylist()
+            self.labels += t.column("label").to_pylist() if "label" in cols else ["unknown"] * t.num_rows
+        self.length = len(self.images)
+
+    def __len__(self):
+        return self.length
+
+    @staticmethod
+    def rand(a=0, b=1):
+        """hf_dataloader.py:107-109"""
+        return np.random.rand() * (b - a) + a
+
+    def draw(self, iw, ih, jitter=.3, hue=.1, sat=0.7, val=0.3, random=True):
+        """the parameters get_random_data (hf_dataloader.py:111-166) draws, in its order"""
+        h, w = self.input_shape
+        if not random:
+            scale = min(w / iw, h / ih)
+            nw, nh = int(iw * scale), int(ih * scale)
+            return dict(nw=nw, nh=nh, dx=(w - nw) // 2, dy=(h - nh) // 2, flip=False, r=None)
+        new_ar = iw / ih * self.rand(1 - jitter, 1 + jitter) / self.rand(1 - jitter, 1 + jitter)
+        scale = self.rand(0.25, 2)
+        if new_ar < 1:
+            nh = int(scale * h)
+            nw = int(nh * new_ar)
+        else:
+            nw = int(scale * w)
+            nh = int(nw / new_ar)
+        if nw <= 0 or nh <= 0:  # PIL's resize refuses an empty size, so does the reference
+            raise ValueError(f"height and width must be > 0 (drew {nw}x{nh})")
+        flip = self.rand() < .5
+        dx = int(self.rand(0, w - nw))
+        dy = int(self.rand(0, h - nh))
+        r = np.random.uniform(-1, 1, 3) * [hue, sat, val] + 1
+        return dict(nw=nw, nh=nh, dx=dx, dy=dy, flip=bool(flip), r=r)
+
+    def cls_label_of(self, index):
+        """hf_dataloader.py:94-103"""
+        name = self.labels[index] or "unknown"
+        for cname, idx in self.CLASS_TO_IDX.items():
+            if name.startswith(cname):
+                return idx
+        return 0
+
+    def __getitem__(self, index) -> RawSample:
+        jpg = _open_image(self.images[index], self.base_dir).convert("RGB")
+        png = _open_image(self.masks[index], self.base_dir).convert("L")
+        iw, ih = jpg.size
+        p = self.draw(iw, ih, random=self.augmentation)
+        return RawSample(image=np.asarray(jpg, np.uint8), mask=np.asarray(png, np.uint8),
+                         cls_label=self.cls_label_of(index) if self.return_cls_label else None, **p)
+
+    def get(self, index, device="cuda"):
+        """the reference's item (jpg fp32 [3,H,W], png int64 [H,W], seg_labels fp32 [H,W,C+1][, cls]) as
+        numpy, produced through the device path (one-sample batch)"""
+        out = hf_unet_dataset_collate([self[index]], self.input_shape, self.num_classes, self.task).to_device(device)
+        torch.cuda.synchronize()
+        vals = [t[0].cpu().numpy() for t in out[:3]]
+        return (*vals, int(out[3][0])) if len(out) == 4 else tuple(vals)
+
+
+@dataclass
+class RawBatch:
+    """host side of one batch: packed pixels + descriptors + tables, ready for unetseg_augment_batch"""
+    src: np.ndarray
+    msk: np.ndarray
+    desc: np.ndarray  # int64 [B][AUG_DESC]
+    tables: np.ndarray  # int32
+    tmp_bytes: int
+    rsz_bytes: int
+    input_shape: tuple
+    num_classes: int
+    binary: bool
+    cls_labels: np.ndarray | None = None
+    pinned: dict = field(default_factory=dict)
+
+    def __len__(self):
+        return self.desc.shape[0]
+
+    def pin(self):
+        """page-lock the host arrays (once) so the uploads run asynchronously"""
+        if not self.pinned:
+            for k in ("src", "msk", "tables", "desc"):
+                self.pinned[k] = torch.from_numpy(getattr(self, k)).pin_memory()
+        return self
+
+    def to_device(self, device="cuda", stream=None, onehot=True):
+        """run the device augmentation; returns (images, pngs, seg_labels[, cls_labels]) on `device`"""
+        from unetseg_hip.lib import lib
+
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise RuntimeError("the device augmentation needs a GPU (no CPU fallback)")
+        stream = stream or torch.cuda.current_stream(device)
+        self.pin()
+        B = len(self)
+        H, W = int(self.input_shape[0]), int(self.input_shape[1])
+        with torch.cuda.stream(stream):
+            dev = {k: v.to(device, non_blocking=True) for k, v in self.pinned.items()}
+            tmp = torch.empty(max(self.tmp_bytes, 1), dtype=torch.uint8, device=device)
+            rsz = torch.empty(max(self.rsz_bytes, 1), dtype=torch.uint8, device=device)
+            img = torch.empty(B, 3, H, W, dtype=torch.float32, device=device)
+            png = torch.empty(B, H, W, dtype=torch.int64, device=device)
+            seg = torch.empty(B, H, W, self.num_classes + 1, dtype=torch.float32, device=device) if onehot else None
+        lib.augment_batch(self.pinned["desc"].data_ptr(), dev["desc"].data_ptr(), B, self.pinned["tables"].data_ptr(),
+                          dev["tables"].data_ptr(), self.tables.size, dev["src"].data_ptr(), self.src.size,
+                          dev["msk"].data_ptr(), self.msk.size, tmp.data_ptr(), self.tmp_bytes, rsz.data_ptr(),
+                          self.rsz_bytes, H, W, self.num_classes, int(self.binary), img.data_ptr(), png.data_ptr(),
+                          seg.data_ptr() if seg is not None else None, stream.cuda_stream)
+        # the scratch and the uploads must outlive the kernels queued on `stream`
+        for t in list(dev.values()) + [tmp, rsz]:
+            t.record_stream(stream)
+        out = (img, png, seg)
+        if self.cls_labels is not None:
+            with torch.cuda.stream(stream):
+                cls = torch.from_numpy(self.cls_labels).to(device, non_blocking=True)
+            out = out + (cls,)
+        return out
+
+
+def pack_batch(samples, input_shape, num_classes, task="multiclass"):
+    """list[RawSample] -> RawBatch (descriptors + tables per utils/augment_tables.py)"""
+    B = len(samples)
+    desc = np.zeros((B, AUG_DESC), np.int64)
+    srcs, msks, tabs = [], [], []
+    src_off = msk_off = tmp_off = rsz_off = tab_off = 0
+    for i, s in enumerate(samples):
+        ih, iw = s.image.shape[:2]
+        mh, mw = s.mask.shape[:2]
+        bh, kh, ksh = bicubic_coeffs(iw, s.nw)
+        bv, kv, ksv = bicubic_coeffs(ih, s.nh)
+        y0 = int(bv[0, 0])
+        y1 = int(bv[-1, 0] + bv[-1, 1])
+        bv = bv.copy()
+        bv[:, 0] -= y0  # ImagingResampleInner: the vertical pass reads the horizontal pass's rows
+        parts = [bh.ravel(), kh.ravel(), bv.ravel(), kv.ravel(), nearest_index(mw, s.nw), nearest_index(mh, s.nh)]
+        hsv = s.r is not None
+        if hsv:
+            parts.append(hsv_luts(np.asarray(s.r)).astype(np.int32).ravel())
+        t = np.concatenate([np.asarray(p, np.int32) for p in parts])
+        rows = y1 - y0
+        desc[i, [D_SRC, D_MSK, D_TMP, D_RSZ, D_IW, D_IH, D_NW, D_NH, D_DX, D_DY, D_FLIP, D_Y0, D_ROWS, D_KSH, D_KSV,
+                 D_TAB, D_HSV, D_MIW, D_MIH]] = [src_off, msk_off, tmp_off, rsz_off, iw, ih, s.nw, s.nh, s.dx, s.dy,
+                                                 int(s.flip), y0, rows, ksh, ksv, tab_off, int(hsv), mw, mh]
+        srcs.append(np.ascontiguousarray(s.image, np.uint8).ravel())
+        msks.append(np.ascontiguousarray(s.mask, np.uint8).ravel())
+        tabs.append(t)
+        src_off += iw * ih * 3
+        msk_off += mw * mh
+        tmp_off += rows * s.nw * 3
+        rsz_off += s.nh * s.nw * 3
+        tab_off += t.size
+    cls = None
+    if samples and samples[0].cls_label is not None:
+        cls = np.array([s.cls_label for s in samples], np.int64)
+    return RawBatch(src=np.concatenate(srcs), msk=np.concatenate(msks), desc=desc, tables=np.concatenate(tabs),
+                    tmp_bytes=tmp_off, rsz_bytes=rsz_off, input_shape=tuple(int(v) for v in input_shape),
+                    num_classes=num_classes, binary=(task == "binary"), cls_labels=cls)
+
+
+class _Collate:
+    """picklable collate bound to the dataset's shape / classes / task"""
+
+    def __init__(self, input_shape, num_classes, task):
+        self.args = (input_shape, num_classes, task)
+
+    def __call__(self, batch):
+        return pack_batch(batch, *self.args)
+
+
+def hf_unet_dataset_collate(batch, input_shape=None, num_classes=None, task="multiclass"):
+    """hf_dataloader.py:183-213.  With a dataset's settings: ``hf_unet_dataset_collate(batch, ...)``
+    or ``make_collate(dataset)`` as the DataLoader's collate_fn.  Returns a RawBatch; the tensors the
+    reference's collate returns come from ``RawBatch.to_device`` / ``DeviceLoader``."""
+    if input_shape is None:
+        raise TypeError("hf_unet_dataset_collate needs the dataset's input_shape / num_classes / task here: "
+                        "use make_collate(dataset) as the DataLoader's collate_fn")
+    return pack_batch(batch, input_shape, num_classes, task)
+
+
+def make_collate(dataset: HFUnetDataset):
+    return _Collate(tuple(dataset.input_shape), dataset.num_classes, dataset.task)
+
+
+class DeviceLoader:
+    """iterate a DataLoader of RawBatch as the reference's collated tensors on `device`; batch i+1 is
+    uploaded and augmented on a side stream while the caller computes on batch i"""
+
+    def __init__(self, loader, device="cuda", onehot=True):
+        self.loader, self.device, self.onehot = loader, torch.device(device), onehot
+        self.sampler = getattr(loader, "sampler", None)
+        self.dataset = getattr(loader, "dataset", None)
+
+    def __len__(self):
+        return len(self.loader)
+
+    def __iter__(self):
+        side = torch.cuda.Stream(self.device)
+        pending = None
+        for raw in self.loader:
+            cur = raw.to_device(self.device, side, self.onehot)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            if pending is not None:
+                yield self._ready(*pending)
+            pending = (cur, ev)
+        if pending is not None:
+            yield self._ready(*pending)
+
+    def _ready(self, tensors, ev):
+        cs = torch.cuda.current_stream(self.device)
+        cs.wait_event(ev)
+        for t in tensors:
+            if t is not None:
+                t.record_stream(cs)
+        return tensors

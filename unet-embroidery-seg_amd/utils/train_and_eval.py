@@ -1,8 +1,10 @@
-"""Binary training / evaluation loops (reference: utils/train_and_eval.py:106-305).
+"""Training / evaluation loops (reference: utils/train_and_eval.py:20-513): binary
+(train_one_epoch_binary / evaluate_binary), multiclass (train_one_epoch / evaluate and the four
+confusion-matrix metrics) and multitask.
 
-Same signatures, return values and metric definitions as the reference; the loss and the
+Same signatures, return values and metric definitions as the reference; the losses and the
 confusion counts run on fused HIP kernels and the per-iteration host syncs are reduced to one
-``loss.item()``.  The multiclass loops (train_one_epoch/evaluate) are outside the hot-path scope.
+``loss.item()``.
 """
 import time
 

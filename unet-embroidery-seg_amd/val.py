@@ -2,8 +2,10 @@
 
 Loads a state_dict (weights_only) into the named model and reports the binary metrics
 (evaluate_binary: Dice / IoU / Precision / Recall / Accuracy, eps 1e-7) or, for multitask, seg
-IoU / Dice (eps 1e-6) plus overall and per-class classification accuracy.  Data: the seeded
-synthetic test split (`--data-path synthetic`); the HF parquet pipeline is out of scope.
+IoU / Dice (eps 1e-6) plus overall and per-class classification accuracy, or for multiclass the
+reference's `evaluate` (CE + Dice loss, pixel / mean accuracy, mean / frequency-weighted IoU).
+Data: the HF parquet test split (utils/hf_dataloader.py, device augmentation) or the seeded
+synthetic test split (`--data-path synthetic`, binary / multitask only).
 """
 from __future__ import annotations
 
@@ -20,25 +22,34 @@ from torch.utils.data import DataLoader  # noqa: E402
 
 from model.model_factory import SUPPORTED_MODELS, build_model  # noqa: E402
 from unetseg_hip import losses  # noqa: E402
+from utils.hf_dataloader import DeviceLoader, HFUnetDataset, make_collate  # noqa: E402
 from utils.synthetic import SyntheticSegDataset, collate  # noqa: E402
-from utils.train_and_eval import LogColor, evaluate_binary  # noqa: E402
+from utils.train_and_eval import LogColor, evaluate, evaluate_binary  # noqa: E402
 
 CLASS_NAMES = ["动物类", "植物类", "复合类"]  # val.py:84
 
 
 def val(args):
-    if args.task == "multiclass":
-        raise NotImplementedError("the multiclass task is outside the hot-path scope (SURVEY.md §2.1)")
-    if args.data_path != "synthetic":
-        raise NotImplementedError("the HF parquet data pipeline is outside this build's scope; use --data-path synthetic")
+    num_classes = args.num_classes + 1 if args.task == "multiclass" else 2  # val.py:22-27
     device = torch.device(args.device)
-    ds = SyntheticSegDataset(args.synthetic_test, [args.input_size] * 2, 2, seed=888_000,
-                             return_cls_label=args.task == "multitask")
-    loader = DataLoader(ds, batch_size=args.batch_size, shuffle=False, num_workers=0, collate_fn=collate)
+    input_shape = [args.input_size] * 2
+    if args.data_path != "synthetic":  # val.py:31-56
+        ds = HFUnetDataset(args.data_path, input_shape, num_classes, augmentation=False, split="test",
+                           config=args.data_config, task="binary" if args.task == "multitask" else args.task,
+                           cache_dir=args.cache_dir, return_cls_label=args.task == "multitask")
+        print(f"Test samples: {len(ds)}")
+        loader = DeviceLoader(DataLoader(ds, batch_size=args.batch_size, shuffle=False, num_workers=0,
+                                         collate_fn=make_collate(ds)), device)
+    else:
+        if args.task == "multiclass":
+            raise ValueError("the synthetic set is binary; the multiclass task needs a real --data-path")
+        ds = SyntheticSegDataset(args.synthetic_test, input_shape, 2, seed=888_000,
+                                 return_cls_label=args.task == "multitask")
+        loader = DataLoader(ds, batch_size=args.batch_size, shuffle=False, num_workers=0, collate_fn=collate)
     if args.task == "multitask":
         model = build_model(args.model, num_classes=1, num_seg_classes=1, num_cls_classes=3)
     else:
-        model = build_model(args.model, num_classes=2)
+        model = build_model(args.model, num_classes=num_classes)
     model.load_state_dict(torch.load(args.weights, map_location="cpu", weights_only=True))
     model.to(device)
     print(f"Model loaded from: {args.weights}")
@@ -48,6 +59,10 @@ def val(args):
         print(f"{LogColor.RED}Dice{LogColor.RESET}\t{LogColor.RED}IoU{LogColor.RESET}\t{LogColor.RED}Precision"
               f"{LogColor.RESET}\t{LogColor.RED}Recall{LogColor.RESET}\t{LogColor.RED}Accuracy{LogColor.RESET}")
         print(f"{m['Dice']:.4f}\t{m['IoU']:.4f}\t{m['Precision']:.4f}\t{m['Recall']:.4f}\t{m['Accuracy']:.4f}")
+        return m
+    if args.task == "multiclass":
+        m = evaluate(model, loader, device, dice_loss=True, focal_loss=False, num_classes=num_classes)
+        print(m)
         return m
 
     model.eval()
