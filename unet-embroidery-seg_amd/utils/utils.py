@@ -30,3 +30,17 @@ def worker_init_fn(worker_id, seed=0):
 def preprocess_input(image):
     image /= 255.0
     return image
+
+
+def cvtColor(image):
+    """utils/utils.py:11-16: anything but a 3-channel image is converted to RGB"""
+    if len(np.shape(image)) == 3 and np.shape(image)[2] == 3:
+        return image
+    return image.convert("RGB")
+
+
+def letterbox_params(iw, ih, w, h):
+    """resize_image's geometry (utils/utils.py:22-34): (nw, nh, dx, dy) of the centred paste"""
+    scale = min(w / iw, h / ih)
+    nw, nh = int(iw * scale), int(ih * scale)
+    return nw, nh, (w - nw) // 2, (h - nh) // 2
