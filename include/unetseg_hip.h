@@ -49,9 +49,11 @@ typedef struct UnetsegPackDesc {
   const float* w;  /* fp32 [K][C][R][S] */
   void* wk;        /* dtype [K][R][S][Cpad] */
   void* wt;        /* dtype [C][R][S][K] or NULL */
-  long long start; /* first tile of this conv (ascending, desc[0].start == 0; ceil(K/32)*ceil(Cpad/64) tiles) */
+  long long start; /* first tile of this conv (ascending, desc[0].start == 0; unetseg_pack_tiles tiles) */
   int K, C, R, S, Cpad, pad_;
 } UnetsegPackDesc;
+/* blocks unetseg_pack_conv_weights spends on one conv: desc[i+1].start = desc[i].start + this */
+int unetseg_pack_tiles(int K, int Cpad, int taps);
 /* every conv weight of a model in one launch (total = number of tiles) */
 int unetseg_pack_conv_weights(int dtype, const void* desc, int n, long total, void* stream);
 /* legacy generic row tile (kept for ABI v1 callers) */

@@ -14,6 +14,7 @@ from collections import defaultdict
 def main():
     d = sys.argv[1]
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    top = int(sys.argv[3]) if len(sys.argv) > 3 else 14
     rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"], r["Kernel_Name"]) for r in rows]
     ks.sort()
@@ -52,7 +53,7 @@ def main():
             key = n.replace("void (anonymous namespace)::", "").replace("(anonymous namespace)::", "").split("(")[0][:70]
             agg[key][0] += 1
             agg[key][1] += (b - a) / 1e6 / steps
-        for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:14]:
+        for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
             print(f"   {t:7.3f} ms {c // steps:4d}x  {n}")
 
 

@@ -97,7 +97,7 @@ struct UnetsegPackDesc {
   const float* w;   // fp32 [K][C][R][S]
   void* wk;         // dtype [K][R][S][Cpad]
   void* wt;         // dtype [C][R][S][K] or NULL
-  long long start;  // first tile of this conv in the batch (ceil(K/32)*ceil(Cpad/64) tiles per conv)
+  long long start;  // first tile of this conv in the batch (unetseg_pack_tiles tiles per conv)
   int K, C, R, S, Cpad, pad_;
 };
 

@@ -520,14 +520,24 @@ __global__ void pack_weights_kernel(const float* w, int K, int C, int R, int S, 
   }
 }
 
-// Every conv of a model in one launch.  A block packs a tile of 32 output x 64 input channels of
-// one conv for all taps: fp32 reads are shared across the tap loop through L1/L2, the wk image
-// ([K][R][S][Cpad], channel-contiguous) is written straight from the loads and the transposed wt
-// image ([C][R][S][K], K-contiguous) through an LDS transpose, so every store is coalesced.
-// desc[i].start = first tile of conv i (tiles of a conv: ceil(K/32) * ceil(Cpad/64)).
+// Batched pack of many conv weights: one block per (16 output channels x CT input channels) tile of
+// one conv (desc[i].start = its first tile; unetseg_pack_tiles gives a conv's tile count).  The fp32
+// source of a tile is 16 contiguous runs of CT*taps floats ([K][C][R][S] keeps c and the taps of
+// one k together), read with unit-stride coalesced loads into LDS; the wk image ([K][R][S][Cpad])
+// and the transposed wt image ([C][R][S][K]) are then written from LDS, channel-contiguous and
+// k-contiguous respectively.  CT = pow2 in [8, 256] with CT * taps <= 512, so the tile fits the
+// static LDS array; the odd row pitch (513) keeps both LDS read patterns conflict-free.
+constexpr int kPackK = 16;
+
+__host__ __device__ inline int pack_ct(int taps) {
+  int ct = 256;
+  while (ct > 8 && ct * taps > 512) ct >>= 1;
+  return ct;
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const UnetsegPackDesc* desc, int n) {
-  __shared__ float tile[32][65];
+  __shared__ float tile[kPackK][513];
   const long b = blockIdx.x;
   int lo = 0, hi = n - 1;
   while (lo < hi) {  // last desc with start <= b
@@ -535,31 +545,87 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const Unetseg
     if (desc[mid].start <= b) lo = mid; else hi = mid - 1;
   }
   const UnetsegPackDesc d = desc[lo];
-  const int lt = (int)(b - d.start);
-  const int ctiles = (d.Cpad + 63) / 64;
-  const int kt = lt / ctiles, ct = lt - kt * ctiles;
   const int taps = d.R * d.S;
+  const int CT = pack_ct(taps);
+  const int lt = (int)(b - d.start);
+  const int ctiles = (d.Cpad + CT - 1) / CT;
+  const int kt = lt / ctiles, ct = lt - kt * ctiles;
+  const int k0 = kt * kPackK, c0 = ct * CT;
+  const int run = CT * taps;                           // floats per k row of the tile
+  const int vrun = max(0, min(CT, d.C - c0)) * taps;   // of which exist in the source
   const int t = threadIdx.x;
-  const int cl = t & 63, kl0 = t >> 6;
-  const int c = ct * 64 + cl;
-  for (int tap = 0; tap < taps; ++tap) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int kl = kl0 + 4 * i, k = kt * 32 + kl;
-      float v = 0.f;
-      if (k < d.K && c < d.C) v = d.w[((long)k * d.C + c) * taps + tap];
-      tile[kl][cl] = v;
-      if (k < d.K && c < d.Cpad) reinterpret_cast<T*>(d.wk)[((long)k * taps + tap) * d.Cpad + c] = (T)v;
+  if ((d.C * taps) % 4 == 0 && vrun % 4 == 0) {  // 16-B loads (rows start 16-B aligned)
+    const int run4 = run >> 2;
+    for (int i = t; i < kPackK * run4; i += 256) {
+      const int kl = i / run4, j = (i - kl * run4) * 4;
+      const int k = k0 + kl;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < d.K && j < vrun) v = *reinterpret_cast<const float4*>(d.w + ((long)k * d.C + c0) * taps + j);
+      tile[kl][j] = v.x;
+      tile[kl][j + 1] = v.y;
+      tile[kl][j + 2] = v.z;
+      tile[kl][j + 3] = v.w;
     }
-    if (d.wt) {
-      __syncthreads();
-      const int kl = t & 31, k = kt * 32 + kl;
+  } else {
+    for (int i = t; i < kPackK * run; i += 256) {
+      const int kl = i / run, j = i - kl * run;
+      const int k = k0 + kl;
+      tile[kl][j] = (k < d.K && j < vrun) ? d.w[((long)k * d.C + c0) * taps + j] : 0.f;
+    }
+  }
+  __syncthreads();
+  // wk[k][tap][c], c fastest, 4 channels per store (padding channels c in [C, Cpad) get the zeros
+  // staged above)
+  T* wk = reinterpret_cast<T*>(d.wk);
+  if (d.Cpad % 4 == 0) {
+    const int CT4 = CT >> 2;
+    for (int i = t; i < kPackK * taps * CT4; i += 256) {
+      const int c4 = i % CT4, rest = i / CT4;
+      const int tap = rest % taps, kl = rest / taps;
+      const int k = k0 + kl, c = c0 + c4 * 4;
+      if (k >= d.K || c >= d.Cpad) continue;
+      T o[4];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int cl2 = (t >> 5) + 8 * i, c2 = ct * 64 + cl2;
-        if (k < d.K && c2 < d.C) reinterpret_cast<T*>(d.wt)[((long)c2 * taps + tap) * d.K + k] = (T)tile[kl][cl2];
+      for (int e = 0; e < 4; ++e) o[e] = (T)tile[kl][(c4 * 4 + e) * taps + tap];
+      T* dst = wk + ((long)k * taps + tap) * d.Cpad + c;
+      if (sizeof(T) == 2) *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(o);
+      else *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(o);
+    }
+  } else {
+    for (int i = t; i < kPackK * taps * CT; i += 256) {
+      const int cl = i % CT, rest = i / CT;
+      const int tap = rest % taps, kl = rest / taps;
+      const int k = k0 + kl, c = c0 + cl;
+      if (k < d.K && c < d.Cpad) wk[((long)k * taps + tap) * d.Cpad + c] = (T)tile[kl][cl * taps + tap];
+    }
+  }
+  if (d.wt) {  // wt[c][tap][k], k fastest, 8 output channels per store
+    T* wt = reinterpret_cast<T*>(d.wt);
+    if (d.K % 8 == 0) {
+      constexpr int K8 = kPackK / 8;
+      for (int i = t; i < K8 * taps * CT; i += 256) {
+        const int k8 = i % K8, rest = i / K8;
+        const int tap = rest % taps, cl = rest / taps;
+        const int k = k0 + k8 * 8, c = c0 + cl;
+        if (k >= d.K || c >= d.C) continue;
+        T o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (T)tile[k8 * 8 + e][cl * taps + tap];
+        T* dst = wt + ((long)c * taps + tap) * d.K + k;
+        if (sizeof(T) == 2) {
+          *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(o);
+        } else {
+          reinterpret_cast<uint4*>(dst)[0] = reinterpret_cast<const uint4*>(o)[0];
+          reinterpret_cast<uint4*>(dst)[1] = reinterpret_cast<const uint4*>(o)[1];
+        }
       }
-      __syncthreads();
+    } else {
+      for (int i = t; i < kPackK * taps * CT; i += 256) {
+        const int kl = i % kPackK, rest = i / kPackK;
+        const int tap = rest % taps, cl = rest / taps;
+        const int k = k0 + kl, c = c0 + cl;
+        if (k < d.K && c < d.C) wt[((long)c * taps + tap) * d.K + k] = (T)tile[kl][cl * taps + tap];
+      }
     }
   }
 }
@@ -961,6 +1027,12 @@ UNETSEG_API int unetseg_conv2d_wgrad_config(int dtype, int c1, int ldc1, int c2,
 // All of a model's conv weights in one launch.  desc: DEVICE array of n UnetsegPackDesc with
 // ascending `start` = first tile (desc[0].start == 0; a conv has ceil(K/32)*ceil(Cpad/64) tiles);
 // total = number of tiles.
+// blocks of unetseg_pack_conv_weights for one conv (its desc.start advances by this much)
+UNETSEG_API int unetseg_pack_tiles(int K, int Cpad, int taps) {
+  const int ct = pack_ct(taps);
+  return ceil_div(K, kPackK) * ceil_div(Cpad, ct);
+}
+
 UNETSEG_API int unetseg_pack_conv_weights(int dtype, const void* desc, int n, long total, void* stream) {
   US_CHECK_ARG(desc && n > 0 && total > 0 && total < (1L << 31), "pack_conv_weights: bad args");
   hipStream_t st = (hipStream_t)stream;

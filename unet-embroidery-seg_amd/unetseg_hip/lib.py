@@ -34,6 +34,7 @@ SIGNATURES = {
     "unetseg_conv2d_wgrad": (I, [I, P, I, I, P, I, I, I, I, I, P, I, I, I, I, I, I, P, SZ, P, I, I, P]),
     "unetseg_pack_conv_weight": (I, [I, P, I, I, I, I, I, P, P, P]),
     "unetseg_pack_conv_weights": (I, [I, P, I, L, P]),
+    "unetseg_pack_tiles": (I, [I, I, I]),
     "unetseg_bn_finalize": (I, [P, I, I, L, I, P, P, P, P, P, F, F, P, P, P, P, P]),
     "unetseg_bn_eval_coeffs": (I, [I, P, P, P, P, F, P, P, P]),
     "unetseg_bn_apply": (I, [I, P, I, P, P, P, I, P, P, I, I, P, I, L, I, P]),
@@ -113,7 +114,7 @@ SIGNATURES = {
 VALUE_FUNCS = {"reduce_tiles", "pw_small_tiles", "conv_tile_m", "abi_version", "conv2d_fwd_tile_m",
                "conv2d_dgrad_post", "stem_fwd_tile_m", "attn_bwd1_tiles", "pw_small_tile", "conv2d_fwd_config",
                "conv2d_dgrad_config", "conv2d_wgrad_config", "stem_config", "pw_head_tiles", "channel_stats_tiles",
-               "augment_tables_len"}
+               "augment_tables_len", "pack_tiles"}
 
 _lib = None
 

@@ -235,7 +235,7 @@ class PackTable:
             for i, (pc, nt) in enumerate(zip(pcs, need_t)):
                 d[i] = (pc.conv.weight.data_ptr(), pc.wk.data_ptr(), pc.wt.data_ptr() if nt else 0, start,
                         pc.K, pc.C, pc.R, pc.S, pc.cpad, 0)
-                start += -(-pc.K // 32) * -(-pc.cpad // 64)
+                start += lib.pack_tiles(pc.K, pc.cpad, pc.R * pc.S)
             self.desc = torch.from_numpy(d.view(np.uint8).copy()).to(ctx.device)
             self.total = start
             self.key = key
