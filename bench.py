@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--probe", type=int, default=1)
     ap.add_argument("--graph", type=int, default=0, help="replay the whole step (fwd+loss+bwd+Adam) as a HIP graph")
     ap.add_argument("--stream", type=int, default=1, help="run the steps on a created (non-default) HIP stream")
+    ap.add_argument("--priority", type=int, default=0, help="priority of that stream (lower = higher priority)")
     return ap.parse_args()
 
 
@@ -166,7 +167,7 @@ def main():
     if args.stream:
         # the legacy default stream synchronises implicitly with other streams, which makes the
         # compute stream's final join with the weight-gradient stream slow; work on a created one
-        torch.cuda.set_stream(torch.cuda.Stream(dev))
+        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=args.priority))
 
     from model.model_factory import create_model
     from unetseg_hip import ops

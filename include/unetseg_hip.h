@@ -66,6 +66,10 @@ int unetseg_conv2d_fwd_tile_m(int dtype, int c1, int ldc1, int c2, int ldc2, int
 int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h,
                        int w, const void* wk, int cout, int r, int s, int stride, int pad, const float* bias, int relu,
                        void* y, int ldy, float* stats, void* stream);
+/* y = [relu](conv(x, wk) * escale[cout] + bias[cout]): eval-mode BN on the accumulator (generic kernel) */
+int unetseg_conv2d_fwd_affine(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n,
+                              int h, int w, const void* wk, int cout, int r, int s, int stride, int pad,
+                              const float* escale, const float* bias, int relu, void* y, int ldy, void* stream);
 /* Kernel-configuration queries (host only, nothing is launched; replace no reference operator:
  * they let the parity tests assert that they exercise every kernel configuration the benchmark
  * selects).  Codes: 0 = halo3 (64-channel 3x3 kernel), 1..14 = TN tile configuration
@@ -132,6 +136,11 @@ int unetseg_bn_finalize(const float* part, int C, int G, long M, int tile, const
  * block's concatenation): part [ceil(M/tile)][2][C] = (sum, M2 about the tile mean), for bn_finalize */
 int unetseg_channel_stats_tiles(long M, int tile);
 int unetseg_channel_stats(int dtype, const void* x, int ldx, long M, int c, int tile, float* part, void* stream);
+/* eval-mode BN folded into the conv epilogue (model/resnet_backbone.py:58-61, model/unet_plain.py:8-15
+ * in .eval()): kscale = gamma / sqrt(running_var + eps), bias = beta - running_mean * kscale
+ * (+ conv_bias * kscale), for unetseg_conv2d_fwd_affine */
+int unetseg_bn_fold(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
+                    const float* conv_bias, float* kscale, float* bias, void* stream);
 int unetseg_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar,
                            float eps, float* scale, float* shift, void* stream);
 /* out = [relu](y*sc + sh [+ r | + r*sc2 + sh2])   res_mode 0 none, 1 identity add, 2 BN'd add */

@@ -52,6 +52,7 @@ struct IgemmArgs {
   void* y;
   int ldy, accumulate;
   const float* bias;
+  const float* escale;     // per-output-channel epilogue scale (generic kernel only; may be NULL)
   int relu;
   float* stats;            // [M tiles][2][Ng] (sum, M2 about the tile mean)
   int stats_ld;
@@ -236,7 +237,8 @@ __global__ __launch_bounds__(256) void igemm_tn_kernel(IgemmArgs a) {
         float v = acc[i][j][e];
         float vr = 0.f;
         if (mok && n < a.Ng) {
-          if (a.bias) v += a.bias[n];
+          if (a.escale) v = fmaf(v, a.escale[n], a.bias ? a.bias[n] : 0.f);  // == bn_apply's fmaf
+          else if (a.bias) v += a.bias[n];
           if (a.relu) v = fmaxf(v, 0.f);
           T* p = y + opix * a.ldy + n;
           if (a.accumulate) v += (float)(*p);
@@ -660,7 +662,7 @@ bool try_fast_tn(const IgemmArgs& a, hipStream_t st) {
 template <typename T>
 int launch_tn(IgemmArgs a, hipStream_t st) {
   if (a.M <= 0 || a.Ng <= 0) return 0;
-  if (sizeof(T) == 2 && try_fast_tn(a, st)) {
+  if (sizeof(T) == 2 && !a.escale && try_fast_tn(a, st)) {
     US_LAUNCH_CHECK("tn_fast");
     return 0;
   }
@@ -753,6 +755,26 @@ UNETSEG_API int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, 
   IgemmArgs a = fwd_args(x1, c1, ldc1, x2, c2, ldc2, n, h, w, wk, cout, r, s, stride, pad);
   a.y = y; a.ldy = ldy; a.accumulate = 0; a.bias = bias; a.relu = relu;
   a.stats = stats; a.stats_ld = ceil_div(a.M, fwd_tile_m(dtype, a));
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DT_BF16 ? launch_tn<bf16>(a, st) : launch_tn<float>(a, st);
+}
+
+// Forward conv with a per-output-channel affine epilogue: y = [relu](conv(x, wk) * escale + bias)
+// -- eval-mode BatchNorm applied on the fp32 accumulator (model.eval() conv -> BN -> ReLU,
+// model/resnet_backbone.py:58-61, model/unet_plain.py:8-15) with the same arithmetic as the separate
+// BN pass, so fp32 results match the unfolded path.  Runs the generic implicit-GEMM kernel (the
+// bf16 fast kernels take the BN scale folded into their packed weights instead).
+UNETSEG_API int unetseg_conv2d_fwd_affine(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2,
+                                          int ldc2, int n, int h, int w, const void* wk, int cout, int r, int s,
+                                          int stride, int pad, const float* escale, const float* bias, int relu,
+                                          void* y, int ldy, void* stream) {
+  US_CHECK_ARG(x1 && wk && y && escale && bias, "conv2d_fwd_affine: null pointer");
+  US_CHECK_ARG((c1 + c2) % 8 == 0 && c1 % 8 == 0, "conv2d_fwd_affine: channels must be multiples of 8");
+  US_CHECK_ARG(c2 == 0 || x2, "conv2d_fwd_affine: c2>0 needs x2");
+  US_CHECK_ARG(ldc1 % 8 == 0 && (c2 == 0 || ldc2 % 8 == 0) && ldy >= cout, "conv2d_fwd_affine: bad strides");
+  US_CHECK_ARG(dtype == DT_F32 || dtype == DT_BF16, "conv2d_fwd_affine: bad dtype");
+  IgemmArgs a = fwd_args(x1, c1, ldc1, x2, c2, ldc2, n, h, w, wk, cout, r, s, stride, pad);
+  a.y = y; a.ldy = ldy; a.accumulate = 0; a.bias = bias; a.escale = escale; a.relu = relu;
   hipStream_t st = (hipStream_t)stream;
   return dtype == DT_BF16 ? launch_tn<bf16>(a, st) : launch_tn<float>(a, st);
 }

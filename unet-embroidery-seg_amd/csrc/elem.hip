@@ -61,6 +61,21 @@ __global__ void bn_finalize_kernel(const float* part, int C, int G, long M, int 
   }
 }
 
+// eval-mode BN folded into the preceding conv: kscale = gamma / sqrt(var + eps),
+// bias = beta - mean * kscale (+ conv_bias * kscale)
+__global__ void bn_fold_kernel(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                               float eps, const float* conv_bias, float* kscale, float* bias) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  // the same float expressions as bn_eval_kernel, so the folded epilogue fmaf(acc, kscale, bias)
+  // equals the unfolded BN pass fmaf(y, scale, shift) bit for bit in fp32
+  const float inv = 1.0f / sqrtf(rvar[c] + eps);
+  const float sc = gamma[c] * inv;
+  kscale[c] = sc;
+  const float sh = beta[c] - rmean[c] * gamma[c] * inv;
+  bias[c] = conv_bias ? sh + conv_bias[c] * sc : sh;
+}
+
 __global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar,
                                float eps, float* scale, float* shift) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1126,6 +1141,15 @@ UNETSEG_API int unetseg_bn_finalize(const float* part, int C, int G, long M, int
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, C, G, M, tile, gamma, beta,
                      rmean, rvar, nbt, momentum, eps, mean, invstd, scale, shift);
   US_LAUNCH_CHECK("bn_finalize");
+  return 0;
+}
+
+UNETSEG_API int unetseg_bn_fold(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                                float eps, const float* conv_bias, float* kscale, float* bias, void* stream) {
+  US_CHECK_ARG(C > 0 && gamma && beta && rmean && rvar && kscale && bias, "bn_fold: bad args");
+  hipLaunchKernelGGL(bn_fold_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, (hipStream_t)stream, C, gamma, beta, rmean,
+                     rvar, eps, conv_bias, kscale, bias);
+  US_LAUNCH_CHECK("bn_fold");
   return 0;
 }
 

@@ -55,10 +55,8 @@ def run_bottleneck(ctx, b, x):
     yd = sd = None
     if b.downsample is not None:
         yd, sd = ops.conv(ctx, x, b.downsample[0]._pc, stats=True)
-    y1, s1 = ops.conv(ctx, x, b.conv1._pc, stats=True)
-    a1 = ops.bn(ctx, y1, s1, b.bn1, relu=True)
-    y2, s2 = ops.conv(ctx, a1, b.conv2._pc, stats=True)
-    a2 = ops.bn(ctx, y2, s2, b.bn2, relu=True)
+    a1 = ops.conv_bn(ctx, x, b.conv1._pc, b.bn1)
+    a2 = ops.conv_bn(ctx, a1, b.conv2._pc, b.bn2)
     y3, s3 = ops.conv(ctx, a2, b.conv3._pc, stats=True)
     if b.downsample is not None:
         return ops.bn(ctx, y3, s3, b.bn3, relu=True, res_bn=(yd, sd, b.downsample[1]))

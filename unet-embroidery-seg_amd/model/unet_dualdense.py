@@ -148,8 +148,7 @@ def run_dense_conv_block(ctx, blk, parts, img=None):
         pc = rc.pc
     else:
         pc = tconv._pc
-    y, st = ops.conv(ctx, buf, pc, stats=True)
-    return ops.bn(ctx, y, st, tbn, relu=True)
+    return ops.conv_bn(ctx, buf, pc, tbn)
 
 
 class DualDenseUNet(HipModel):

@@ -20,10 +20,8 @@ class DoubleConv(nn.Module):
 
 
 def run_double_conv(ctx, dc, x, x2=None):
-    y, s = ops.conv(ctx, x, dc.net[0]._pc, x2=x2, stats=True)
-    a = ops.bn(ctx, y, s, dc.net[1], relu=True)
-    y, s = ops.conv(ctx, a, dc.net[3]._pc, stats=True)
-    return ops.bn(ctx, y, s, dc.net[4], relu=True)
+    a = ops.conv_bn(ctx, x, dc.net[0]._pc, dc.net[1], x2=x2)
+    return ops.conv_bn(ctx, a, dc.net[3]._pc, dc.net[4])
 
 
 class Down(nn.Module):

@@ -32,6 +32,8 @@ def call_configs(desc, dt=DT_BF16):
     Pq, Qq = _out_hw(H, W, R, S, stride, pad)
     if d == "fwd":
         return ["fwd:" + _lib.fwd_config(dt, C1, ld1 or C1, C2, ld2 or C2, N, H, W, K, R, S, stride, pad)]
+    if d == "fwd_affine":  # eval-mode BN on the accumulator: always the generic kernel
+        return ["fwd_affine:generic"]
     if d in ("dgrad", "dgrad_post1", "dgrad_post2"):
         tag = "dgrad" if d == "dgrad" else d
         return [f"{tag}:{c}" for c in _lib.dgrad_config(dt, K, N, Pq, Qq, K, cin, R, S, stride, pad, cin, H, W)]

@@ -35,6 +35,8 @@ SIGNATURES = {
     "unetseg_pack_conv_weight": (I, [I, P, I, I, I, I, I, P, P, P]),
     "unetseg_pack_conv_weights": (I, [I, P, I, L, P]),
     "unetseg_pack_tiles": (I, [I, I, I]),
+    "unetseg_bn_fold": (I, [I, P, P, P, P, F, P, P, P, P]),
+    "unetseg_conv2d_fwd_affine": (I, [I, P, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P, P, I, P, I, P]),
     "unetseg_bn_finalize": (I, [P, I, I, L, I, P, P, P, P, P, F, F, P, P, P, P, P]),
     "unetseg_bn_eval_coeffs": (I, [I, P, P, P, P, F, P, P, P]),
     "unetseg_bn_apply": (I, [I, P, I, P, P, P, I, P, P, I, I, P, I, L, I, P]),

@@ -91,10 +91,14 @@ OVERLAP = os.environ.get("UNETSEG_NO_OVERLAP", "0") != "1"
 _SIDE = {}
 
 
+#: priority of the weight-gradient stream (torch convention: lower = higher priority)
+SIDE_PRIORITY = int(os.environ.get("UNETSEG_SIDE_PRIORITY", "0"))
+
+
 def side_stream(device):
     key = (device.type, device.index)
     if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device)
+        _SIDE[key] = torch.cuda.Stream(device, priority=SIDE_PRIORITY)
     return _SIDE[key]
 
 
@@ -276,6 +280,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None):
     M = N * Pq * Qq
     y = ctx.empty(N, Pq, Qq, K) if out is None else out
     st = None
+    stats = stats and ctx.training  # eval-mode BN normalises with the running statistics
     if stats:
         tile = lib.conv2d_fwd_tile_m(ctx.dt, C1, ldp(X1), C2, ldp(X2), N, H, W, K, R, S, stride, pad)
         st = (ctx.f32(math.ceil(M / tile), 2, K), tile)  # [row tiles][sum, M2][K]
@@ -375,6 +380,40 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None):
 
     ctx.push(bwd)
     return out, st
+
+
+#: eval-mode BatchNorm folded into the preceding conv (UNETSEG_NO_BN_FOLD=1: separate BN pass)
+BN_FOLD = os.environ.get("UNETSEG_NO_BN_FOLD", "0") != "1"
+
+
+def conv_bn(ctx, x, pc, bnm, x2=None):
+    """relu(BN(conv(cat[x, x2]))) for a conv whose only consumer is that BN (model/resnet_backbone.py:
+    58-61 bottleneck conv1/conv2, model/unet_plain.py:8-15 DoubleConv).  Training: the conv writes
+    BN partial statistics in its epilogue, then the BN-ReLU pass.  Eval in fp32 (the reference's
+    evaluate / val / predict precision; no autograd tape): BN and ReLU run in the conv's epilogue on
+    the fp32 accumulator, one launch (unetseg_conv2d_fwd_affine with unetseg_bn_fold's coefficients,
+    the same float arithmetic as the separate pass, so the result is unchanged).  bf16 eval keeps
+    the separate pass: its kernels round the conv output before BN, which is what the bf16
+    emulation in the parity tests models."""
+    if ctx.training or ctx.tape is not None or not BN_FOLD or ctx.dt != DT_F32:
+        y, st = conv(ctx, x, pc, x2=x2, stats=True)
+        return bn(ctx, y, st, bnm, relu=True)
+    K, C, R, S = pc.K, pc.C, pc.R, pc.S
+    kscale, bias = ctx.f32(K), ctx.f32(K)
+    lib.bn_fold(K, P(bnm.weight), P(bnm.bias), P(bnm.running_mean), P(bnm.running_var), bnm.eps, P(pc.conv.bias),
+                P(kscale), P(bias), ctx.stream)
+    use(x, x2)
+    X1, X2 = x.data, (x2.data if x2 is not None else None)
+    N, H, W, C1 = X1.shape
+    C2 = X2.shape[-1] if X2 is not None else 0
+    stride, pad = pc.conv.stride, pc.conv.padding
+    Pq, Qq = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+    y = ctx.empty(N, Pq, Qq, K)
+    desc = (N, H, W, C1, C2, K, R, S, stride, pad, ldp(X1), ldp(X2))
+    with _probe("igemm_tn", 2.0 * N * Pq * Qq * K * C * R * S, 1, ("fwd_affine",) + desc):
+        lib.conv2d_fwd_affine(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride, pad,
+                              P(kscale), P(bias), 1, P(y), K, ctx.stream)
+    return Node(y)
 
 
 def _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
