@@ -66,6 +66,17 @@ int unetseg_conv2d_fwd_tile_m(int dtype, int c1, int ldc1, int c2, int ldc2, int
 int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h,
                        int w, const void* wk, int cout, int r, int s, int stride, int pad, const float* bias, int relu,
                        void* y, int ldy, float* stats, void* stream);
+/* 1x1 stride-1 conv reading relu(x1 * in_sc[c] + in_sh[c]) -- the producer's BN-ReLU output, never
+ * stored (model/resnet_backbone.py:58-62 bn2 -> ReLU -> conv3); epilogue as unetseg_conv2d_fwd. bf16 */
+int unetseg_conv2d_fwd_bnrelu_in(int dtype, const void* x1, int c1, int ldc1, int n, int h, int w, const void* wk,
+                                 int cout, const float* in_sc, const float* in_sh, const float* bias, int relu,
+                                 void* y, int ldy, float* stats, void* stream);
+/* TN configuration that call runs (host-only query, -1 = none) */
+int unetseg_conv2d_fwd_bnrelu_in_config(int dtype, int c1, int ldc1, int n, int h, int w, int cout);
+/* its weight gradient with the same input prologue (workspace: unetseg_conv2d_wgrad_workspace) */
+int unetseg_conv2d_wgrad_bnrelu_in(int dtype, const void* x1, int c1, int ldc1, int n, int h, int w, const void* dy,
+                                   int ldy, int cout, const float* in_sc, const float* in_sh, float* ws,
+                                   size_t ws_bytes, float* dw, int dw_c, int accumulate, void* stream);
 /* y = [relu](conv(x, wk) * escale[cout] + bias[cout]): eval-mode BN on the accumulator (generic kernel) */
 int unetseg_conv2d_fwd_affine(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n,
                               int h, int w, const void* wk, int cout, int r, int s, int stride, int pad,

@@ -102,6 +102,17 @@ CASES = {
     "wgrad128_s2": ("wgrad", (16, 32, 32, 512, 0, 512, 3, 2), ["wgrad:wgrad128", None]),
     "wgrad128_r16_16x16": ("wgrad", (16, 16, 16, 2048, 0, 512, 1, 1), ["wgrad:wgrad128", None]),
     "wgrad64x256_row": ("wgrad", (16, 128, 128, 256, 0, 64, 1, 1), ["wgrad:wgrad64x256_row", "reduce16"]),
+    # bottleneck conv3 reading bn2-ReLU on load (ops.bn(lazy=True), unetseg_conv2d_*_bnrelu_in)
+    "bnin_tn128x128_1step": ("fwd_bnrelu_in", (16, 128, 128, 64, 0, 256, 1, 1), ["fwd_bnrelu_in:tn128x128_1step"]),
+    "bnin_tn128x128": ("fwd_bnrelu_in", (16, 64, 64, 128, 0, 512, 1, 1), ["fwd_bnrelu_in:tn128x128"]),
+    "bnin_tn128x128_k256": ("fwd_bnrelu_in", (16, 32, 32, 256, 0, 1024, 1, 1), ["fwd_bnrelu_in:tn128x128"]),
+    "bnin_tn256x128": ("fwd_bnrelu_in", (16, 16, 16, 512, 0, 2048, 1, 1), ["fwd_bnrelu_in:tn256x128"]),
+    "bnin_tn64x128": ("fwd_bnrelu_in", (1, 16, 16, 512, 0, 2048, 1, 1), ["fwd_bnrelu_in:tn64x128"]),
+    "bnin_ragged": ("fwd_bnrelu_in", (1, 15, 17, 64, 0, 256, 1, 1), None),
+    "bnin_wgrad_row_r16": ("wgrad_bnrelu_in", (16, 128, 128, 64, 0, 256, 1, 1), ["wgrad_bnrelu_in:wgrad128_row", "reduce16"]),
+    "bnin_wgrad_row_r4": ("wgrad_bnrelu_in", (1, 64, 64, 128, 0, 512, 1, 1), ["wgrad_bnrelu_in:wgrad128_row", "reduce4"]),
+    "bnin_wgrad_16x16": ("wgrad_bnrelu_in", (16, 16, 16, 512, 0, 2048, 1, 1), ["wgrad_bnrelu_in:wgrad128", None]),
+    "bnin_wgrad_ragged": ("wgrad_bnrelu_in", (1, 15, 17, 64, 0, 256, 1, 1), None),
 }
 
 
@@ -157,7 +168,8 @@ def _key_list(direction, shape):
     from unetseg_hip import introspect
     N, H, W, C1, C2, K, R, s = shape
     d = {"fwd_relu": "fwd", "fwd_stats": "fwd", "fwd_all": "fwd", "dgrad": "dgrad", "post1": "dgrad_post1",
-         "post2": "dgrad_post2", "wgrad": "wgrad"}[direction]
+         "post2": "dgrad_post2", "wgrad": "wgrad", "fwd_bnrelu_in": "fwd_bnrelu_in",
+         "wgrad_bnrelu_in": "wgrad_bnrelu_in"}[direction]
     return introspect.call_configs((d, N, H, W, C1, C2, K, R, R, s, R // 2, C1, C2))
 
 
@@ -223,6 +235,9 @@ def test_config_case(cid):
     x64, w64, dy64 = op.x.double(), op.w32.double(), op.dy.double()
     wk, wt = op.packed()
     st = _st()
+    if direction.endswith("bnrelu_in"):
+        _bnrelu_in_case(cid, direction, shape, op, wk, lib, st)
+        return
     if direction.startswith("fwd"):
         x1, x2 = op.x_parts()
         relu = direction in ("fwd_relu", "fwd_all")
@@ -319,6 +334,52 @@ def test_config_case(cid):
     lib.conv2d_wgrad(DT_BF16, _P(x1), C1, C1, _P(x2), C2, C2, N, H, W, _P(dyh), K, K, R, R, s, pad, _P(ws), ws_bytes,
                      _P(dw), cin, 1, st)
     assert torch.equal(dw, dw1 + dw1), f"{cid}: accumulated wgrad is not 2x the first (non-deterministic reduce?)"
+
+
+def _bnrelu_in_case(cid, direction, shape, op, wk, lib, st):
+    """x1 = z (the producer's BN input); the conv must read a = bf16(relu(fmaf(z, sc, sh))), as the
+    bn_apply pass would have stored it.  fwd: output and BN partials vs the float64 conv of a;
+    wgrad: dW vs the float64 reference and bit-equal to the plain wgrad of the materialised a."""
+    from unetseg_hip.lib import DT_BF16
+    N, H, W, C1, C2, K, R, s = shape
+    z = _nhwc(op.x)
+    sc = (1 + 0.3 * torch.randn(C1, generator=op.gen, device=DEV)).float()
+    sh = (0.3 * torch.randn(C1, generator=op.gen, device=DEV)).float()
+    # fmaf(z, sc, sh) = the exact value rounded once to fp32 (exact in float64: 8 x 24-bit product)
+    a = torch.relu((z.double() * sc.double() + sh.double()).float()).to(torch.bfloat16)
+    a64 = _nchw(a)
+    if direction == "fwd_bnrelu_in":
+        M = N * H * W
+        tile = lib.conv2d_fwd_tile_m(DT_BF16, C1, C1, 0, 0, N, H, W, K, 1, 1, 1, 0)
+        G = -(-M // tile)
+        stt = torch.empty(G, 2, K, dtype=torch.float32, device=DEV)
+        y = torch.empty(N, H, W, K, dtype=torch.bfloat16, device=DEV)
+        lib.conv2d_fwd_bnrelu_in(DT_BF16, _P(z), C1, C1, N, H, W, _P(wk), K, _P(sc), _P(sh), 0, 0, _P(y), K, _P(stt),
+                                 st)
+        ref = _ref_fwd(a64, op.w32.double(), 1, 0)
+        out = _nchw(y)
+        _check_bf16(out, ref, f"{cid} y")
+        # same values as the unfused conv of the stored activation
+        y2 = torch.empty_like(y)
+        st2 = torch.empty_like(stt)
+        lib.conv2d_fwd(DT_BF16, _P(a), C1, C1, 0, 0, 0, N, H, W, _P(wk), K, 1, 1, 1, 0, 0, 0, _P(y2), K, _P(st2), st)
+        torch.testing.assert_close(y.float(), y2.float(), rtol=0, atol=0)
+        torch.testing.assert_close(stt, st2, rtol=1e-6, atol=1e-5)
+        return
+    dyh = _nhwc(op.dy)
+    ws_bytes = lib.conv2d_wgrad_workspace(DT_BF16, N, H, W, K, C1, 1, 1)
+    ws = torch.empty(max(ws_bytes, 1) // 4 + 1, dtype=torch.float32, device=DEV)
+    dw = torch.empty(K, C1, 1, 1, dtype=torch.float32, device=DEV)
+    lib.conv2d_wgrad_bnrelu_in(DT_BF16, _P(z), C1, C1, N, H, W, _P(dyh), K, K, _P(sc), _P(sh), _P(ws), ws_bytes, _P(dw),
+                               C1, 0, st)
+    ref = _ref_wgrad(a64, op.dy.double(), 1, 1, 0)
+    m = ref.abs().max().item()
+    err = (dw.double() - ref).abs()
+    assert int((err > 1e-3 * ref.abs() + 2e-5 * m).sum()) == 0, f"{cid}: max err {err.max().item():.3e}"
+    dw2 = torch.empty_like(dw)
+    lib.conv2d_wgrad(DT_BF16, _P(a), C1, C1, 0, 0, 0, N, H, W, _P(dyh), K, K, 1, 1, 1, 0, _P(ws), ws_bytes, _P(dw2), C1,
+                     0, st)
+    assert torch.equal(dw, dw2), f"{cid}: fused wgrad differs from the wgrad of the stored activation"
 
 
 @pytest.mark.parametrize("N,H", [(16, 512), (2, 200)])

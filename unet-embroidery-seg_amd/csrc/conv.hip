@@ -53,6 +53,8 @@ struct IgemmArgs {
   int ldy, accumulate;
   const float* bias;
   const float* escale;     // per-output-channel epilogue scale (generic kernel only; may be NULL)
+  const float* in_sc;      // input BN-ReLU prologue (fast register-staged kernels only; may be NULL)
+  const float* in_sh;
   int relu;
   float* stats;            // [M tiles][2][Ng] (sum, M2 about the tile mean)
   int stats_ld;
@@ -649,6 +651,7 @@ bool fast_tn_args(const IgemmArgs& a, FastTNArgs& f) {
   f.ostride = a.ostride; f.ph = a.ph; f.pw = a.pw; f.OH = a.OH; f.OW = a.OW;
   f.y = a.y; f.ldy = a.ldy; f.accumulate = a.accumulate; f.bias = a.bias; f.relu = a.relu;
   f.stats = a.stats; f.stats_ld = a.stats_ld; f.M = a.M;
+  f.in_sc = a.in_sc; f.in_sh = a.in_sh;
   return tn_fast_ok(f);
 }
 
@@ -666,6 +669,7 @@ int launch_tn(IgemmArgs a, hipStream_t st) {
     US_LAUNCH_CHECK("tn_fast");
     return 0;
   }
+  US_CHECK_ARG(!a.in_sc, "conv: the BN-ReLU input prologue needs the fast bf16 path");
   dim3 grid(ceil_div(a.M, kBM), 1, 1);
   if (a.Ng <= 64) {
     grid.y = ceil_div(a.Ng, 64);
@@ -757,6 +761,82 @@ UNETSEG_API int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, 
   a.stats = stats; a.stats_ld = ceil_div(a.M, fwd_tile_m(dtype, a));
   hipStream_t st = (hipStream_t)stream;
   return dtype == DT_BF16 ? launch_tn<bf16>(a, st) : launch_tn<float>(a, st);
+}
+
+static bool wgrad_fast_eligible(int dtype, int q, int cin, int cout);
+
+// Forward 1x1 / stride-1 conv whose input is the BN-ReLU output of the producer, never
+// materialised: x1 holds the BN input z and the conv stages relu(z * in_sc[c] + in_sh[c]) (the
+// bn_apply arithmetic, rounded to bf16) between its global loads and LDS stores -- the ResNet
+// bottleneck's bn2 -> ReLU -> conv3 (model/resnet_backbone.py:58-62).  bf16 only, single source,
+// register-staged fast configurations; epilogue as unetseg_conv2d_fwd (bias, ReLU, BN partials of
+// its own output with the same row tile).
+UNETSEG_API int unetseg_conv2d_fwd_bnrelu_in(int dtype, const void* x1, int c1, int ldc1, int n, int h, int w,
+                                             const void* wk, int cout, const float* in_sc, const float* in_sh,
+                                             const float* bias, int relu, void* y, int ldy, float* stats,
+                                             void* stream) {
+  US_CHECK_ARG(dtype == DT_BF16, "conv2d_fwd_bnrelu_in: bf16 only");
+  US_CHECK_ARG(x1 && wk && y && in_sc && in_sh, "conv2d_fwd_bnrelu_in: null pointer");
+  US_CHECK_ARG(c1 % 64 == 0 && ldc1 % 8 == 0 && ldy >= cout && c1 <= 2048, "conv2d_fwd_bnrelu_in: bad channels");
+  IgemmArgs a = fwd_args(x1, c1, ldc1, nullptr, 0, 0, n, h, w, wk, cout, 1, 1, 1, 0);
+  a.y = y; a.ldy = ldy; a.accumulate = 0; a.bias = bias; a.relu = relu;
+  a.stats = stats; a.stats_ld = ceil_div(a.M, fwd_tile_m(dtype, a));
+  a.in_sc = in_sc; a.in_sh = in_sh;
+  FastTNArgs f;
+  US_CHECK_ARG(fast_tn_args(a, f), "conv2d_fwd_bnrelu_in: shape has no fast path");
+  US_CHECK_ARG(launch_tn_fast(f, (hipStream_t)stream) == 0, "conv2d_fwd_bnrelu_in: no register-staged tile");
+  US_LAUNCH_CHECK("tn_fast_bnrelu_in");
+  return 0;
+}
+
+// configuration unetseg_conv2d_fwd_bnrelu_in runs for this shape (host only; -1: no fast path)
+UNETSEG_API int unetseg_conv2d_fwd_bnrelu_in_config(int dtype, int c1, int ldc1, int n, int h, int w, int cout) {
+  IgemmArgs a = fwd_args(kSomePtr, c1, ldc1, nullptr, 0, 0, n, h, w, kSomePtr, cout, 1, 1, 1, 0);
+  a.ldy = cout;
+  static const float kOne = 1.f;
+  a.in_sc = a.in_sh = &kOne;
+  FastTNArgs f;
+  if (dtype != DT_BF16 || !fast_tn_args(a, f)) return -1;
+  return tn_fast_config(f, nullptr);
+}
+
+// Weight gradient of that conv: X = relu(x1 * in_sc + in_sh) staged on the fly (fast bf16 wgrad),
+// then the usual deterministic split-K reduce into dw (fp32 [cout][dw_c], (+)= with accumulate).
+UNETSEG_API int unetseg_conv2d_wgrad_bnrelu_in(int dtype, const void* x1, int c1, int ldc1, int n, int h, int w,
+                                               const void* dy, int ldy, int cout, const float* in_sc,
+                                               const float* in_sh, float* ws, size_t ws_bytes, float* dw, int dw_c,
+                                               int accumulate, void* stream) {
+  US_CHECK_ARG(dtype == DT_BF16, "conv2d_wgrad_bnrelu_in: bf16 only");
+  US_CHECK_ARG(x1 && dy && ws && dw && in_sc && in_sh, "conv2d_wgrad_bnrelu_in: null pointer");
+  US_CHECK_ARG(c1 % 8 == 0 && cout % 64 == 0 && ldy % 8 == 0 && dw_c > 0 && dw_c <= c1,
+               "conv2d_wgrad_bnrelu_in: bad channels");
+  const long pix = (long)n * h * w;
+  const long b1 = pix * ldc1 * 2, bdy = pix * ldy * 2;
+  US_CHECK_ARG(b1 < (1L << 31) && bdy < (1L << 31) && wgrad_fast_eligible(dtype, w, c1, cout),
+               "conv2d_wgrad_bnrelu_in: shape has no fast path");
+  FastWgradArgs f{};
+  f.x1 = x1; f.x2 = nullptr; f.x1_bytes = (unsigned)b1; f.x2_bytes = 0u;
+  f.ldc1b = ldc1 * 2; f.ldc2b = 0; f.c1 = c1; f.cin = c1;
+  f.H = h; f.W = w; f.P = h; f.Q = w; f.stride = 1; f.pad = 0; f.padw = 0; f.S = 1;
+  f.dy = dy; f.dy_bytes = (unsigned)bdy; f.ldyb = ldy * 2; f.Cout = cout; f.Ng = c1; f.Kpix = pix;
+  f.ws = ws; f.in_sc = in_sc; f.in_sh = in_sh;
+  const int splits = wgrad_fast_splits(cout, c1, pix);
+  US_CHECK_ARG(ws_bytes >= (size_t)splits * cout * c1 * sizeof(float), "conv2d_wgrad_bnrelu_in: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  launch_wgrad_fast(f, splits, st);
+  US_LAUNCH_CHECK("wgrad_fast_bnrelu_in");
+  const long total = (long)cout * dw_c;
+  if (splits >= 16)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(ceil_div(total, 16)), dim3(256), 0, st, ws, splits, cout, c1, 1,
+                       dw, dw_c, accumulate);
+  else if (splits >= 4)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(ceil_div(total, 64)), dim3(256), 0, st, ws, splits, cout, c1, 1,
+                       dw, dw_c, accumulate);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(ceil_div(total, 256)), dim3(256), 0, st, ws, splits, cout, c1, 1,
+                       dw, dw_c, accumulate);
+  US_LAUNCH_CHECK("wgrad_reduce");
+  return 0;
 }
 
 // Forward conv with a per-output-channel affine epilogue: y = [relu](conv(x, wk) * escale + bias)

@@ -39,6 +39,10 @@ struct FastTNArgs {
   const float* pinv;
   float* ppart;
   int t2d;  // rows of a 2D spatial tile (BM = t2d x 32 pixels), 0 = row-major GEMM rows (set by the launcher)
+  // input prologue: x1 is the producer's BN input z, the conv reads relu(z * in_sc[c] + in_sh[c])
+  // (its BN-ReLU output, never materialised); register-staged configurations only, x2 == NULL
+  const float* in_sc;
+  const float* in_sh;
 };
 
 struct FastWgradArgs {
@@ -54,6 +58,8 @@ struct FastWgradArgs {
   long Kpix;
   int kt_per_split;
   float* ws;
+  const float* in_sc;  // as FastTNArgs: X = relu(x1 * in_sc[c] + in_sh[c]) on load (x2 == NULL)
+  const float* in_sh;
 };
 
 // 3x3 / stride 1 / pad 1 weight gradient on the halo path (conv_halo.hip)

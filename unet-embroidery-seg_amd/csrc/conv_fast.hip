@@ -32,12 +32,23 @@ namespace {
 template <int BM, int BN, int NWM, int NWN>
 constexpr int tn_waves_per_simd() { return (BM == 64 || (BM == 128 && BN == 64)) ? 3 : 2; }
 
+// byte offset of the input-prologue coefficients in the TN kernel's dynamic LDS: after the operand
+// stages or the epilogue's transpose tiles + stats scratch, whichever is larger
+template <int BM, int BN, int NWM, int NWN, int ST>
+constexpr size_t kPreOff() {
+  constexpr size_t stages = (size_t)(ST == 1 ? 1 : ST >= 13 ? ST - 10 : 2) * (BM + BN) * 8 * 16;
+  constexpr size_t epi = (size_t)NWM * NWN * 64 * ((BN / NWN) * 2 + 16) + 2 * NWM * BN * 4;
+  return ((stages > epi ? stages : epi) + 15) / 16 * 16;
+}
+
 // TAPS (LDS-DMA ring only): the filter has exactly TAPS = nr x ns taps, known at compile time.  The
 // K loop is then unrolled over the taps and every (row, tap) gather offset is precomputed, so a K
 // step issues its loads with one multiply-add per row and a scalar channel offset (the generic
 // ring re-derives tap deltas, validity masks and offsets every step: ~70 VALU + ~90 SALU per step
 // on the 256x128 tile, which is what held its MFMA pipe at ~45 % busy).
-template <int BM, int BN, int NWM, int NWN, int ST, bool POST, int TAPS = 0>
+// PRE: the input prologue of FastTNArgs (x1 = BN input z, staged as relu(z*in_sc + in_sh) between the
+// global load and the LDS store); the per-channel coefficients sit in LDS after the tile stages.
+template <int BM, int BN, int NWM, int NWN, int ST, bool POST, int TAPS = 0, bool PRE = false>
 __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN>())) void tn_fast_kernel(FastTNArgs a) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int WTM = BM / NWM, WTN = BN / NWN;
@@ -47,6 +58,7 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
   extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // [2 or NS][(BM+BN)*8]
   constexpr int STAGE = (BM + BN) * 8;
   constexpr bool kDMA = ST >= 13;
+  static_assert(!(PRE && kDMA), "the input prologue needs register staging");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -154,7 +166,8 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
   // zeros without touching memory.  Issuing them anyway keeps the loop free of conditional loads,
   // which lets hipcc count vmcnt exactly (with conditional loads it waits for the loads of the
   // step in flight too, exposing their latency every K step).
-  auto gload = [&](uint4 (&ra)[A_PER], uint4 (&rbv)[B_PER], bool live = true) {
+  auto gload = [&](uint4 (&ra)[A_PER], uint4 (&rbv)[B_PER], int& kc, bool live = true) {
+    kc = s_c;  // channel base of this K step (input prologue)
     const int dh = a.dh0 + a.dhs * s_jr, dw = a.dw0 + a.dws * s_js;
     const int tapbit = (s_jr * a.ns + s_js) & 31;
     const int tapdelta = dh * a.W + dw;
@@ -188,12 +201,36 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
       }
     }
   };
-  auto sstore = [&](int buf, const uint4 (&ra)[A_PER], const uint4 (&rbv)[B_PER]) {
+  // input prologue coefficients: [2][cin] floats after the operand stages / epilogue scratch
+  const float* pre_l = reinterpret_cast<const float*>(lds + kPreOff<BM, BN, NWM, NWN, ST>() / 16);
+  if constexpr (PRE) {
+    float* w = reinterpret_cast<float*>(lds + kPreOff<BM, BN, NWM, NWN, ST>() / 16);
+    for (int c = tid; c < a.c1; c += NT) {
+      w[c] = a.in_sc[c];
+      w[a.c1 + c] = a.in_sh[c];
+    }
+    __syncthreads();
+  }
+  auto sstore = [&](int buf, const uint4 (&ra)[A_PER], const uint4 (&rbv)[B_PER], int kc) {
     uint4* L = lds + buf * STAGE;
+    float psc[8], psh[8];
+    if constexpr (PRE) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        psc[e] = pre_l[kc + kv * 8 + e];
+        psh[e] = pre_l[a.c1 + kc + kv * 8 + e];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int row = rb + RSTEP * i;
-      L[row * 8 + swz8(row, kv)] = ra[i];
+      uint4 v = ra[i];
+      if constexpr (PRE) {  // == bn_apply: (bf16) relu(fmaf(z, sc, sh))
+        bf16* e8 = reinterpret_cast<bf16*>(&v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) e8[e] = (bf16)fmaxf(fmaf((float)e8[e], psc[e], psh[e]), 0.f);
+      }
+      L[row * 8 + swz8(row, kv)] = v;
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
@@ -323,47 +360,50 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
     // every DMA (past-the-end ones write zeros) has landed before the epilogue reuses the LDS
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   } else if (ST == 1) {  // one K step
+    int kc0 = 0;
     if (nsteps > 0) {
-      gload(ra0, rb0);
-      sstore(0, ra0, rb0);
+      gload(ra0, rb0, kc0);
+      sstore(0, ra0, rb0, kc0);
       __syncthreads();
       compute(0);
     }
     __syncthreads();
   } else if (ST == 2) {  // loads one step ahead (one register set)
+    int kc0 = 0;
     if (nsteps > 0) {
-      gload(ra0, rb0);
-      sstore(0, ra0, rb0);
+      gload(ra0, rb0, kc0);
+      sstore(0, ra0, rb0, kc0);
       __syncthreads();
     }
     for (int kt = 0; kt < nsteps; ++kt) {
       const int cur = kt & 1;
-      if (kt + 1 < nsteps) gload(ra0, rb0);
+      if (kt + 1 < nsteps) gload(ra0, rb0, kc0);
       compute(cur);
-      if (kt + 1 < nsteps) sstore(cur ^ 1, ra0, rb0);
+      if (kt + 1 < nsteps) sstore(cur ^ 1, ra0, rb0, kc0);
       __syncthreads();
     }
   } else {  // ST == 3: loads two steps ahead (two register sets)
     // Loads and LDS stores are unconditional inside the loop (past-the-end steps load zeros), so
     // the in-order vmcnt bookkeeping is the same on every path: each sstore waits only for the
     // register set it writes, while the set issued in the same half stays in flight.
+    int kc0 = 0, kc1 = 0;
     if (nsteps > 0) {
-      gload(ra0, rb0);
-      sstore(0, ra0, rb0);
-      gload(ra1, rb1, nsteps > 1);
+      gload(ra0, rb0, kc0);
+      sstore(0, ra0, rb0, kc0);
+      gload(ra1, rb1, kc1, nsteps > 1);
       __syncthreads();
     }
     for (int kt = 0; kt < nsteps; kt += 2) {
       // even step: stage 0 holds kt, registers 1 hold kt+1 (in flight)
-      gload(ra0, rb0, kt + 2 < nsteps);
+      gload(ra0, rb0, kc0, kt + 2 < nsteps);
       compute(0);
-      sstore(1, ra1, rb1);
+      sstore(1, ra1, rb1, kc1);
       __syncthreads();
       if (kt + 1 >= nsteps) break;
       // odd step: stage 1 holds kt+1, registers 0 hold kt+2 (in flight)
-      gload(ra1, rb1, kt + 3 < nsteps);
+      gload(ra1, rb1, kc1, kt + 3 < nsteps);
       compute(1);
-      sstore(0, ra0, rb0);
+      sstore(0, ra0, rb0, kc0);
       __syncthreads();
     }
   }
@@ -582,7 +622,9 @@ constexpr int kWgBK = 32;  // 64 halves the barriers but costs a wave per SIMD: 
 // first column) is wave-uniform scalar state and each staged row's offset is a scalar base plus a
 // per-lane constant (tap shift, column, channel): a few VALU per row instead of re-deriving the
 // pixel, its bounds and its 32-bit offset every step.
-template <int BM, int BN, int NWM, int NWN, bool ROW32 = false>
+// PRE: X = relu(x1 * in_sc[c] + in_sh[c]) for the rows that exist (padding / past-the-end rows
+// stay zero); each thread's 8 channels are fixed, so their coefficients live in registers.
+template <int BM, int BN, int NWM, int NWN, bool ROW32 = false, bool PRE = false>
 __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArgs a) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int BKW = kWgBK;
@@ -646,6 +688,20 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     b_q[i] = rem - b_p[i] * a.Q;
   }
   const unsigned a_colb0 = (unsigned)m0 * 2u;
+  float pre_sc[PRE ? B_PER : 1][8], pre_sh[PRE ? B_PER : 1][8];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int nn = n0 + b_cv[i] * 8;
+      const int c = nn < a.Ng ? nn % a.cin : 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        pre_sc[i][e] = nn < a.Ng ? a.in_sc[c + e] : 0.f;
+        pre_sh[i][e] = nn < a.Ng ? a.in_sh[c + e] : 0.f;
+      }
+    }
+  }
+  unsigned b_okm = 0u;  // rows of the staged X set that exist (PRE)
 
   uint4 ra[A_PER], rbv[B_PER];
   // ---- ROW32 addressing: lane constants and scalar (image, row, column) of the next K step ----
@@ -679,9 +735,11 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     const int ihb = s_p * a.stride, iwb = s_q * a.stride;
     const int pixb = (s_n * a.H + ihb) * a.W + iwb;
     const unsigned base1 = (unsigned)pixb * (unsigned)a.ldc1b, base2 = (unsigned)pixb * (unsigned)a.ldc2b;
+    b_okm = 0u;
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const bool ok = (unsigned)(ihb + b_dh[i]) < (unsigned)a.H && (unsigned)(iwb + b_lw[i]) < (unsigned)a.W;
+      b_okm |= ok ? 1u << i : 0u;
       if (b_src[i] == 0)
         rbv[i] = bload(r1, ok ? base1 + b_l1[i] : kOOB);
       else
@@ -702,6 +760,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
       return;
     }
     const long k0 = kt * BKW;  // first pixel of the step (uniform)
+    b_okm = 0u;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const long k = k0 + a_row[i];
@@ -714,6 +773,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
       const int ih = b_p[i] * a.stride + b_dh[i];
       const int iw = b_q[i] * a.stride + b_dw[i];
       const bool ok = (k0 + b_row[i]) < a.Kpix && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      b_okm |= ok ? 1u << i : 0u;
       const unsigned pixi = (unsigned)((b_n[i] * a.H + ih) * a.W + iw);
       if (b_src[i] == 0)
         rbv[i] = bload(r1, ok ? pixi * (unsigned)a.ldc1b + b_cb[i] : kOOB);
@@ -745,7 +805,15 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     for (int i = 0; i < B_PER; ++i) {
       const int row = b_row[i];
       const int sw = CPB >= 16 ? swz_tr16(row) : swz_tr8(row);
-      L[BKW * CPA + row * CPB + (b_cv[i] ^ sw)] = rbv[i];
+      uint4 v = rbv[i];
+      if constexpr (PRE) {  // == bn_apply: (bf16) relu(fmaf(z, sc, sh)); absent rows stay zero
+        if ((b_okm >> i) & 1u) {
+          bf16* e8 = reinterpret_cast<bf16*>(&v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) e8[e] = (bf16)fmaxf(fmaf((float)e8[e], pre_sc[i][e], pre_sh[i][e]), 0.f);
+        }
+      }
+      L[BKW * CPA + row * CPB + (b_cv[i] ^ sw)] = v;
     }
   };
 
@@ -826,17 +894,18 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     }
 }
 
-template <int BM, int BN, int NWM, int NWN, int ST, bool POST = false, int TAPS = 0>
+template <int BM, int BN, int NWM, int NWN, int ST, bool POST = false, int TAPS = 0, bool PRE = false>
 int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   constexpr int NT = 64 * NWM * NWN;
-  // operand stages, or the epilogue's per-wave transpose tiles + stats scratch if larger
-  const size_t stages = (size_t)(ST == 1 ? 1 : ST >= 13 ? ST - 10 : 2) * (BM + BN) * 8 * 16;
-  const size_t epi = (size_t)NWM * NWN * 64 * ((BN / NWN) * 2 + 16) + 2 * NWM * BN * 4;
-  const size_t lds = stages > epi ? stages : epi;
+  // operand stages, or the epilogue's per-wave transpose tiles + stats scratch if larger; then the
+  // input-prologue coefficients (PRE)
+  constexpr size_t kMaxPre = 2 * 2048 * 4;
+  const size_t lds = kPreOff<BM, BN, NWM, NWN, ST>() + (PRE ? (size_t)2 * a.c1 * 4 : 0);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_fast_kernel<BM, BN, NWM, NWN, ST, POST, TAPS>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_fast_kernel<BM, BN, NWM, NWN, ST, POST, TAPS, PRE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(kPreOff<BM, BN, NWM, NWN, ST>() + (PRE ? kMaxPre : 0)));
     attr = true;
   }
   dim3 grid(ceil_div(a.M, BM), ceil_div(a.Ng, BN), 1);
@@ -845,7 +914,7 @@ int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   // 2D spatial tiles measured slower than row-major tiles with the chunk-outer K order: opt-in
   static const bool t2d = getenv("UNETSEG_T2D") != nullptr;
   b.t2d = (t2d && a.nr * a.ns > 1 && a.wc % 32 == 0 && a.wc > 32 && a.hc % TR == 0) ? TR : 0;
-  hipLaunchKernelGGL((tn_fast_kernel<BM, BN, NWM, NWN, ST, POST, TAPS>), grid, dim3(NT), lds, st, b);
+  hipLaunchKernelGGL((tn_fast_kernel<BM, BN, NWM, NWN, ST, POST, TAPS, PRE>), grid, dim3(NT), lds, st, b);
   return 0;
 }
 
@@ -879,12 +948,14 @@ static int launch_tn_dma(const FastTNArgs& a, hipStream_t st) {
 // (3 stages) beats the register-staged 256x128 by 3-8 % on every large layer; the 64x128 ring (4
 // stages) is 15 % faster on deep-K small-M layers (3x3 at 16x16, 72 K steps) but slower on short K.
 static int tn_config(const FastTNArgs& a) {
-  if (const char* e = getenv("UNETSEG_TN_CFG")) {  // experiments: force a configuration (1..10)
+  if (const char* e = getenv("UNETSEG_TN_CFG")) {  // experiments: force a configuration (1..14)
     const int c = atoi(e);
-    if (c >= 1 && c <= 14) return c;
+    if (c >= 1 && c <= 14 && !(a.in_sc && c >= 7)) return c;
   }
-  static const bool no_dma = getenv("UNETSEG_TN_NO_DMA") != nullptr;
-  if (halo3_ok(a)) return 0;
+  static const bool no_dma_env = getenv("UNETSEG_TN_NO_DMA") != nullptr;
+  // the input prologue transforms registers between load and LDS store: register-staged tiles only
+  const bool no_dma = no_dma_env || a.in_sc != nullptr;
+  if (!a.in_sc && halo3_ok(a)) return 0;
   const int nsteps = a.nr * a.ns * (a.cin >> 6);
   if (nsteps == 1 && a.Ng > 64) return 4;
   // 128x64 (two-step prefetch, 3 blocks/CU): 5-10 % over 256x64; deep 3x3 K on the 3-stage ring
@@ -937,6 +1008,17 @@ int tn_fast_config(const FastTNArgs& a, int* taps_out) {
 
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
   if (a.M <= 0 || a.Ng <= 0) return 0;
+  if (a.in_sc) {  // input prologue (fwd only: no post-op), register-staged configurations
+    switch (tn_config(a)) {
+      case 1: return launch_tn_cfg<256, 64, 4, 1, 2, false, 0, true>(a, st);
+      case 2: return launch_tn_cfg<256, 128, 4, 2, 3, false, 0, true>(a, st);
+      case 4: return launch_tn_cfg<128, 128, 2, 2, 1, false, 0, true>(a, st);
+      case 5: return launch_tn_cfg<64, 128, 1, 4, 3, false, 0, true>(a, st);
+      case 6: return launch_tn_cfg<128, 64, 2, 2, 3, false, 0, true>(a, st);
+      case 3: return launch_tn_cfg<128, 128, 2, 2, 3, false, 0, true>(a, st);
+      default: return -1;
+    }
+  }
   switch (tn_config(a)) {
     case 0: return launch_halo3(a, st);
     case 1: return a.post ? launch_tn_cfg<256, 64, 4, 1, 2, true>(a, st) : launch_tn_cfg<256, 64, 4, 1, 2>(a, st);
@@ -975,17 +1057,17 @@ int wgrad_fast_splits(int Cout, int Ng, long Kpix) {
   return sp;
 }
 
-template <int BM, int BN, int NWM, int NWN, bool ROW32>
+template <int BM, int BN, int NWM, int NWN, bool ROW32, bool PRE = false>
 static void launch_wgrad_cfg(const FastWgradArgs& a, int splits, hipStream_t st) {
   const size_t lds = 2 * (size_t)kWgBK * (BM / 8 + BN / 8) * 16;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_fast_kernel<BM, BN, NWM, NWN, ROW32>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_fast_kernel<BM, BN, NWM, NWN, ROW32, PRE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   dim3 grid(ceil_div(a.Cout, BM), ceil_div(a.Ng, BN), splits);
-  hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN, NWM, NWN, ROW32>), grid, dim3(64 * NWM * NWN), lds, st, a);
+  hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN, NWM, NWN, ROW32, PRE>), grid, dim3(64 * NWM * NWN), lds, st, a);
 }
 
 int launch_wgrad_fast(FastWgradArgs a, int splits, hipStream_t st) {
@@ -995,6 +1077,16 @@ int launch_wgrad_fast(FastWgradArgs a, int splits, hipStream_t st) {
   // ROW32: every K step is one 32-pixel run of an output row, and the per-lane pixel deltas and
   // scalar bases fit 32-bit offsets (the caller bounds both tensors below 2^31 bytes)
   const bool row32 = !no_row && a.Q % kWgBK == 0;
+  if (a.in_sc) {
+    if (a.Cout <= 64) {
+      if (row32) launch_wgrad_cfg<64, 256, 1, 4, true, true>(a, splits, st);
+      else launch_wgrad_cfg<64, 256, 1, 4, false, true>(a, splits, st);
+    } else {
+      if (row32) launch_wgrad_cfg<128, 128, 2, 2, true, true>(a, splits, st);
+      else launch_wgrad_cfg<128, 128, 2, 2, false, true>(a, splits, st);
+    }
+    return 0;
+  }
   if (a.Cout <= 64) {
     if (row32) launch_wgrad_cfg<64, 256, 1, 4, true>(a, splits, st);
     else launch_wgrad_cfg<64, 256, 1, 4, false>(a, splits, st);

@@ -56,7 +56,7 @@ def run_bottleneck(ctx, b, x):
     if b.downsample is not None:
         yd, sd = ops.conv(ctx, x, b.downsample[0]._pc, stats=True)
     a1 = ops.conv_bn(ctx, x, b.conv1._pc, b.bn1)
-    a2 = ops.conv_bn(ctx, a1, b.conv2._pc, b.bn2)
+    a2 = ops.conv_bn(ctx, a1, b.conv2._pc, b.bn2, lazy=True)  # conv3 applies bn2-ReLU on load
     y3, s3 = ops.conv(ctx, a2, b.conv3._pc, stats=True)
     if b.downsample is not None:
         return ops.bn(ctx, y3, s3, b.bn3, relu=True, res_bn=(yd, sd, b.downsample[1]))

@@ -34,12 +34,18 @@ def call_configs(desc, dt=DT_BF16):
         return ["fwd:" + _lib.fwd_config(dt, C1, ld1 or C1, C2, ld2 or C2, N, H, W, K, R, S, stride, pad)]
     if d == "fwd_affine":  # eval-mode BN on the accumulator: always the generic kernel
         return ["fwd_affine:generic"]
+    if d == "fwd_bnrelu_in":  # 1x1 conv applying the producer's BN-ReLU on load (register-staged)
+        cfg = _lib.load().unetseg_conv2d_fwd_bnrelu_in_config(dt, C1, ld1 or C1, N, H, W, K)
+        return ["fwd_bnrelu_in:" + _lib.CFG_NAMES.get(cfg, str(cfg))]
     if d in ("dgrad", "dgrad_post1", "dgrad_post2"):
         tag = "dgrad" if d == "dgrad" else d
         return [f"{tag}:{c}" for c in _lib.dgrad_config(dt, K, N, Pq, Qq, K, cin, R, S, stride, pad, cin, H, W)]
     if d == "dgrad_padk":
         Kp = -(-K // 64) * 64
         return [f"dgrad:{c}" for c in _lib.dgrad_config(dt, Kp, N, Pq, Qq, Kp, C1, 1, 1, 1, 0, C1, H, W)]
+    if d == "wgrad_bnrelu_in":
+        kern, sp, red = _lib.wgrad_config(dt, C1, ld1 or C1, 0, 0, N, H, W, K, K, 1, 1, 1, 0)
+        return [f"wgrad_bnrelu_in:{kern}", red]
     if d in ("wgrad", "wgrad_padk"):
         Kw = -(-K // 64) * 64 if d == "wgrad_padk" else K
         c2 = 0 if d == "wgrad_padk" else C2

@@ -36,6 +36,9 @@ SIGNATURES = {
     "unetseg_pack_conv_weights": (I, [I, P, I, L, P]),
     "unetseg_pack_tiles": (I, [I, I, I]),
     "unetseg_bn_fold": (I, [I, P, P, P, P, F, P, P, P, P]),
+    "unetseg_conv2d_fwd_bnrelu_in": (I, [I, P, I, I, I, I, I, P, I, P, P, P, I, P, I, P, P]),
+    "unetseg_conv2d_fwd_bnrelu_in_config": (I, [I, I, I, I, I, I, I]),
+    "unetseg_conv2d_wgrad_bnrelu_in": (I, [I, P, I, I, I, I, I, P, I, I, P, P, P, SZ, P, I, I, P]),
     "unetseg_conv2d_fwd_affine": (I, [I, P, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P, P, I, P, I, P]),
     "unetseg_bn_finalize": (I, [P, I, I, L, I, P, P, P, P, P, F, F, P, P, P, P, P]),
     "unetseg_bn_eval_coeffs": (I, [I, P, P, P, P, F, P, P, P]),
@@ -116,7 +119,8 @@ SIGNATURES = {
 VALUE_FUNCS = {"reduce_tiles", "pw_small_tiles", "conv_tile_m", "abi_version", "conv2d_fwd_tile_m",
                "conv2d_dgrad_post", "stem_fwd_tile_m", "attn_bwd1_tiles", "pw_small_tile", "conv2d_fwd_config",
                "conv2d_dgrad_config", "conv2d_wgrad_config", "stem_config", "pw_head_tiles", "channel_stats_tiles",
-               "augment_tables_len", "pack_tiles"}
+               "augment_tables_len", "pack_tiles",
+               "conv2d_fwd_bnrelu_in_config"}
 
 _lib = None
 

@@ -32,9 +32,11 @@ def ldp(t):
 class Node:
     """An activation.  ``uses`` counts the ops that consumed it; ``fuse`` describes the ReLU that
     produced it, so that a sole consumer conv can apply that op's backward mask and first reduction
-    in its data-gradient epilogue (``fused`` then holds the partials for the producer's backward)."""
+    in its data-gradient epilogue (``fused`` then holds the partials for the producer's backward).
+    ``lazy`` (a BNState): the node stands for relu(BN(data)) that was never stored -- ``data`` is the
+    BN input and the consuming conv applies BN-ReLU on load (``bn(..., lazy=True)``)."""
 
-    __slots__ = ("data", "grad", "need_grad", "uses", "fuse", "fused")
+    __slots__ = ("data", "grad", "need_grad", "uses", "fuse", "fused", "lazy")
 
     def __init__(self, data, need_grad=True):
         self.data = data
@@ -43,6 +45,7 @@ class Node:
         self.uses = 0
         self.fuse = None
         self.fused = None
+        self.lazy = None
 
     @property
     def shape(self):
@@ -269,6 +272,11 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None):
     Conv2d container.  out: an NHWC view (pixel stride >= K) to write y into, e.g. a channel slice
     of a dense block's concatenation buffer.  Returns (Node y, BN partials or None)."""
     stride, pad = pc.conv.stride, pc.conv.padding
+    lazy = x1.lazy
+    if lazy is not None and not (x2 is None and ctx.dt == DT_BF16 and pc.R == 1 and pc.S == 1 and stride == 1 and
+                                 pad == 0 and x1.data.shape[-1] % 64 == 0 and pc.K % 64 == 0):
+        _materialize(ctx, x1)
+        lazy = None
     use(x1, x2)
     X1 = x1.data
     N, H, W, C1 = X1.shape
@@ -289,9 +297,14 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None):
     # probe descriptor: (N, H, W, C1, C2, K, R, S, stride, pad, ld1, ld2); bench/tools map it to the
     # kernel configuration through the unetseg_conv2d_*_config queries
     desc = (N, H, W, C1, C2, K, R, S, stride, pad, ldp(X1), ldp(X2))
-    with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
-        lib.conv2d_fwd(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride, pad,
-                       P(b), int(relu), P(y), ldp(y), P(st[0] if st else None), ctx.stream)
+    if lazy is not None:
+        with _probe("igemm_tn", flops, 1, ("fwd_bnrelu_in",) + desc):
+            lib.conv2d_fwd_bnrelu_in(ctx.dt, P(X1), C1, ldp(X1), N, H, W, P(pc.wk), K, P(lazy.sc), P(lazy.sh), P(b),
+                                     int(relu), P(y), ldp(y), P(st[0] if st else None), ctx.stream)
+    else:
+        with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
+            lib.conv2d_fwd(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride, pad,
+                           P(b), int(relu), P(y), ldp(y), P(st[0] if st else None), ctx.stream)
     out = Node(y)
     if relu:
         out.fuse = (1, y, None)
@@ -350,6 +363,10 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None):
                 lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), 0, 0, 0, N, H, W, P(dY), Kp, Kp, 1, 1, 1, 0, P(ws),
                                  ws.numel(), P(dwp), pc.C, 0, wst)
                 lib.add(DT_F32, P(dwp), pc.C, P(pc.conv.weight.grad), pc.C, K, pc.C, wst)
+        elif lazy is not None:
+            with _probe("wgrad", flops, 1, ("wgrad_bnrelu_in",) + desc, stream=side):
+                lib.conv2d_wgrad_bnrelu_in(ctx.dt, P(X1), C1, ldp(X1), N, H, W, P(dY), ldp(dY), K, P(lazy.sc),
+                                           P(lazy.sh), P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, wst)
         else:
             with _probe("wgrad", flops, 1, ("wgrad",) + desc, stream=side):
                 lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(dY), ldp(dY), K, R, S,
@@ -386,10 +403,11 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None):
 BN_FOLD = os.environ.get("UNETSEG_NO_BN_FOLD", "0") != "1"
 
 
-def conv_bn(ctx, x, pc, bnm, x2=None):
+def conv_bn(ctx, x, pc, bnm, x2=None, lazy=False):
     """relu(BN(conv(cat[x, x2]))) for a conv whose only consumer is that BN (model/resnet_backbone.py:
     58-61 bottleneck conv1/conv2, model/unet_plain.py:8-15 DoubleConv).  Training: the conv writes
-    BN partial statistics in its epilogue, then the BN-ReLU pass.  Eval in fp32 (the reference's
+    BN partial statistics in its epilogue, then the BN-ReLU pass (or, lazy, the consumer applies it on
+    load; see bn).  Eval in fp32 (the reference's
     evaluate / val / predict precision; no autograd tape): BN and ReLU run in the conv's epilogue on
     the fp32 accumulator, one launch (unetseg_conv2d_fwd_affine with unetseg_bn_fold's coefficients,
     the same float arithmetic as the separate pass, so the result is unchanged).  bf16 eval keeps
@@ -397,7 +415,7 @@ def conv_bn(ctx, x, pc, bnm, x2=None):
     emulation in the parity tests models."""
     if ctx.training or ctx.tape is not None or not BN_FOLD or ctx.dt != DT_F32:
         y, st = conv(ctx, x, pc, x2=x2, stats=True)
-        return bn(ctx, y, st, bnm, relu=True)
+        return bn(ctx, y, st, bnm, relu=True, lazy=lazy)
     K, C, R, S = pc.K, pc.C, pc.R, pc.S
     kscale, bias = ctx.f32(K), ctx.f32(K)
     lib.bn_fold(K, P(bnm.weight), P(bnm.bias), P(bnm.running_mean), P(bnm.running_var), bnm.eps, P(pc.conv.bias),
@@ -524,9 +542,27 @@ def _bn_coeffs(ctx, bn, st, M, tile=None):
     return s
 
 
-def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None):
+#: BN-ReLU applied by the consuming 1x1 conv on load instead of a separate pass (UNETSEG_NO_BN_PROLOGUE=1: off)
+BN_PROLOGUE = os.environ.get("UNETSEG_NO_BN_PROLOGUE", "0") != "1"
+
+
+def _materialize(ctx, node):
+    """store relu(BN(data)) of a lazy node (a consumer that cannot apply it on load)"""
+    s = node.lazy
+    Y = node.data
+    N, H, W, C = Y.shape
+    a = ctx.empty(N, H, W, C)
+    lib.bn_apply(ctx.dt, P(Y), ldp(Y), P(s.sc), P(s.sh), 0, 0, 0, 0, 0, 1, P(a), C, N * H * W, C, ctx.stream)
+    node.data = a
+    node.lazy = None
+
+
+def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None, lazy=False):
     """a = act(BN(y) [+ res | + BN2(y2)]).  y: conv output Node with partial stats st.
-    res: raw residual Node; res_bn: (Node y2, stats2, bn module 2)."""
+    res: raw residual Node; res_bn: (Node y2, stats2, bn module 2).  lazy (plain BN-ReLU in bf16
+    training): no apply pass -- the returned node carries y and the coefficients, and its consumer
+    (a 1x1 conv: model/resnet_backbone.py:62 conv3 after bn2) applies BN-ReLU on load, forward and
+    weight gradient; the backward below needs only y, so nothing else changes."""
     use(y, res, res_bn[0] if res_bn is not None else None)
     Y = y.data
     N, H, W, C = Y.shape
@@ -538,10 +574,14 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None):
     elif res_bn is not None:
         mode, R = 2, res_bn[0].data
         s2 = _bn_coeffs(ctx, res_bn[2], res_bn[1], M)
-    a = ctx.empty(N, H, W, C)
-    lib.bn_apply(ctx.dt, P(Y), ldp(Y), P(s1.sc), P(s1.sh), P(R), ldp(R), P(s2.sc if s2 else None),
-                 P(s2.sh if s2 else None), mode, int(relu), P(a), C, M, C, ctx.stream)
-    out = Node(a)
+    if lazy and BN_PROLOGUE and relu and mode == 0 and ctx.training and ctx.dt == DT_BF16:
+        out = Node(Y)
+        out.lazy = s1
+    else:
+        a = ctx.empty(N, H, W, C)
+        lib.bn_apply(ctx.dt, P(Y), ldp(Y), P(s1.sc), P(s1.sh), P(R), ldp(R), P(s2.sc if s2 else None),
+                     P(s2.sh if s2 else None), mode, int(relu), P(a), C, M, C, ctx.stream)
+        out = Node(a)
     plain_relu = relu and res is None and res_bn is None
     if plain_relu and ctx.training:
         out.fuse = (2, Y, s1)
@@ -570,7 +610,7 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None):
         Y2 = y2.data if y2 is not None else None
         # plain BN-ReLU: the mask is recomputed from y (no read of the activation)
         plain = relu and res is None and res_bn is None
-        mA = 0 if (plain or not relu) else P(a)
+        mA = 0 if (plain or not relu) else P(out.data)
         msc, msh = (P(s1.sc), P(s1.sh)) if plain else (0, 0)
         lib.bn_bwd_reduce(ctx.dt, P(dA), ldp(dA), mA, C, msc, msh, P(Y), ldp(Y), P(s1.mean), P(s1.inv),
                           P(Y2), ldp(Y2), P(s2.mean if s2 else None), P(s2.inv if s2 else None), M, C, P(part), Gr,
