@@ -530,22 +530,41 @@ __global__ void linear_bwd_w_kernel(const float* dyp, const float* x, int B, int
 }
 
 // cross entropy (mean) over B rows of K logits; dlog = (softmax - onehot)/B (unscaled)
+// nn.CrossEntropyLoss() (mean, ignore_index -100): rows whose target is -100 contribute nothing and
+// the mean runs over the others; any other target outside [0, K) makes the loss and its gradient
+// NaN (torch raises; no out-of-range read here either way).
 __global__ void ce_kernel(const float* logits, const int64_t* tgt, int B, int K, float* loss, float* dlog) {
   __shared__ double sred[16];
+  __shared__ int cnt[2];
+  if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  int nvalid = 0, nbad = 0;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const long long t = tgt[b];
+    nvalid += (t >= 0 && t < K) ? 1 : 0;
+    nbad += (t != -100 && (t < 0 || t >= K)) ? 1 : 0;
+  }
+  atomicAdd(&cnt[0], nvalid);  // LDS atomics
+  atomicAdd(&cnt[1], nbad);
+  __syncthreads();
+  const float denom = (float)max(cnt[0], 1);
+  const bool bad = cnt[1] > 0;
   double s = 0.0;
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     const float* l = logits + (long)b * K;
+    const long long t = tgt[b];
+    const bool ok = t >= 0 && t < K;
     float mx = l[0];
     for (int k = 1; k < K; ++k) mx = fmaxf(mx, l[k]);
     float se = 0.f;
     for (int k = 0; k < K; ++k) se += expf(l[k] - mx);
     const float lse = mx + logf(se);
-    const int t = (int)tgt[b];
-    s += (double)(lse - l[t]);
-    for (int k = 0; k < K; ++k) dlog[(long)b * K + k] = (expf(l[k] - lse) - (k == t ? 1.f : 0.f)) / (float)B;
+    if (ok) s += (double)(lse - l[t]);
+    for (int k = 0; k < K; ++k)
+      dlog[(long)b * K + k] = bad ? NAN : ok ? (expf(l[k] - lse) - (k == t ? 1.f : 0.f)) / denom : 0.f;
   }
   s = block_sum(s, sred);
-  if (threadIdx.x == 0) loss[0] = (float)(s / B);
+  if (threadIdx.x == 0) loss[0] = bad ? NAN : cnt[0] == 0 ? NAN : (float)(s / (double)cnt[0]);
 }
 
 // multiply a per-element gradient buffer by a device scalar: out = g * (s1[0]*a1 + s2[0]*a2)

@@ -22,6 +22,12 @@ def _prep(outputs, targets):
     if not outputs.is_cuda:
         raise RuntimeError("HIP losses need device tensors")
     out = outputs.detach().float().contiguous()
+    if targets.is_floating_point():
+        # MultiTaskLoss passes seg_targets.float() (model/unet_multitask.py:131) to BCE, which would
+        # take soft labels as given; the kernels take 0/1 labels, so anything else is refused rather
+        # than silently binarised (a host check: float targets only come from that path)
+        if bool(((targets != 0) & (targets != 1)).any()):
+            raise ValueError("float segmentation targets must be 0/1 (soft labels are not supported)")
     tgt = targets.detach().to(torch.int64).contiguous()
     return out, tgt
 
