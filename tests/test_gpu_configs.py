@@ -1,8 +1,8 @@
 """GPU: every conv kernel configuration the benchmark step selects, at shapes that select it.
 
 The library picks a kernel configuration per call from the shape (conv_fast.hip tn_config: halo /
-register-staged TN tiles / LDS-DMA rings with compile-time taps; wgrad: halo / fast tiles with
-split-K slabs and a 16- / 4- / 1-lane reduce).  Each case below names the configuration it must
+register-staged TN tiles / LDS-DMA rings with compile-time taps; wgrad: halo / LDS-DMA ring /
+register-staged tiles with split-K slabs and their reduce).  Each case below names the configuration it must
 select -- asserted through the host-only ``unetseg_conv2d_*_config`` queries of the C ABI -- and
 checks the launch against a float64 reference computed on the same bf16-rounded operands
 (im2col + GEMM in torch float64 on the GPU: exact products, so the only error left is the
@@ -96,12 +96,19 @@ CASES = {
     # ---- weight gradient (+ split-K reduce) ----
     "wgrad_halo3": ("wgrad", (2, 64, 256, 64, 0, 64, 3, 1), ["wgrad:halo3_wgrad", None]),
     "wgrad_halo3_cat": ("wgrad", (16, 32, 32, 1024, 2048, 512, 3, 1), ["wgrad:halo3_wgrad", None]),
-    "wgrad128_row_r16": ("wgrad", (16, 128, 128, 64, 0, 256, 1, 1), ["wgrad:wgrad128_row", "reduce16"]),
-    "wgrad128_row_r4": ("wgrad", (1, 64, 64, 128, 0, 512, 1, 1), ["wgrad:wgrad128_row", "reduce4"]),
-    "wgrad128_row_r1": ("wgrad", (1, 32, 32, 256, 0, 1024, 1, 1), ["wgrad:wgrad128_row", "reduce1"]),
-    "wgrad128_s2": ("wgrad", (16, 32, 32, 512, 0, 512, 3, 2), ["wgrad:wgrad128", None]),
-    "wgrad128_r16_16x16": ("wgrad", (16, 16, 16, 2048, 0, 512, 1, 1), ["wgrad:wgrad128", None]),
-    "wgrad64x256_row": ("wgrad", (16, 128, 128, 256, 0, 64, 1, 1), ["wgrad:wgrad64x256_row", "reduce16"]),
+    "wgrad_ring128_r16": ("wgrad", (16, 128, 128, 64, 0, 256, 1, 1), ["wgrad:wgrad_ring128", "reduce"]),
+    "wgrad_ring128_r4": ("wgrad", (1, 64, 64, 128, 0, 512, 1, 1), ["wgrad:wgrad_ring128", "reduce"]),
+    "wgrad_ring128_r1": ("wgrad", (1, 32, 32, 256, 0, 1024, 1, 1), ["wgrad:wgrad_ring128", "reduce"]),
+    "wgrad_ring128_s2": ("wgrad", (16, 32, 32, 512, 0, 512, 3, 2), ["wgrad:wgrad_ring128", None]),
+    "wgrad_ring128_1x1s2": ("wgrad", (2, 32, 32, 256, 0, 512, 1, 2), ["wgrad:wgrad_ring128", None]),
+    # 8-wide rows (4 rows per K step), a partial column tile (Ng = 576), padding taps
+    "wgrad_ring128_q8": ("wgrad", (2, 8, 8, 64, 0, 128, 3, 1), ["wgrad:wgrad_ring128", None]),
+    "wgrad_ring128_16x16": ("wgrad", (16, 16, 16, 2048, 0, 512, 1, 1), ["wgrad:wgrad_ring128", None]),
+    # register-staged kernels: K steps that straddle rows (ragged grids), a concat source
+    "wgrad128_ragged": ("wgrad", (1, 15, 17, 64, 0, 256, 1, 1), ["wgrad:wgrad128", None]),
+    "wgrad64x256_ragged": ("wgrad", (1, 15, 17, 256, 0, 64, 1, 1), ["wgrad:wgrad64x256", None]),
+    "wgrad128_row_cat": ("wgrad", (2, 64, 64, 64, 64, 256, 1, 1), ["wgrad:wgrad128_row", None]),
+    "wgrad_ring64x256": ("wgrad", (16, 128, 128, 256, 0, 64, 1, 1), ["wgrad:wgrad_ring64x256", "reduce"]),
     # bottleneck conv3 reading bn2-ReLU on load (ops.bn(lazy=True), unetseg_conv2d_*_bnrelu_in)
     "bnin_tn128x128_1step": ("fwd_bnrelu_in", (16, 128, 128, 64, 0, 256, 1, 1), ["fwd_bnrelu_in:tn128x128_1step"]),
     "bnin_tn128x128": ("fwd_bnrelu_in", (16, 64, 64, 128, 0, 512, 1, 1), ["fwd_bnrelu_in:tn128x128"]),
@@ -109,10 +116,11 @@ CASES = {
     "bnin_tn256x128": ("fwd_bnrelu_in", (16, 16, 16, 512, 0, 2048, 1, 1), ["fwd_bnrelu_in:tn256x128"]),
     "bnin_tn64x128": ("fwd_bnrelu_in", (1, 16, 16, 512, 0, 2048, 1, 1), ["fwd_bnrelu_in:tn64x128"]),
     "bnin_ragged": ("fwd_bnrelu_in", (1, 15, 17, 64, 0, 256, 1, 1), None),
-    "bnin_wgrad_row_r16": ("wgrad_bnrelu_in", (16, 128, 128, 64, 0, 256, 1, 1), ["wgrad_bnrelu_in:wgrad128_row", "reduce16"]),
-    "bnin_wgrad_row_r4": ("wgrad_bnrelu_in", (1, 64, 64, 128, 0, 512, 1, 1), ["wgrad_bnrelu_in:wgrad128_row", "reduce4"]),
-    "bnin_wgrad_16x16": ("wgrad_bnrelu_in", (16, 16, 16, 512, 0, 2048, 1, 1), ["wgrad_bnrelu_in:wgrad128", None]),
-    "bnin_wgrad_ragged": ("wgrad_bnrelu_in", (1, 15, 17, 64, 0, 256, 1, 1), None),
+    "bnin_wgrad_ring_r16": ("wgrad_bnrelu_in", (16, 128, 128, 64, 0, 256, 1, 1), ["wgrad_bnrelu_in:wgrad_ring128", "reduce"]),
+    "bnin_wgrad_ring_r4": ("wgrad_bnrelu_in", (1, 64, 64, 128, 0, 512, 1, 1), ["wgrad_bnrelu_in:wgrad_ring128", "reduce"]),
+    "bnin_wgrad_ring64x256": ("wgrad_bnrelu_in", (2, 32, 32, 256, 0, 64, 1, 1), ["wgrad_bnrelu_in:wgrad_ring64x256", None]),
+    "bnin_wgrad_ring_16x16": ("wgrad_bnrelu_in", (16, 16, 16, 512, 0, 2048, 1, 1), ["wgrad_bnrelu_in:wgrad_ring128", None]),
+    "bnin_wgrad_ragged": ("wgrad_bnrelu_in", (1, 15, 17, 64, 0, 256, 1, 1), ["wgrad_bnrelu_in:wgrad128", None]),
 }
 
 
@@ -385,7 +393,7 @@ def _bnrelu_in_case(cid, direction, shape, op, wk, lib, st):
 @pytest.mark.parametrize("N,H", [(16, 512), (2, 200)])
 def test_stem_bench_size(N, H):
     """ResNet stem at the benchmark size (model/resnet_backbone.py:126-131): 7x7/s2/p3 3->64 on the
-    width-packed fast kernels (stem_fwd: TN 128x64 tile; stem_wgrad: 64x256 split-K + reduce<16>)."""
+    width-packed fast kernels (stem_fwd: TN 128x64 tile; stem_wgrad: 64x256 split-K ring + reduce)."""
     from unetseg_hip import ops
     from unetseg_hip.lib import DT_BF16, stem_config
     from unetseg_hip.nn import Conv2d
@@ -442,6 +450,6 @@ def test_bench_configs_covered():
     finally:
         ops.PROBE = None
     assert np.isfinite(loss.item())
-    stem = {"stem_fwd:tn128x64", "stem_wgrad:wgrad64x256_row"}  # test_stem_bench_size
+    stem = {"stem_fwd:tn128x64", "stem_wgrad:wgrad_ring64x256"}  # test_stem_bench_size
     missing = sorted(used - covered_keys() - stem)
     assert not missing, f"bench configurations without a parity case: {missing}"

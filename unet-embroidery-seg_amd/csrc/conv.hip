@@ -474,38 +474,81 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
     }
 }
 
-// dW[k][c][tap] (+)= sum_z ws[z][k][tap*cin + c] for c < dw_c.  Thread i walks (k, tap, c) with c
-// fastest, so slab reads are coalesced; the permuted writes touch only Cout*dw_c*taps floats.
-// Block = (256/SL) outputs x SL split lanes; lane l sums splits l, l+SL, ... and the SL partials
-// are combined in LDS in a fixed order: deterministic, parallel over splits as well as outputs.
+// dW[k][c][tap] (+)= sum_z ws[z][k][tap*cin + c] for c < dw_c.  Block = (output channel k, a run of
+// cw input channels) x SL split lanes: item i = (tap, 4 channels) is one 16-B load per slab; lane l
+// sums slabs l, l+SL, ... in ascending order, the SL partials are combined in LDS in a fixed order
+// (deterministic), and the block's dW run -- cw x taps consecutive floats of PyTorch's [K][C][R][S]
+// -- is written through an LDS transpose, so both the slab reads and the dW writes are contiguous.
 template <int SL>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* ws, int splits, int Cout, int cin, int taps,
-                                                           float* dw, int dw_c, int accumulate) {
-  constexpr int OPB = 256 / SL;
-  __shared__ float red[SL][OPB];
-  const long Ng = (long)taps * cin;
-  const long total = (long)Cout * taps * dw_c;
-  const long slab = (long)Cout * Ng;
-  const int o = threadIdx.x % OPB, sl = threadIdx.x / OPB;
-  const long i = (long)blockIdx.x * OPB + o;
-  float v = 0.f;
-  long dst = 0;
-  if (i < total) {
-    long t = i;
-    const int c = (int)(t % dw_c); t /= dw_c;
-    const int tap = (int)(t % taps);
-    const long k = t / taps;
-    const long src = k * Ng + (long)tap * cin + c;
-    dst = (k * dw_c + c) * taps + tap;
-    for (int z = sl; z < splits; z += SL) v += ws[z * slab + src];
+                                                           float* dw, int dw_c, int accumulate, int cw) {
+  constexpr int IT = 256 / SL;
+  __shared__ float4 red[SL][IT];
+  __shared__ float tile[1024];
+  const long Ng = (long)taps * cin, slab = (long)Cout * Ng;
+  const int nchunk = (dw_c + cw - 1) / cw;
+  const int k = blockIdx.x / nchunk, cc0 = (blockIdx.x - k * nchunk) * cw;
+  const int q4 = cw >> 2, items = taps * q4;
+  const int it = threadIdx.x % IT, sl = threadIdx.x / IT;
+  const int tap = it / q4, cl = (it - tap * q4) * 4;
+  const bool live = it < items && cc0 + cl < dw_c;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (live) {
+    const float4* p = reinterpret_cast<const float4*>(ws + (long)k * Ng + (long)tap * cin + cc0 + cl);
+    const long s4 = slab >> 2;
+    int z = sl;
+    for (; z + 3 * SL < splits; z += 4 * SL) {
+      const float4 a = p[z * s4], b = p[(z + SL) * s4], c = p[(z + 2 * SL) * s4], d = p[(z + 3 * SL) * s4];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+      v.x += c.x; v.y += c.y; v.z += c.z; v.w += c.w;
+      v.x += d.x; v.y += d.y; v.z += d.z; v.w += d.w;
+    }
+    for (; z < splits; z += SL) {
+      const float4 a = p[z * s4];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
   }
-  if (SL > 1) {
-    red[sl][o] = v;
+  if constexpr (SL > 1) {
+    red[sl][it] = v;
     __syncthreads();
-    if (sl != 0) return;
-    for (int jj = 1; jj < SL; ++jj) v += red[jj][o];
+    if (sl == 0)
+      for (int j = 1; j < SL; ++j) {
+        const float4 a = red[j][it];
+        v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      }
   }
-  if (i < total) dw[dst] = accumulate ? dw[dst] + v : v;
+  if (sl == 0 && it < items) {  // [c][tap] order of the block's dW run
+    tile[(cl + 0) * taps + tap] = v.x;
+    tile[(cl + 1) * taps + tap] = v.y;
+    tile[(cl + 2) * taps + tap] = v.z;
+    tile[(cl + 3) * taps + tap] = v.w;
+  }
+  __syncthreads();
+  const int run = min(cw, dw_c - cc0) * taps;
+  float* out = dw + ((long)k * dw_c + cc0) * taps;
+  for (int i = threadIdx.x; i < run; i += 256) out[i] = accumulate ? out[i] + tile[i] : tile[i];
+}
+
+// split lanes from the slab count (parallel over splits when there are many), then the widest
+// channel run whose (tap, 4-channel) items fit one lane group
+static void launch_wgrad_reduce(const float* ws, int splits, int cout, int cin, int taps, float* dw, int dw_c,
+                                int accumulate, hipStream_t st) {
+  int sl = splits >= 64 ? 16 : splits >= 8 ? 4 : 1;
+  while (sl > 1 && (256 / sl) / taps < 1) sl /= 4;  // every tap of one 4-channel item in a lane group
+  int cw = 4 * ((256 / sl) / taps);
+  if (cw > 1024 / taps / 4 * 4) cw = 1024 / taps / 4 * 4;  // LDS transpose tile
+  if (cw > ceil_div(dw_c, 4) * 4) cw = ceil_div(dw_c, 4) * 4;
+  const int blocks = cout * ceil_div(dw_c, cw);
+  if (sl == 16)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c,
+                       accumulate, cw);
+  else if (sl == 4)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c,
+                       accumulate, cw);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c,
+                       accumulate, cw);
 }
 
 // fp32 [K][C][R][S] -> T [K][R][S][Cpad] (zero-padded channels) and optionally T [C][R][S][K]
@@ -825,16 +868,7 @@ UNETSEG_API int unetseg_conv2d_wgrad_bnrelu_in(int dtype, const void* x1, int c1
   hipStream_t st = (hipStream_t)stream;
   launch_wgrad_fast(f, splits, st);
   US_LAUNCH_CHECK("wgrad_fast_bnrelu_in");
-  const long total = (long)cout * dw_c;
-  if (splits >= 16)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(ceil_div(total, 16)), dim3(256), 0, st, ws, splits, cout, c1, 1,
-                       dw, dw_c, accumulate);
-  else if (splits >= 4)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(ceil_div(total, 64)), dim3(256), 0, st, ws, splits, cout, c1, 1,
-                       dw, dw_c, accumulate);
-  else
-    hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(ceil_div(total, 256)), dim3(256), 0, st, ws, splits, cout, c1, 1,
-                       dw, dw_c, accumulate);
+  launch_wgrad_reduce(ws, splits, cout, c1, 1, dw, dw_c, accumulate, st);
   US_LAUNCH_CHECK("wgrad_reduce");
   return 0;
 }
@@ -1087,22 +1121,13 @@ UNETSEG_API int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1
   US_LAUNCH_CHECK("wgrad");
   }
   US_CHECK_ARG(dw_c > 0 && dw_c <= a.cin, "conv2d_wgrad: bad dw_c");
-  const long total = (long)cout * dw_c * r * s;
-  if (splits >= 16)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(ceil_div(total, 16)), dim3(256), 0, st, ws, splits, cout, a.cin,
-                       r * s, dw, dw_c, accumulate);
-  else if (splits >= 4)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(ceil_div(total, 64)), dim3(256), 0, st, ws, splits, cout, a.cin,
-                       r * s, dw, dw_c, accumulate);
-  else
-    hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(ceil_div(total, 256)), dim3(256), 0, st, ws, splits, cout, a.cin,
-                       r * s, dw, dw_c, accumulate);
+  launch_wgrad_reduce(ws, splits, cout, a.cin, r * s, dw, dw_c, accumulate, st);
   US_LAUNCH_CHECK("wgrad_reduce");
   return 0;
 }
 
-// Kernel unetseg_conv2d_wgrad runs for this shape: kWg* code; *splits_out = split-K slabs (the
-// reduce is wgrad_reduce_kernel<16> from 16 slabs, <4> from 4, else <1>).
+// Kernel unetseg_conv2d_wgrad runs for this shape: kWg* code; *splits_out = split-K slabs (summed by
+// wgrad_reduce_kernel).
 UNETSEG_API int unetseg_conv2d_wgrad_config(int dtype, int c1, int ldc1, int c2, int ldc2, int n, int h, int w,
                                             int ldy, int cout, int r, int s, int stride, int pad, int* splits_out) {
   const int p = (h + 2 * pad - r) / stride + 1, q = (w + 2 * pad - s) / stride + 1;
@@ -1118,6 +1143,10 @@ UNETSEG_API int unetseg_conv2d_wgrad_config(int dtype, int c1, int ldc1, int c2,
   } else if (fit && wgrad_fast_eligible(dtype, q, cin, cout) && c1 % 8 == 0) {
     const bool row32 = !getenv("UNETSEG_WG_NO_ROW32") && q % 32 == 0;
     kind = cout <= 64 ? (row32 ? kWgFastRow64x256 : kWgFast64x256) : (row32 ? kWgFastRow128 : kWgFast128);
+    FastWgradArgs f{};
+    f.x2 = c2 ? kSomePtr : nullptr; f.c1 = c1; f.cin = cin; f.H = h; f.W = w; f.P = p; f.Q = q;
+    f.stride = stride; f.pad = pad; f.padw = pad; f.S = s; f.Cout = cout; f.Ng = Ng; f.Kpix = kpix;
+    if (wgrad_ring_ok(f)) kind = cout <= 64 ? kWgRing64x256 : kWgRing128;
     splits = wgrad_fast_splits(cout, Ng, kpix);
   } else {
     splits = wgrad_splits(cout, Ng, kpix, dtype == DT_BF16 ? 32 : 16);
@@ -1280,9 +1309,7 @@ UNETSEG_API int unetseg_stem_wgrad(const void* xp, int n, int h, int w, const vo
   launch_wgrad_fast(f, splits, st);
   // parallel deterministic split reduce into v = ws tail, [K][64 virtual channels][7 rows], then permute
   float* v = ws + (size_t)splits * K * f.Ng;
-  const long total = (long)K * 64 * 7;
-  hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(ceil_div(total, 16)), dim3(256), 0, st, ws, splits, K, 64, 7, v, 64,
-                     0);
+  launch_wgrad_reduce(ws, splits, K, 64, 7, v, 64, 0, st);
   hipLaunchKernelGGL(stem_wgrad_remap_kernel, dim3(ceil_div((long)K * C * 49, 256)), dim3(256), 0, st, v, K, C, dw,
                      accumulate);
   US_LAUNCH_CHECK("stem_wgrad");

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+constexpr int kWgBK = 32;  // wgrad K step (pixels); 64 halves the barriers but costs a wave per SIMD: slower
+
 struct FastTNArgs {
   const void* x1;
   const void* x2;
@@ -60,6 +62,7 @@ struct FastWgradArgs {
   float* ws;
   const float* in_sc;  // as FastTNArgs: X = relu(x1 * in_sc[c] + in_sh[c]) on load (x2 == NULL)
   const float* in_sh;
+  int xcd_map;  // ring kernel: XCD-contiguous work order (set by the launcher)
 };
 
 // 3x3 / stride 1 / pad 1 weight gradient on the halo path (conv_halo.hip)
@@ -77,7 +80,8 @@ struct HaloWgradArgs {
 
 // kernel-configuration codes reported by the unetseg_conv2d_*_config queries (include/unetseg_hip.h)
 enum { kCfgHalo = 0, kCfgGeneric = 100 };  // 1..14: TN tile configurations of tn_config (conv_fast.hip)
-enum { kWgHalo = 0, kWgFastRow64x256 = 1, kWgFastRow128 = 2, kWgFast64x256 = 3, kWgFast128 = 4, kWgGeneric = 5 };
+enum { kWgHalo = 0, kWgFastRow64x256 = 1, kWgFastRow128 = 2, kWgFast64x256 = 3, kWgFast128 = 4, kWgGeneric = 5,
+       kWgRing64x256 = 6, kWgRing128 = 7 };
 
 bool tn_fast_ok(const FastTNArgs& a);
 int tn_fast_config(const FastTNArgs& a, int* taps_out);  // kCfgHalo or a TN configuration 1..14
@@ -92,5 +96,7 @@ bool halo3_wgrad_ok(const HaloWgradArgs& a);
 int halo3_wgrad_splits(const HaloWgradArgs& a);
 int launch_halo3_wgrad(const HaloWgradArgs& a, int G_per, hipStream_t st);
 bool wgrad_fast_ok(const FastWgradArgs& a);
+bool wgrad_ring_ok(const FastWgradArgs& a);  // launch_wgrad_fast takes the LDS-DMA ring kernel
+int launch_wgrad_ring(const FastWgradArgs& a, int splits, hipStream_t st);  // conv_wgrad_ring.hip
 int wgrad_fast_splits(int Cout, int Ng, long Kpix);
 int launch_wgrad_fast(FastWgradArgs a, int splits, hipStream_t st);

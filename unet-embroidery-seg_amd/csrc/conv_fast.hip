@@ -616,7 +616,6 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
 // tracks (image, row, col) of the pixels it stages and advances them by one step at a time, so
 // any output width works.
 // ------------------------------------------------------------------------------------------
-constexpr int kWgBK = 32;  // 64 halves the barriers but costs a wave per SIMD: slower here
 
 // ROW32 (Q % 32 == 0): the 32 pixels of a K step are one run of an output row, so (image, row,
 // first column) is wave-uniform scalar state and each staged row's offset is a scalar base plus a
@@ -1073,6 +1072,7 @@ static void launch_wgrad_cfg(const FastWgradArgs& a, int splits, hipStream_t st)
 int launch_wgrad_fast(FastWgradArgs a, int splits, hipStream_t st) {
   const long nkt = (a.Kpix + kWgBK - 1) / kWgBK;
   a.kt_per_split = (int)((nkt + splits - 1) / splits);
+  if (wgrad_ring_ok(a)) return launch_wgrad_ring(a, splits, st);
   static const bool no_row = getenv("UNETSEG_WG_NO_ROW32") != nullptr;
   // ROW32: every K step is one 32-pixel run of an output row, and the per-lane pixel deltas and
   // scalar bases fit 32-bit offsets (the caller bounds both tensors below 2^31 bytes)

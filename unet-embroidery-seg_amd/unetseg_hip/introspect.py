@@ -8,6 +8,8 @@ every configuration the benchmark step runs; ``tools/bench_conv_configs.py`` pri
 """
 from __future__ import annotations
 
+import os
+
 from . import lib as _lib
 from .lib import DT_BF16
 
@@ -24,11 +26,12 @@ def call_configs(desc, dt=DT_BF16):
         cfg, _ = _lib.stem_config(N, H, W, K)
         return [f"stem_fwd:{cfg}"]
     if d == "stem_wgrad":
-        # unetseg_stem_wgrad: wgrad_fast (64x256 for K = 64; row-run walk when Q % 32 == 0), then a
-        # fixed reduce<16> over its slabs
+        # unetseg_stem_wgrad: the wgrad_fast family (64x256 for K = 64: the LDS-DMA ring when the
+        # output width is a multiple of 32, else the register-staged walk), then the split-K reduce
         Qs = (W - 1) // 2 + 1
+        ring = Qs % 32 == 0 and not os.environ.get("UNETSEG_WG_NO_RING")
         tile = "wgrad64x256" if K <= 64 else "wgrad128"
-        return [f"stem_wgrad:{tile}{'_row' if Qs % 32 == 0 else ''}", "reduce16"]
+        return [f"stem_wgrad:{'wgrad_ring64x256' if ring and K <= 64 else tile}", "reduce"]
     Pq, Qq = _out_hw(H, W, R, S, stride, pad)
     if d == "fwd":
         return ["fwd:" + _lib.fwd_config(dt, C1, ld1 or C1, C2, ld2 or C2, N, H, W, K, R, S, stride, pad)]

@@ -180,7 +180,7 @@ CFG_NAMES = {0: "halo3", 1: "tn256x64", 2: "tn256x128", 3: "tn128x128", 4: "tn12
              6: "tn128x64", 7: "ring256x128", 8: "ring128x128", 9: "ring64x128", 10: "ring128x128_5st",
              11: "ring256x64", 12: "ring128x64_4st", 13: "ring128x64", 14: "ring256x64_8w", 100: "generic"}
 WG_NAMES = {0: "halo3_wgrad", 1: "wgrad64x256_row", 2: "wgrad128_row", 3: "wgrad64x256", 4: "wgrad128",
-            5: "wgrad_generic"}
+            5: "wgrad_generic", 6: "wgrad_ring64x256", 7: "wgrad_ring128"}
 
 
 def _cfg_name(cfg, taps):
@@ -208,12 +208,10 @@ def wgrad_config(dtype, c1, ldc1, c2, ldc2, n, h, w, ldy, cout, r, s, stride, pa
     sp = ctypes.c_int(0)
     kind = load().unetseg_conv2d_wgrad_config(dtype, c1, ldc1, c2, ldc2, n, h, w, ldy, cout, r, s, stride, pad,
                                               ctypes.byref(sp))
-    red = 16 if sp.value >= 16 else 4 if sp.value >= 4 else 1
-    return WG_NAMES.get(kind, str(kind)), sp.value, f"reduce{red}"
+    return WG_NAMES.get(kind, str(kind)), sp.value, "reduce"
 
 
 def stem_config(n, h, w, K):
     sp = ctypes.c_int(0)
     cfg = load().unetseg_stem_config(n, h, w, K, ctypes.byref(sp))
-    red = 16 if sp.value >= 16 else 4 if sp.value >= 4 else 1
     return CFG_NAMES.get(cfg, str(cfg)), sp.value
