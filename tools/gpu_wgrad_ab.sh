@@ -18,7 +18,7 @@ for r in rows:
     k = r["Kernel_Name"]
     if not re.search("wgrad", k):
         continue
-    key = (re.sub(r"\(.*", "", k).replace("void (anonymous namespace)::", "")[:60], r["Grid_Size_X"], r["Grid_Size_Y"], r["Grid_Size_Z"])
+    key = (k.replace("void (anonymous namespace)::", "").split("(")[0][:60], r["Grid_Size_X"], r["Grid_Size_Y"], r["Grid_Size_Z"])
     agg.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for (k, gx, gy, gz), v in agg.items():
     v = sorted(v)[: max(1, len(v) // 2)]

@@ -19,7 +19,7 @@ from collections import defaultdict
 
 GROUPS = {
     "igemm_tn": re.compile(r"(tn_fast_kernel|halo3_kernel<|igemm_tn_kernel)"),
-    "wgrad": re.compile(r"(wgrad_fast_kernel|halo3_wgrad_kernel|wgrad_kernel<)"),
+    "wgrad": re.compile(r"(wgrad_fast_kernel|wgrad_ring_kernel|halo3_wgrad_kernel|wgrad_kernel<)"),
 }
 SIMDS = 256 * 4
 FLOP_PER_MFMA = 16 * 16 * 32 * 2

@@ -16,7 +16,7 @@ import sys
 
 GROUPS = {
     "igemm_tn": re.compile(r"(tn_fast_kernel|halo3_kernel<|igemm_tn_kernel)"),
-    "wgrad": re.compile(r"(wgrad_fast_kernel|wgrad_kernel|wgrad_reduce_kernel)"),
+    "wgrad": re.compile(r"(wgrad_fast_kernel|wgrad_ring_kernel|wgrad_kernel|wgrad_reduce_kernel)"),
 }
 
 
@@ -37,7 +37,7 @@ def main():
         if not fb or not wb:
             continue
         # launches of the main GEMM kernels (reduce kernels fold into their wgrad launch)
-        main_pat = re.compile(r"(tn_fast_kernel|halo3_kernel<|igemm_tn_kernel|wgrad_fast_kernel<|wgrad_kernel<)")
+        main_pat = re.compile(r"(tn_fast_kernel|halo3_kernel<|igemm_tn_kernel|wgrad_fast_kernel<|wgrad_ring_kernel<|wgrad_kernel<)")
         nl = sum(1 for n, _ in fetch if main_pat.search(n) and pat.search(n))
         f2, w = 2.0 * sum(fb), sum(wb)
         res["groups"][g] = {"launches": nl, "fetch_bytes_per_launch": f2 / nl, "write_bytes_per_launch": w / nl,

@@ -530,25 +530,91 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* ws, int 
   for (int i = threadIdx.x; i < run; i += 256) out[i] = accumulate ? out[i] + tile[i] : tile[i];
 }
 
-// split lanes from the slab count (parallel over splits when there are many), then the widest
-// channel run whose (tap, 4-channel) items fit one lane group
+// The same sum when there are many slabs (or a 1x1 filter): block = IT consecutive float4 items of a
+// slab x SL split lanes; lane l sums the contiguous slab range [l*R, (l+1)*R), R = ceil(splits/SL),
+// four loads in flight, and the SL partials are added in LDS in lane order (deterministic).  Enough
+// (item, lane) pairs to keep every CU streaming; the dW writes are permuted 4-B stores (float4 for
+// 1x1), a 1/splits share of the traffic.
+template <int SL>
+__global__ __launch_bounds__(256) void wgrad_reduce_split_kernel(const float* ws, int splits, int Cout, int cin,
+                                                                 int taps, float* dw, int dw_c, int accumulate) {
+  constexpr int IT = 256 / SL;
+  __shared__ float4 red[SL][IT];
+  const long Ng = (long)taps * cin, s4 = (long)Cout * Ng / 4;
+  const int it = threadIdx.x % IT, sl = threadIdx.x / IT;
+  const long q = (long)blockIdx.x * IT + it;
+  const int R = (splits + SL - 1) / SL;
+  const int z1 = min(splits, (sl + 1) * R);
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (q < s4) {
+    const float4* p = reinterpret_cast<const float4*>(ws) + q;
+    int z = sl * R;
+    for (; z + 3 < z1; z += 4) {
+      const float4 a = p[z * s4], b = p[(z + 1) * s4], c = p[(z + 2) * s4], d = p[(z + 3) * s4];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+      v.x += c.x; v.y += c.y; v.z += c.z; v.w += c.w;
+      v.x += d.x; v.y += d.y; v.z += d.z; v.w += d.w;
+    }
+    for (; z < z1; ++z) {
+      const float4 a = p[z * s4];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+  }
+  if constexpr (SL > 1) {
+    red[sl][it] = v;
+    __syncthreads();
+    if (sl != 0) return;
+    v = red[0][it];
+    for (int j = 1; j < SL; ++j) {
+      const float4 a = red[j][it];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+  }
+  if (q >= s4) return;
+  const long k = q * 4 / Ng;
+  const int col = (int)(q * 4 - k * Ng);
+  const int tap = col / cin, c0 = col - tap * cin;
+  if (taps == 1 && c0 + 4 <= dw_c && dw_c % 4 == 0) {
+    float4* o = reinterpret_cast<float4*>(dw + k * dw_c + c0);
+    if (accumulate) {
+      const float4 w = *o;
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
+    *o = v;
+    return;
+  }
+  const float e4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (c0 + e >= dw_c) break;
+    const long dst = (k * dw_c + c0 + e) * taps + tap;
+    dw[dst] = accumulate ? dw[dst] + e4[e] : e4[e];
+  }
+}
+
+// Few slabs of a multi-tap filter: the transposing kernel (coalesced dW runs, one lane group per
+// block); otherwise the split-parallel kernel with ~4 (up to splits / 16) slabs per lane.
 static void launch_wgrad_reduce(const float* ws, int splits, int cout, int cin, int taps, float* dw, int dw_c,
                                 int accumulate, hipStream_t st) {
-  int sl = splits >= 64 ? 16 : splits >= 8 ? 4 : 1;
-  while (sl > 1 && (256 / sl) / taps < 1) sl /= 4;  // every tap of one 4-channel item in a lane group
-  int cw = 4 * ((256 / sl) / taps);
-  if (cw > 1024 / taps / 4 * 4) cw = 1024 / taps / 4 * 4;  // LDS transpose tile
-  if (cw > ceil_div(dw_c, 4) * 4) cw = ceil_div(dw_c, 4) * 4;
-  const int blocks = cout * ceil_div(dw_c, cw);
-  if (sl == 16)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c,
-                       accumulate, cw);
-  else if (sl == 4)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c,
-                       accumulate, cw);
-  else
-    hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c,
-                       accumulate, cw);
+  if (taps > 1 && splits <= 8 && taps <= 256) {
+    int cw = 4 * (256 / taps);
+    if (cw > 1024 / taps / 4 * 4) cw = 1024 / taps / 4 * 4;  // LDS transpose tile
+    if (cw > 64) cw = 64;
+    if (cw > ceil_div(dw_c, 4) * 4) cw = ceil_div(dw_c, 4) * 4;
+    hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(cout * ceil_div(dw_c, cw)), dim3(256), 0, st, ws, splits, cout,
+                       cin, taps, dw, dw_c, accumulate, cw);
+    return;
+  }
+  int sl = 1;  // at most 16 lanes: 16-item (256-B) runs per slab read, a short LDS combine
+  while (sl < 16 && sl * 4 < splits) sl *= 4;
+  const long s4 = (long)cout * taps * cin / 4;
+  const unsigned blocks = (unsigned)((s4 + 256 / sl - 1) / (256 / sl));
+  switch (sl) {
+    case 16: hipLaunchKernelGGL(wgrad_reduce_split_kernel<16>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c, accumulate); break;
+    case 4: hipLaunchKernelGGL(wgrad_reduce_split_kernel<4>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c, accumulate); break;
+    default: hipLaunchKernelGGL(wgrad_reduce_split_kernel<1>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c, accumulate); break;
+  }
 }
 
 // fp32 [K][C][R][S] -> T [K][R][S][Cpad] (zero-padded channels) and optionally T [C][R][S][K]
