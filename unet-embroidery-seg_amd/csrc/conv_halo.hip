@@ -100,30 +100,34 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     }
   }
 
-  // ---- halo geometry of this lane's DMA slots (identical for every tile) ----
-  int hrc[HI];  // (hr << 8) | hc, or -1 for lanes past the halo
+  // ---- halo geometry of this lane's DMA slots (identical for every tile): byte offset relative to
+  // the halo's top-left pixel (swizzle included) and which border of the halo the pixel lies on --
+  // with hc % TH == 0 and wc % 32 == 0 only border pixels can leave the image, so a tile's load is
+  // one add and one mask test per row ----
+  unsigned hoff[HI], hflag[HI];
 #pragma unroll
   for (int i = 0; i < HI; ++i) {
     const int idx = (i * NW + wid) * 64 + lane;
-    const int hp = idx >> 3;
-    hrc[i] = idx < HCH ? (((hp / (HW_TW + 2)) << 8) | (hp % (HW_TW + 2))) : -1;
+    const int hp = idx >> 3, hr = hp / (HW_TW + 2), hc = hp % (HW_TW + 2);
+    hoff[i] = (unsigned)(hr * a.W + hc) * (unsigned)a.ldc1b + swzh(hp, lane & 7) * 16u;
+    hflag[i] = idx >= HCH ? 16u : (hr == 0 ? 1u : 0u) | (hr == TH + 1 ? 2u : 0u) | (hc == 0 ? 4u : 0u) | (hc == HW_TW + 1 ? 8u : 0u);
   }
   auto issue_halo = [&](int t, int stage) {
     const int sp = slot + t * G_per;
     const int tw = sp % tiles_w, rest = sp / tiles_w;
     const int th = rest % tiles_h, nb = rest / tiles_h;
-    const int gh0 = th * TH - 1, gw0 = tw * HW_TW - 1;
-    const unsigned base = lds_addr(hl + stage * HCH);
+    const int h0 = th * TH, w0 = tw * HW_TW;
+    const unsigned base = __builtin_amdgcn_readfirstlane(lds_addr(hl + stage * HCH));
+    // origin (h0 - 1, w0 - 1) wraps below zero on the first row / column; the edge mask sends
+    // those lanes out of range
+    const unsigned hb = __builtin_amdgcn_readfirstlane((unsigned)((nb * a.H + h0 - 1) * a.W + w0 - 1) * (unsigned)a.ldc1b);
+    const unsigned kill = __builtin_amdgcn_readfirstlane(16u | (h0 == 0 ? 1u : 0u) | (h0 + TH >= a.H ? 2u : 0u) |
+                                                         (w0 == 0 ? 4u : 0u) | (w0 + HW_TW >= a.W ? 8u : 0u));
 #pragma unroll
     for (int i = 0; i < HI; ++i) {
-      const int v = hrc[i];
-      const int hr = v >> 8, hc = v & 255;
-      const int gh = gh0 + hr, gw = gw0 + hc;
-      const int hp = hr * (HW_TW + 2) + hc;
-      const int pc = lane & 7;
-      const bool ok = v >= 0 && gh >= 0 && gh < a.H && gw >= 0 && gw < a.W;
-      const unsigned off = ok ? (unsigned)((nb * a.H + gh) * a.W + gw) * (unsigned)a.ldc1b + swzh(hp, pc) * 16u : kOOB;
-      if (v >= 0 || HCH % (64 * NW) == 0) dma16(rx, base + (unsigned)((i * NW + wid) * 1024), off);
+      const unsigned off = (hflag[i] & kill) ? kOOB : hb + hoff[i];
+      // only the last row can hold lanes past the halo (they must not write LDS)
+      if (i < HI - 1 || HCH % (64 * NW) == 0 || hflag[i] != 16u) dma16(rx, base + (unsigned)((i * NW + wid) * 1024), off);
     }
   };
 
@@ -386,38 +390,45 @@ __global__ __launch_bounds__(256) void halo3_wgrad_kernel(HaloWgradArgs a, int t
   const __amdgpu_buffer_rsrc_t rdy = srd(a.dy, a.dy_bytes);
   const unsigned dycb = (unsigned)mt * 128u;
 
-  int hrc[HI];
+  // Lane constants of the DMA rows, so that a tile's loads cost one add (+ the halo edge test) per
+  // row: the byte offset relative to the tile's first pixel (dY) / its halo's top-left pixel (X),
+  // swizzle included, and for the halo which border (top, bottom, left, right) the lane's pixel
+  // lies on -- with H % TH == 0 and W % HW_TW == 0 only border halo pixels can leave the image.
+  const int pc = lane & 7;
+  unsigned doff[DI];
+#pragma unroll
+  for (int i = 0; i < DI; ++i) {
+    const int px = ((i * NW + wid) * 64 + lane) >> 3;
+    doff[i] = (unsigned)((px / HW_TW) * a.W + px % HW_TW) * (unsigned)a.ldyb + dycb + (unsigned)((pc ^ swz_tr8(px)) * 16);
+  }
+  unsigned hoff[HI], hflag[HI];
 #pragma unroll
   for (int i = 0; i < HI; ++i) {
     const int idx = (i * NW + wid) * 64 + lane;
-    const int hp = idx >> 3;
-    hrc[i] = idx < HCH ? (((hp / (HW_TW + 2)) << 8) | (hp % (HW_TW + 2))) : -1;
+    const int hp = idx >> 3, hr = hp / (HW_TW + 2), hc = hp % (HW_TW + 2);
+    hoff[i] = (unsigned)(hr * a.W + hc) * ldxb + xcb + (unsigned)((pc ^ swz_tr8(hp)) * 16);
+    hflag[i] = idx >= HCH ? 16u : (hr == 0 ? 1u : 0u) | (hr == TH + 1 ? 2u : 0u) | (hc == 0 ? 4u : 0u) | (hc == HW_TW + 1 ? 8u : 0u);
   }
   auto issue = [&](int t, int stage) {
     const int sp = slot + t * G_per;
     const int tw = sp % tiles_w, rest = sp / tiles_w;
     const int th = rest % tiles_h, nb = rest / tiles_h;
     const int h0 = th * TH, w0 = tw * HW_TW;
-    const unsigned base = lds_addr(lds + stage * STG);
-    const int pc = lane & 7;
+    const unsigned base = __builtin_amdgcn_readfirstlane(lds_addr(lds + stage * STG));
+    const unsigned tb = __builtin_amdgcn_readfirstlane((unsigned)((nb * a.H + h0) * a.W + w0) * (unsigned)a.ldyb);
 #pragma unroll
-    for (int i = 0; i < DI; ++i) {
-      const int inst = i * NW + wid;
-      const int px = (inst * 64 + lane) >> 3;
-      const unsigned pix = (unsigned)((nb * a.H + h0 + px / HW_TW) * a.W + w0 + px % HW_TW);
-      dma16(rdy, base + (unsigned)inst * 1024u, pix * (unsigned)a.ldyb + dycb + (unsigned)((pc ^ swz_tr8(px)) * 16));
-    }
+    for (int i = 0; i < DI; ++i) dma16(rdy, base + (unsigned)((i * NW + wid) * 1024), tb + doff[i]);
     const unsigned hbase = base + DCH * 16;
+    // halo origin (h0 - 1, w0 - 1): wraps below zero on the first row / column, whose lanes the
+    // edge mask sends out of range
+    const unsigned hb = __builtin_amdgcn_readfirstlane((unsigned)((nb * a.H + h0 - 1) * a.W + w0 - 1) * ldxb);
+    const unsigned kill = __builtin_amdgcn_readfirstlane(16u | (h0 == 0 ? 1u : 0u) | (h0 + TH >= a.H ? 2u : 0u) |
+                                                         (w0 == 0 ? 4u : 0u) | (w0 + HW_TW >= a.W ? 8u : 0u));
 #pragma unroll
     for (int i = 0; i < HI; ++i) {
-      const int v = hrc[i];
-      const int hr = v >> 8, hc = v & 255;
-      const int gh = h0 - 1 + hr, gw = w0 - 1 + hc;
-      const int hp = hr * (HW_TW + 2) + hc;
-      const bool ok = v >= 0 && gh >= 0 && gh < a.H && gw >= 0 && gw < a.W;
-      const unsigned off =
-          ok ? (unsigned)((nb * a.H + gh) * a.W + gw) * ldxb + xcb + (unsigned)((pc ^ swz_tr8(hp)) * 16) : kOOB;
-      if (v >= 0 || HCH % (64 * NW) == 0) dma16(rx, hbase + (unsigned)((i * NW + wid) * 1024), off);
+      const unsigned off = (hflag[i] & kill) ? kOOB : hb + hoff[i];
+      // only the last row can hold lanes past the halo (they must not write LDS)
+      if (i < HI - 1 || HCH % (64 * NW) == 0 || hflag[i] != 16u) dma16(rx, hbase + (unsigned)((i * NW + wid) * 1024), off);
     }
   };
 
