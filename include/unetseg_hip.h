@@ -73,6 +73,15 @@ int unetseg_conv2d_fwd_bnrelu_in(int dtype, const void* x1, int c1, int ldc1, in
                                  void* y, int ldy, float* stats, void* stream);
 /* TN configuration that call runs (host-only query, -1 = none) */
 int unetseg_conv2d_fwd_bnrelu_in_config(int dtype, int c1, int ldc1, int n, int h, int w, int cout);
+/* The decoder's last 3x3 conv (64 -> 64, stride 1, pad 1, bias + ReLU; reference model/unet_resnet.py:77-78)
+ * with the final 1x1 conv (model/unet_resnet.py:79, 64 -> head_k in {1, 2}) fused into its epilogue:
+ * y as unetseg_conv2d_fwd, logits fp32 [n][head_k][h][w] = head_b + head_w . y (the stored bf16 y).
+ * Replaces the reference's Conv2d -> ReLU -> Conv2d(1x1) forward.  bf16, halo path only; the _ok
+ * query (host only) says whether a shape qualifies. */
+int unetseg_conv2d_fwd_head_ok(int dtype, int ldc1, int n, int h, int w, int ldy, int head_k);
+int unetseg_conv2d_fwd_head(int dtype, const void* x1, int ldc1, int n, int h, int w, const void* wk,
+                            const float* bias, void* y, int ldy, int head_k, const float* head_w, const float* head_b,
+                            float* logits, void* stream);
 /* its weight gradient with the same input prologue (workspace: unetseg_conv2d_wgrad_workspace) */
 int unetseg_conv2d_wgrad_bnrelu_in(int dtype, const void* x1, int c1, int ldc1, int n, int h, int w, const void* dy,
                                    int ldy, int cout, const float* in_sc, const float* in_sh, float* ws,

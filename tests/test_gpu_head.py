@@ -1,0 +1,98 @@
+"""GPU: the model's 1x1 head fused into the epilogue of the decoder's last 3x3 conv
+(unetseg_conv2d_fwd_head; reference model/unet_resnet.py:77-79 up_conv[3..4] -> final, and the
+multitask seg_head).
+
+* the activation y it stores is bit-identical to the plain conv (unetseg_conv2d_fwd);
+* its logits equal a float64 head applied to that stored bf16 y (fp32 sums in another order than the
+  separate head kernel: 1e-5 of max|logit|), for 1 and 2 logits, at the bench's 512x512 rows and a
+  multi-image case;
+* unet_resnet50 / multitask_unet bf16 forward: logits with the fusion equal those without within the
+  same bound, and the training step's gradients agree to 1 % in norm (the backward is the same
+  kernels; only bf16 roundings of the loss gradient can flip).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from unetseg_hip import load
+    load()
+
+
+def _st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+@pytest.mark.parametrize("N,H,W,Kh", [(2, 64, 256, 2), (2, 64, 256, 1), (3, 32, 64, 2), (1, 512, 512, 2)])
+def test_conv_fwd_head(N, H, W, Kh):
+    from unetseg_hip.lib import DT_BF16, lib
+    g = torch.Generator(device=DEV).manual_seed(N * 1000 + H + Kh)
+    C = 64
+    x = torch.randn(N, H, W, C, generator=g, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(C, C, 3, 3, generator=g, device=DEV) / math.sqrt(9 * C)).contiguous()
+    b = torch.randn(C, generator=g, device=DEV) * 0.1
+    hw = torch.randn(Kh, C, 1, 1, generator=g, device=DEV) / 8.0
+    hb = torch.randn(Kh, generator=g, device=DEV)
+    wk = torch.empty(C, 3, 3, C, dtype=torch.bfloat16, device=DEV)
+    wt = torch.empty(C, 3, 3, C, dtype=torch.bfloat16, device=DEV)
+    lib.pack_conv_weight(DT_BF16, w.data_ptr(), C, C, 3, 3, C, wk.data_ptr(), wt.data_ptr(), _st())
+    assert lib.conv2d_fwd_head_ok(DT_BF16, C, N, H, W, C, Kh) == 1
+    assert lib.conv2d_fwd_head_ok(DT_BF16, C, N, H, W, C, 3) == 0
+    y_ref = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=DEV)
+    lib.conv2d_fwd(DT_BF16, x.data_ptr(), C, C, 0, 0, 0, N, H, W, wk.data_ptr(), C, 3, 3, 1, 1, b.data_ptr(), 1,
+                   y_ref.data_ptr(), C, 0, _st())
+    y = torch.full((N, H, W, C), float("nan"), dtype=torch.bfloat16, device=DEV)
+    logits = torch.full((N, Kh, H, W), float("nan"), device=DEV)
+    lib.conv2d_fwd_head(DT_BF16, x.data_ptr(), C, N, H, W, wk.data_ptr(), b.data_ptr(), y.data_ptr(), C, Kh,
+                        hw.data_ptr(), hb.data_ptr(), logits.data_ptr(), _st())
+    torch.cuda.synchronize()
+    assert torch.equal(y.view(torch.int16), y_ref.view(torch.int16)), "stored activation differs from the plain conv"
+    ref = torch.einsum("nhwc,kc->nkhw", y.double(), hw.view(Kh, C).double()) + hb.double().view(1, Kh, 1, 1)
+    err = (logits.double() - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item() + 1e-6, err
+
+
+@pytest.mark.parametrize("name", ["unet_resnet50", "multitask_unet"])
+def test_model_head_fusion_unchanged(name):
+    from model.model_factory import build_model
+    from unetseg_hip import ops
+    from unetseg_hip.losses import binary_segmentation_loss
+    from utils.synthetic import make_batch
+
+    torch.manual_seed(0)
+    kw = dict(num_classes=1) if name == "multitask_unet" else dict(num_classes=2)
+    m = build_model(name, **kw).cuda().train()
+    m.compute_dtype = "bf16"
+    x, y = make_batch(2, 64, seed=7)
+    x, y = x.cuda(), y.cuda()
+    outs = []
+    for fuse in (False, True):
+        ops.FUSE_HEAD = fuse
+        try:
+            m.zero_grad(set_to_none=False)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = m(x)
+            seg = out[0] if isinstance(out, tuple) else out
+            if seg.shape[1] == 2:
+                loss = binary_segmentation_loss(seg, y, "bce")
+            else:
+                loss = torch.nn.functional.binary_cross_entropy_with_logits(seg[:, 0], y.float())
+            loss.backward()
+            torch.cuda.synchronize()
+            outs.append((seg.detach().clone(), [p.grad.detach().clone() for p in m.parameters()]))
+        finally:
+            ops.FUSE_HEAD = True
+    (s0, g0), (s1, g1) = outs
+    assert (s0 - s1).abs().max().item() <= 1e-5 * s0.abs().max().item() + 1e-6
+    # the backward runs the same kernels; the logits differ by fp32 summation order only, which can
+    # flip a bf16 rounding of the gradient here and there: relative norm, not elementwise
+    for a, b in zip(g0, g1):
+        assert (a - b).norm().item() <= 1e-2 * a.norm().item() + 1e-8

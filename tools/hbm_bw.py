@@ -18,3 +18,10 @@ for mb in (64, 256, 1024):
     e1.record(); torch.cuda.synchronize()
     t = e0.elapsed_time(e1) / 20 * 1e-3
     print(f"sum {mb} MB: {n/t/1e12:.2f} TB/s read {t*1e6:.1f} us")
+    for _ in range(3): y.fill_(1)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(20): y.fill_(1)
+    e1.record(); torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 20 * 1e-3
+    print(f"fill {mb} MB: {n/t/1e12:.2f} TB/s write {t*1e6:.1f} us")

@@ -909,6 +909,38 @@ UNETSEG_API int unetseg_conv2d_fwd_bnrelu_in_config(int dtype, int c1, int ldc1,
   return tn_fast_config(f, nullptr);
 }
 
+// The decoder's last 3x3 conv (64 -> 64, stride 1, pad 1, bias, ReLU; model/unet_resnet.py:77-78
+// up_conv[3..4]) with the model's 1x1 head (model/unet_resnet.py:79 `final`, 64 -> head_k logits,
+// head_k = 1 or 2) fused into its epilogue: y as unetseg_conv2d_fwd, plus fp32 planar NCHW logits
+// computed from the stored (rounded) y -- the separate head pass (unetseg_pw_small_fwd) would
+// re-read all of y.  bf16, halo path only (unetseg_conv2d_fwd_head_ok).
+static bool head_args(const void* x1, int ldc1, int n, int h, int w, const void* wk, int ldy, FastTNArgs& f) {
+  IgemmArgs a = fwd_args(x1, 64, ldc1, nullptr, 0, 0, n, h, w, wk, 64, 3, 3, 1, 1);
+  a.ldy = ldy; a.relu = 1;
+  return fast_tn_args(a, f) && halo3_ok(f);
+}
+
+UNETSEG_API int unetseg_conv2d_fwd_head_ok(int dtype, int ldc1, int n, int h, int w, int ldy, int head_k) {
+  FastTNArgs f;
+  return dtype == DT_BF16 && (head_k == 1 || head_k == 2) && ldy >= 64 && ldc1 % 8 == 0 &&
+         head_args(kSomePtr, ldc1, n, h, w, kSomePtr, ldy, f);
+}
+
+UNETSEG_API int unetseg_conv2d_fwd_head(int dtype, const void* x1, int ldc1, int n, int h, int w, const void* wk,
+                                        const float* bias, void* y, int ldy, int head_k, const float* head_w,
+                                        const float* head_b, float* logits, void* stream) {
+  US_CHECK_ARG(x1 && wk && bias && y && head_w && head_b && logits, "conv2d_fwd_head: null pointer");
+  US_CHECK_ARG(unetseg_conv2d_fwd_head_ok(dtype, ldc1, n, h, w, ldy, head_k),
+               "conv2d_fwd_head: needs bf16, 64 -> 64 channels on the halo path and head_k 1 or 2");
+  FastTNArgs f;
+  head_args(x1, ldc1, n, h, w, wk, ldy, f);
+  f.y = y; f.bias = bias; f.relu = 1;
+  f.head_w = head_w; f.head_b = head_b; f.head_y = logits; f.head_k = head_k;
+  US_CHECK_ARG(launch_halo3(f, (hipStream_t)stream) == 0, "conv2d_fwd_head: launch refused");
+  US_LAUNCH_CHECK("conv2d_fwd_head");
+  return 0;
+}
+
 // Weight gradient of that conv: X = relu(x1 * in_sc + in_sh) staged on the fly (fast bf16 wgrad),
 // then the usual deterministic split-K reduce into dw (fp32 [cout][dw_c], (+)= with accumulate).
 UNETSEG_API int unetseg_conv2d_wgrad_bnrelu_in(int dtype, const void* x1, int c1, int ldc1, int n, int h, int w,

@@ -45,6 +45,12 @@ struct FastTNArgs {
   // (its BN-ReLU output, never materialised); register-staged configurations only, x2 == NULL
   const float* in_sc;
   const float* in_sh;
+  // fused 1x1 head (halo forward with bias + ReLU only): head_y[n][k][pixel] = head_b[k] +
+  // sum_c bf16(y[pixel][c]) * head_w[k][c], k < head_k (1 or 2), fp32 planar NCHW logits
+  const float* head_w;
+  const float* head_b;
+  float* head_y;
+  int head_k;
 };
 
 struct FastWgradArgs {

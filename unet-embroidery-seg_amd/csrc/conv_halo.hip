@@ -36,7 +36,14 @@ __device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, unsigned off,
 // EPI: epilogue flags fixed at compile time (kEpiBias | kEpiRelu | kEpiStats | kEpiAcc), or kEpiDyn
 // to read them from the arguments; with them fixed the tile epilogue has no uniform branches and
 // the bias sits in registers.
-constexpr int kEpiBias = 1, kEpiRelu = 2, kEpiStats = 4, kEpiAcc = 8, kEpiDyn = 16;
+// kEpiHead1 / kEpiHead2: the model's final 1x1 conv (64 -> 1 or 2 logits) on the rounded outputs
+// (model/unet_resnet.py:99-103 `final`, model/unet_multitask.py seg_head): the 512^2 activation is
+// not read back by a separate head pass.
+constexpr int kEpiBias = 1, kEpiRelu = 2, kEpiStats = 4, kEpiAcc = 8, kEpiDyn = 16, kEpiHead1 = 32, kEpiHead2 = 64;
+
+__device__ __forceinline__ void bstore32(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
+  asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
+}
 
 template <int TH, int NW, int POST, int EPI>
 __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_w, int tiles_h, int n_sp, int G_per,
@@ -46,6 +53,8 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   const bool do_relu = kDyn ? a.relu != 0 : (EPI & kEpiRelu) != 0;
   const bool do_stats = kDyn ? a.stats != nullptr : (EPI & kEpiStats) != 0;
   const bool do_acc = kDyn ? a.accumulate != 0 : (EPI & kEpiAcc) != 0;
+  constexpr int HK = (EPI & kEpiHead2) ? 2 : (EPI & kEpiHead1) ? 1 : 0;  // fused head logits
+  static_assert(HK == 0 || (!kDyn && POST == 0), "the fused head rides on a fixed bias + ReLU epilogue");
   // wave w owns output rows [w*TH/NW, (w+1)*TH/NW)
   constexpr int RPW = TH / NW;               // rows per wave
   constexpr int FP = RPW * (HW_TW / 16);     // 16-pixel groups per wave
@@ -61,6 +70,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   uint4* hl = lds + WCH;                     // [2][HP][8]
   float* red = reinterpret_cast<float*>(hl + 2 * HCH);  // [NW][64]
   float* sbias = red + NW * 64;              // [64]
+  float* hwl = sbias + 64;                   // head: [HK][64] weights, then [HK] biases
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -73,6 +83,10 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   const __amdgpu_buffer_rsrc_t rw = srd(a.wt, a.w_bytes);
   const __amdgpu_buffer_rsrc_t ry = srd(a.y, y_bytes);
   (void)ntn;
+  const unsigned hw_img = (unsigned)(a.OH * a.OW);
+  const __amdgpu_buffer_rsrc_t rh = srd(HK ? (const void*)a.head_y : a.y,
+                                        HK ? (unsigned)(a.M / (a.OH * a.OW)) * HK * hw_img * 4u : 0u);
+  if (HK && tid < HK * 65) hwl[tid] = tid < HK * 64 ? a.head_w[tid] : a.head_b[tid - HK * 64];
 
   if (kDyn && a.bias && tid < 64) sbias[tid] = a.bias[n0 + tid];
   // BN post-op coefficients of this block's 64 channels live in `red` (free in dgrad: no stats)
@@ -268,6 +282,29 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
         outv[c][p] = *reinterpret_cast<uint2*>(o);
       }
     }
+    if (HK) {
+      // head logits of this lane's pixels: 16 channels per lane, then the four channel groups
+      // (lanes j16 + 16 kg) summed by cross-row shuffles; lanes kg == 0 store, the others' stores
+      // go out of range (every wave issues exactly FP * HK head stores)
+#pragma unroll
+      for (int p = 0; p < FP; ++p) {
+        const int r = wid * RPW + p / (HW_TW / 16);
+        const int col = (p % (HW_TW / 16)) * 16 + j16;
+        const unsigned pix = (unsigned)((th * TH + r) * a.OW + tw * HW_TW + col);
+#pragma unroll
+        for (int k = 0; k < HK; ++k) {
+          float hs = 0.f;
+#pragma unroll
+          for (int c = 0; c < FC; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) hs = fmaf(acc[c][p][e], hwl[k * 64 + c * 16 + kg * 4 + e], hs);
+          hs += __shfl_xor(hs, 16);
+          hs += __shfl_xor(hs, 32);
+          hs += hwl[HK * 64 + k];
+          bstore32(rh, kg == 0 ? ((unsigned)(nb * HK + k) * hw_img + pix) * 4u : kOOB, hs);
+        }
+      }
+    }
     if (do_stats) {
       // per-tile BN partials over the TH*32 pixels: column sums, then M2 about the tile mean
 #pragma unroll
@@ -324,7 +361,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
       for (int c = 0; c < FC; ++c) bstore64(ry, outo[p] + (c * 16 + kg * 4) * 2, outv[c][p]);
     // next halo landed (all but this tile's FP*FC stores retired) and every wave is done with
     // both the current stage (WAR for the DMA after next) and `red`
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(FP * FC) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(FP * FC + FP * HK) : "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (POST) {
@@ -504,8 +541,9 @@ __global__ __launch_bounds__(256) void halo3_wgrad_kernel(HaloWgradArgs a, int t
 }
 
 template <int TH, int NW>
-size_t halo_lds_bytes() {
-  return (size_t)9 * 64 * 128 + 2 * (size_t)(TH + 2) * (HW_TW + 2) * 128 + NW * 64 * 4 + 64 * 4;
+size_t halo_lds_bytes(int head_k = 0) {
+  return (size_t)9 * 64 * 128 + 2 * (size_t)(TH + 2) * (HW_TW + 2) * 128 + NW * 64 * 4 + 64 * 4 +
+         (size_t)head_k * 65 * 4;
 }
 
 }  // namespace
@@ -534,7 +572,8 @@ static int launch_halo3_cfg(const FastTNArgs& a, hipStream_t st) {
   int G_per = 256 / ntn;
   if (G_per < 1) G_per = 1;
   if (G_per > n_sp) G_per = n_sp;
-  const size_t lds = halo_lds_bytes<TH, NW>();
+  constexpr int HK = (EPI & kEpiHead2) ? 2 : (EPI & kEpiHead1) ? 1 : 0;
+  const size_t lds = halo_lds_bytes<TH, NW>(HK);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_kernel<TH, NW, POST, EPI>),
@@ -563,6 +602,11 @@ int launch_halo3(const FastTNArgs& a, hipStream_t st) {
   static const bool dyn = getenv("UNETSEG_HALO_EPI_DYN") != nullptr;
   const int epi = (a.bias ? kEpiBias : 0) | (a.relu ? kEpiRelu : 0) | (a.stats ? kEpiStats : 0) |
                   (a.accumulate ? kEpiAcc : 0);
+  if (a.head_y) {  // fused head: bias + ReLU epilogue only (checked by the caller)
+    if (a.post || epi != (kEpiBias | kEpiRelu) || (a.head_k != 1 && a.head_k != 2)) return -1;
+    return a.head_k == 2 ? launch_halo3_cfg<8, 8, 0, kEpiBias | kEpiRelu | kEpiHead2>(a, st)
+                         : launch_halo3_cfg<8, 8, 0, kEpiBias | kEpiRelu | kEpiHead1>(a, st);
+  }
   // fused dgrad post-ops come with a plain epilogue (no bias / ReLU / stats / accumulate)
   if (a.post == 1) return epi == 0 && !dyn ? launch_halo3_cfg<8, 8, 1, 0>(a, st) : launch_halo3_cfg<8, 8, 1, kEpiDyn>(a, st);
   if (a.post == 2) return epi == 0 && !dyn ? launch_halo3_cfg<8, 8, 2, 0>(a, st) : launch_halo3_cfg<8, 8, 2, kEpiDyn>(a, st);

@@ -46,7 +46,7 @@ class MultiTaskUNet(HipModel):
         self._drop_step += 1
         cls, cls_holder, _ = ops.cls_head(ctx, feats[4], self.cls_head, self.dropout_mask,
                                           seed=0x5EED0000 + self._drop_step)
-        u = run_resnet_decoder(ctx, self, feats)
+        u = run_resnet_decoder(ctx, self, feats, head=self.seg_head)
         seg, seg_holder = ops.pw_head(ctx, u, self.seg_head)
         ctx.out_holders = [seg_holder, cls_holder]
         return seg, cls

@@ -33,8 +33,9 @@ def run_unet_up(ctx, m, skip, x):
     return h
 
 
-def run_resnet_decoder(ctx, m, feats):
-    """unet_resnet.py:92-100 (shared by MultiTaskUNet)"""
+def run_resnet_decoder(ctx, m, feats, head=None):
+    """unet_resnet.py:92-100 (shared by MultiTaskUNet).  head: the model's 1x1 head conv, fused into
+    the last conv's epilogue where the shape allows (ops.pw_head then reuses those logits)"""
     f1, f2, f3, f4, f5 = feats
     u = run_unet_up(ctx, m.up_concat4, f4, f5)
     u = run_unet_up(ctx, m.up_concat3, f3, u)
@@ -42,7 +43,7 @@ def run_resnet_decoder(ctx, m, feats):
     u = run_unet_up(ctx, m.up_concat1, f1, u)
     u = ops.upsample2x(ctx, u, align_corners=True)
     u, _ = ops.conv(ctx, u, m.up_conv[1]._pc, relu=True)
-    u, _ = ops.conv(ctx, u, m.up_conv[3]._pc, relu=True)
+    u, _ = ops.conv(ctx, u, m.up_conv[3]._pc, relu=True, head=head)
     return u
 
 
@@ -68,7 +69,7 @@ class Unet(HipModel):
     def _run(self, ctx, x):
         self._pack_weights(ctx, ctx.tape is not None)
         feats = run_resnet(ctx, self.resnet, x)
-        u = run_resnet_decoder(ctx, self, feats)
+        u = run_resnet_decoder(ctx, self, feats, head=self.final)
         logits, holder = ops.pw_head(ctx, u, self.final)
         ctx.out_holders = [holder]
         return logits

@@ -36,7 +36,7 @@ class Node:
     ``lazy`` (a BNState): the node stands for relu(BN(data)) that was never stored -- ``data`` is the
     BN input and the consuming conv applies BN-ReLU on load (``bn(..., lazy=True)``)."""
 
-    __slots__ = ("data", "grad", "need_grad", "uses", "fuse", "fused", "lazy")
+    __slots__ = ("data", "grad", "need_grad", "uses", "fuse", "fused", "lazy", "head")
 
     def __init__(self, data, need_grad=True):
         self.data = data
@@ -46,6 +46,7 @@ class Node:
         self.fuse = None
         self.fused = None
         self.lazy = None
+        self.head = None  # (head Conv2d, fp32 logits) computed by the producing conv's epilogue
 
     @property
     def shape(self):
@@ -60,6 +61,8 @@ def use(*nodes):
 
 #: fuse ReLU / BN-ReLU backward pass 1 into the consumer conv's dgrad (UNETSEG_NO_FUSE=1 disables)
 FUSE = os.environ.get("UNETSEG_NO_FUSE", "0") != "1"
+#: the model's 1x1 head computed in the epilogue of the conv before it (UNETSEG_NO_HEAD_FUSE=1 disables)
+FUSE_HEAD = os.environ.get("UNETSEG_NO_HEAD_FUSE", "0") != "1"
 
 
 _WORKSPACES = {}
@@ -267,10 +270,13 @@ def pack_input(ctx, x, cpad=8):
 PAD_K = os.environ.get("UNETSEG_NO_PADK", "0") != "1"
 
 
-def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None):
+def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
     """y = conv(cat[x1, x2]) (+bias if the conv has one, ReLU).  Stride/padding come from the
     Conv2d container.  out: an NHWC view (pixel stride >= K) to write y into, e.g. a channel slice
-    of a dense block's concatenation buffer.  Returns (Node y, BN partials or None)."""
+    of a dense block's concatenation buffer.  head: the 1x1 Conv2d (1 or 2 outputs) that consumes y
+    next -- its logits come out of this conv's epilogue when the shape runs on the halo kernel
+    (unetseg_conv2d_fwd_head) and ride on the returned node for pw_head.  Returns (Node y, BN
+    partials or None)."""
     stride, pad = pc.conv.stride, pc.conv.padding
     lazy = x1.lazy
     if lazy is not None and not (x2 is None and ctx.dt == DT_BF16 and pc.R == 1 and pc.S == 1 and stride == 1 and
@@ -301,11 +307,23 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None):
         with _probe("igemm_tn", flops, 1, ("fwd_bnrelu_in",) + desc):
             lib.conv2d_fwd_bnrelu_in(ctx.dt, P(X1), C1, ldp(X1), N, H, W, P(pc.wk), K, P(lazy.sc), P(lazy.sh), P(b),
                                      int(relu), P(y), ldp(y), P(st[0] if st else None), ctx.stream)
+    elif head is not None and (FUSE_HEAD and x2 is None and relu and st is None and b is not None and
+                               head.bias is not None and K == 64 and
+                               C1 == 64 and (R, S, stride, pad) == (3, 3, 1, 1) and
+                               lib.conv2d_fwd_head_ok(ctx.dt, ldp(X1), N, H, W, ldp(y), head.weight.shape[0])):
+        Kh = head.weight.shape[0]
+        logits = torch.empty((N, Kh, Pq, Qq), dtype=torch.float32, device=ctx.device)
+        with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
+            lib.conv2d_fwd_head(ctx.dt, P(X1), ldp(X1), N, H, W, P(pc.wk), P(b), P(y), ldp(y), Kh, P(head.weight),
+                                P(head.bias), P(logits), ctx.stream)
+        head = (head, logits)
     else:
+        head = None
         with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
             lib.conv2d_fwd(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride, pad,
                            P(b), int(relu), P(y), ldp(y), P(st[0] if st else None), ctx.stream)
     out = Node(y)
+    out.head = head
     if relu:
         out.fuse = (1, y, None)
 
@@ -754,10 +772,13 @@ def pw_head(ctx, x, conv_mod):
     N, H, W, C = X.shape
     K = conv_mod.weight.shape[0]
     M = N * H * W
-    y = torch.empty((N, K, H, W), dtype=torch.float32, device=ctx.device)
-    if K > 2:
+    if x.head is not None and x.head[0] is conv_mod:
+        y = x.head[1]  # computed by the producing conv's epilogue (conv(..., head=conv_mod))
+    elif K > 2:
+        y = torch.empty((N, K, H, W), dtype=torch.float32, device=ctx.device)
         lib.pw_head_fwd(ctx.dt, P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(conv_mod.bias), P(y), ctx.stream)
     else:
+        y = torch.empty((N, K, H, W), dtype=torch.float32, device=ctx.device)
         lib.pw_small_fwd(ctx.dt, P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(conv_mod.bias), P(y), 0,
                          ctx.stream)
     holder = {}
