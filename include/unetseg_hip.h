@@ -205,6 +205,14 @@ int unetseg_upsample2x_fwd(int dtype, const void* x, int ldx, int n, int h, int 
                            int ldy, void* stream);
 int unetseg_upsample2x_bwd(int dtype, const void* dy, int ldy, int n, int h, int w, int c, int align_corners,
                            void* dx, int ldx, int accumulate, void* stream);
+/* upsample2x_bwd with the backward of the ReLU that produced x fused in (x = A, that ReLU's output, the
+ * upsample its sole consumer; reference model/unet_resnet.py:25-33 unetUp conv2 -> ReLU -> next
+ * block's UpsamplingBilinear2d): dx = (A > 0) ? adjoint(dy) : 0 (no accumulate); part fp32
+ * [rows][2][c], slot 0 = per-block column sums of dx (the conv's bias-gradient partials,
+ * unetseg_colsum_rows); rows = unetseg_upsample2x_bwd_tiles(...) */
+int unetseg_upsample2x_bwd_tiles(int dtype, int n, int h, int w, int c);
+int unetseg_upsample2x_bwd_relu(int dtype, const void* dy, int ldy, int n, int h, int w, int c, int align_corners,
+                                const void* a, int lda, void* dx, int ldx, float* part, int rows, void* stream);
 int unetseg_add(int dtype, const void* x, int ldx, void* out, int ldo, long M, int c, void* stream);
 /* general bilinear resize to (oh, ow) with ATen's source-index rule (F.interpolate(size=...):
  * model/unet_attention.py:31-33,52-53, model/unet_dualdense.py:57-58; align_corners=True for the

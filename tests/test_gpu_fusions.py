@@ -1,4 +1,6 @@
-"""GPU: the model's 1x1 head fused into the epilogue of the decoder's last 3x3 conv
+"""GPU: producer/consumer fusions of the decoder, each against its unfused kernels.
+
+Head: the model's 1x1 head fused into the epilogue of the decoder's last 3x3 conv
 (unetseg_conv2d_fwd_head; reference model/unet_resnet.py:77-79 up_conv[3..4] -> final, and the
 multitask seg_head).
 
@@ -9,6 +11,11 @@ multitask seg_head).
 * unet_resnet50 / multitask_unet bf16 forward: logits with the fusion equal those without within the
   same bound, and the training step's gradients agree to 1 % in norm (the backward is the same
   kernels; only bf16 roundings of the loss gradient can flip).
+
+Upsample backward + ReLU backward (unetseg_upsample2x_bwd_relu; unetUp conv2 -> ReLU -> the next
+block's UpsamplingBilinear2d, model/unet_resnet.py:25-33): the stored gradient is bit-identical to
+upsample2x_bwd followed by relu_bwd_bias, the bias partials sum to the same column sums (fp32
+summation order: 1e-5 relative), at every decoder shape of the 512x512 bench.
 """
 import math
 
@@ -96,3 +103,32 @@ def test_model_head_fusion_unchanged(name):
     # flip a bf16 rounding of the gradient here and there: relative norm, not elementwise
     for a, b in zip(g0, g1):
         assert (a - b).norm().item() <= 1e-2 * a.norm().item() + 1e-8
+
+
+@pytest.mark.parametrize("N,H,W,C,align", [(16, 256, 256, 64, 1), (16, 128, 128, 128, 1), (16, 32, 32, 512, 1),
+                                           (2, 24, 40, 64, 0), (3, 5, 7, 256, 1)])
+def test_upsample_bwd_relu(N, H, W, C, align):
+    from unetseg_hip.lib import DT_BF16, lib
+    g = torch.Generator(device=DEV).manual_seed(N * 7 + H + C)
+    dy = torch.randn(N, 2 * H, 2 * W, C, generator=g, device=DEV).to(torch.bfloat16)
+    a = torch.relu(torch.randn(N, H, W, C, generator=g, device=DEV)).to(torch.bfloat16)
+    # reference: the unfused kernels
+    da = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=DEV)
+    lib.upsample2x_bwd(DT_BF16, dy.data_ptr(), C, N, H, W, C, align, da.data_ptr(), C, 0, _st())
+    M = N * H * W
+    Gr = lib.reduce_tiles(DT_BF16, M, C, None, None)
+    pref = torch.zeros(C, Gr, device=DEV)
+    dref = torch.empty_like(da)
+    lib.relu_bwd_bias(DT_BF16, da.data_ptr(), C, a.data_ptr(), C, dref.data_ptr(), C, M, C, pref.data_ptr(), Gr,
+                      _st())
+    rows = lib.upsample2x_bwd_tiles(DT_BF16, N, H, W, C)
+    part = torch.full((rows, 2, C), float("nan"), device=DEV)
+    dx = torch.full((N, H, W, C), float("nan"), dtype=torch.bfloat16, device=DEV)
+    lib.upsample2x_bwd_relu(DT_BF16, dy.data_ptr(), C, N, H, W, C, align, a.data_ptr(), C, dx.data_ptr(), C,
+                            part.data_ptr(), rows, _st())
+    torch.cuda.synchronize()
+    assert torch.equal(dx.view(torch.int16), dref.view(torch.int16)), "masked gradient differs"
+    got = part[:, 0, :].double().sum(0)
+    ref = pref.double().sum(1)
+    assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-5
+    assert torch.allclose(got, dx.double().sum((0, 1, 2)), rtol=1e-5, atol=1e-4)

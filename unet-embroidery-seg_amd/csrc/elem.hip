@@ -620,44 +620,72 @@ __device__ __forceinline__ void up_range(int i, int in, int out, int align, int&
   hi = min(hi, out - 1);
 }
 
+// Nonzero taps of input index i along one axis: the bilinear hat's support is contiguous and holds
+// at most kUpK output indices at x2 in either align mode (open interval of length 4 + 2/(in-1) for
+// align_corners, 4 for half-pixel) -> d0 and the weights of d0 .. d0 + kUpK - 1 (zero past the end).
+constexpr int kUpK = 5;
+__device__ __forceinline__ void up_taps(int i, int in, int out, int align, int& d0, float (&wt)[kUpK]) {
+  int lo, hi;
+  up_range(i, in, out, align, lo, hi);
+  d0 = hi + 1;
+  for (int d = hi; d >= lo; --d)
+    if (up_w(d, i, in, out, align) != 0.f) d0 = d;
+#pragma unroll
+  for (int k = 0; k < kUpK; ++k) wt[k] = d0 + k <= hi ? up_w(d0 + k, i, in, out, align) : 0.f;
+  if (d0 > hi) d0 = lo;
+}
+
+// adjoint of one input pixel (row r = n*H + h, this lane's columns cd0.. with weights cw): every tap
+// load is issued before the first is consumed (the skip-zero loop exposed one load latency per
+// tap); same products and summation order (rows, then columns; zero weights skipped) as that loop
+template <typename T>
+__device__ __forceinline__ void up_adjoint(const T* dy, int ldy, int n, int h, int H, int OH, int OW, int align,
+                                           int cd0, const float (&cw)[kUpK], int c0, float (&acc)[VE<T>]) {
+  constexpr int V = VE<T>;
+  int rd0;
+  float rw[kUpK];
+  up_taps(h, H, OH, align, rd0, rw);
+  uint4 g[kUpK][kUpK];
+#pragma unroll
+  for (int kh = 0; kh < kUpK; ++kh)
+#pragma unroll
+    for (int kw = 0; kw < kUpK; ++kw)
+      g[kh][kw] = (rw[kh] != 0.f && cw[kw] != 0.f)
+                      ? *reinterpret_cast<const uint4*>(dy + ((long)(n * OH + rd0 + kh) * OW + cd0 + kw) * ldy + c0)
+                      : uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = 0.f;
+#pragma unroll
+  for (int kh = 0; kh < kUpK; ++kh)
+#pragma unroll
+    for (int kw = 0; kw < kUpK; ++kw)
+      if (rw[kh] != 0.f && cw[kw] != 0.f) {
+        float gv[V];
+        cvt16<T>(g[kh][kw], gv);
+        const float wt = rw[kh] * cw[kw];
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] += wt * gv[e];
+      }
+}
+
 // gather form of the adjoint: dx[h][w] (+)= sum_{oh,ow} wh(oh,h) ww(ow,w) dy[oh][ow]; row-blocked
 // like the forward (row weights wave-uniform, column weights once per lane)
 template <typename T>
-__global__ void upsample_bwd_kernel(const T* dy, int ldy, int N, int H, int W, int C, int align, T* dx, int ldx,
+__global__ __launch_bounds__(256) void upsample_bwd_kernel(const T* dy, int ldy, int N, int H, int W, int C, int align, T* dx, int ldx,
                                     int accumulate) {
   constexpr int V = VE<T>;
   const int cv = C / V, OH = 2 * H, OW = 2 * W;
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= W * cv) return;
   const int w = idx / cv, c0 = (idx - w * cv) * V;
-  int owl, owh;
-  up_range(w, W, OW, align, owl, owh);
-  float wwv[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) wwv[k] = owl + k <= owh ? up_w(owl + k, w, W, OW, align) : 0.f;
+  int cd0;
+  float cw[kUpK];
+  up_taps(w, W, OW, align, cd0, cw);
   const int r0 = blockIdx.y * kUpRowsPB, r1 = min(r0 + kUpRowsPB, N * H);
   for (int r = r0; r < r1; ++r) {
     const int n = r / H, h = r - n * H;
-    int ohl, ohh;
-    up_range(h, H, OH, align, ohl, ohh);
     float acc[V];
-#pragma unroll
-    for (int e = 0; e < V; ++e) acc[e] = 0.f;
-#pragma unroll
-    for (int kh = 0; kh < 8; ++kh) {
-      const float wh = ohl + kh <= ohh ? up_w(ohl + kh, h, H, OH, align) : 0.f;
-      if (wh == 0.f) continue;
-      const T* row = dy + (long)(n * OH + ohl + kh) * OW * ldy + c0;
-#pragma unroll
-      for (int kw = 0; kw < 8; ++kw) {
-        if (wwv[kw] == 0.f) continue;
-        float g[V];
-        load_vec(row + (long)(owl + kw) * ldy, g);
-        const float wt = wh * wwv[kw];
-#pragma unroll
-        for (int e = 0; e < V; ++e) acc[e] += wt * g[e];
-      }
-    }
+    up_adjoint<T>(dy, ldy, n, h, H, OH, OW, align, cd0, cw, c0, acc);
     T* o = dx + ((long)r * W + w) * ldx + c0;
     if (accumulate) {
       float old[V];
@@ -666,6 +694,58 @@ __global__ void upsample_bwd_kernel(const T* dy, int ldy, int N, int H, int W, i
       for (int e = 0; e < V; ++e) acc[e] += old[e];
     }
     store_vec(o, acc);
+  }
+}
+
+// upsample_bwd with the backward of the ReLU that produced x fused in (x = that ReLU's output, the
+// upsample its sole consumer: the decoder's unetUp conv2 -> next block's Upsample,
+// model/unet_resnet.py:25-33): dx = (A > 0) ? adjoint(dy) : 0, rounded to T as stored; part[g][0][c]
+// = per-block column sums of the stored dx (the producer conv's bias-gradient partials, reduced by
+// unetseg_colsum_rows), g = blockIdx.y * gridDim.x + blockIdx.x.  No accumulate.
+template <typename T>
+__global__ __launch_bounds__(256) void upsample_bwd_relu_kernel(const T* dy, int ldy, int N, int H, int W, int C,
+                                                                 int align, const T* A, int lda, T* dx, int ldx,
+                                                                 float* part) {
+  constexpr int V = VE<T>;
+  __shared__ float red[256 * V];
+  const int cv = C / V, OH = 2 * H, OW = 2 * W;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = idx < W * cv;
+  const int w = live ? idx / cv : 0, c0 = live ? (idx - w * cv) * V : 0;
+  float s[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) s[e] = 0.f;
+  if (live) {
+    int cd0;
+    float cw[kUpK];
+    up_taps(w, W, OW, align, cd0, cw);
+    const int r0 = blockIdx.y * kUpRowsPB, r1 = min(r0 + kUpRowsPB, N * H);
+    for (int r = r0; r < r1; ++r) {
+      const int n = r / H, h = r - n * H;
+      float am[V];
+      load_vec(A + ((long)r * W + w) * lda + c0, am);  // mask first: its latency hides under the gather
+      float acc[V];
+      up_adjoint<T>(dy, ldy, n, h, H, OH, OW, align, cd0, cw, c0, acc);
+      T o[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        o[e] = (T)(am[e] > 0.f ? acc[e] : 0.f);  // == upsample_bwd's stored value, then relu_bwd's mask
+        s[e] += (float)o[e];
+      }
+      *reinterpret_cast<uint4*>(dx + ((long)r * W + w) * ldx + c0) = *reinterpret_cast<uint4*>(o);
+    }
+  }
+  // block partials: the threads of one 8-channel group are tid % cv (256 % cv == 0, blocks start
+  // at a pixel boundary)
+#pragma unroll
+  for (int e = 0; e < V; ++e) red[threadIdx.x * V + e] = s[e];
+  __syncthreads();
+  const long g = (long)blockIdx.y * gridDim.x + blockIdx.x;
+  for (int i = threadIdx.x; i < cv * V; i += 256) {
+    const int cx = i / V, e = i - cx * V;
+    float t = 0.f;
+    for (int j = cx; j < 256; j += cv) t += red[j * V + e];
+    part[g * 2 * C + cx * V + e] = t;
   }
 }
 
@@ -1359,6 +1439,28 @@ UNETSEG_API int unetseg_upsample2x_bwd(int dtype, const void* dy, int ldy, int n
                                        (hipStream_t)stream, (const T*)dy, ldy, n, h, w, c, align_corners, (T*)dx, ldx,
                                        accumulate));
   US_LAUNCH_CHECK("upsample_bwd");
+  return 0;
+}
+
+// partial rows (blocks) of unetseg_upsample2x_bwd_relu for this shape
+UNETSEG_API int unetseg_upsample2x_bwd_tiles(int dtype, int n, int h, int w, int c) {
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  return ceil_div((long)w * (c / V), 256) * ceil_div((long)n * h, kUpRowsPB);
+}
+
+UNETSEG_API int unetseg_upsample2x_bwd_relu(int dtype, const void* dy, int ldy, int n, int h, int w, int c,
+                                            int align_corners, const void* a, int lda, void* dx, int ldx, float* part,
+                                            int rows, void* stream) {
+  CHECK_VEC(dtype, c, "upsample_bwd_relu");
+  US_CHECK_ARG(dy && a && dx && part, "upsample_bwd_relu: null pointer");
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  US_CHECK_ARG(c / V <= 256 && 256 % (c / V) == 0, "upsample_bwd_relu: channels / vector must divide 256");
+  US_CHECK_ARG(rows == unetseg_upsample2x_bwd_tiles(dtype, n, h, w, c), "upsample_bwd_relu: rows mismatch");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(upsample_bwd_relu_kernel<T>,
+                                       dim3(ceil_div(w * (c / VE<T>), 256), ceil_div(n * h, kUpRowsPB)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)dy, ldy, n, h, w, c, align_corners, (const T*)a,
+                                       lda, (T*)dx, ldx, part));
+  US_LAUNCH_CHECK("upsample_bwd_relu");
   return 0;
 }
 

@@ -39,6 +39,8 @@ SIGNATURES = {
     "unetseg_conv2d_fwd_bnrelu_in": (I, [I, P, I, I, I, I, I, P, I, P, P, P, I, P, I, P, P]),
     "unetseg_conv2d_fwd_bnrelu_in_config": (I, [I, I, I, I, I, I, I]),
     "unetseg_conv2d_fwd_head_ok": (I, [I, I, I, I, I, I, I]),
+    "unetseg_upsample2x_bwd_tiles": (I, [I, I, I, I, I]),
+    "unetseg_upsample2x_bwd_relu": (I, [I, P, I, I, I, I, I, I, P, I, P, I, P, I, P]),
     "unetseg_conv2d_fwd_head": (I, [I, P, I, I, I, I, P, P, P, I, I, P, P, P, P]),
     "unetseg_conv2d_wgrad_bnrelu_in": (I, [I, P, I, I, I, I, I, P, I, I, P, P, P, SZ, P, I, I, P]),
     "unetseg_conv2d_fwd_affine": (I, [I, P, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P, P, I, P, I, P]),
@@ -122,7 +124,7 @@ VALUE_FUNCS = {"reduce_tiles", "pw_small_tiles", "conv_tile_m", "abi_version", "
                "conv2d_dgrad_post", "stem_fwd_tile_m", "attn_bwd1_tiles", "pw_small_tile", "conv2d_fwd_config",
                "conv2d_dgrad_config", "conv2d_wgrad_config", "stem_config", "pw_head_tiles", "channel_stats_tiles",
                "augment_tables_len", "pack_tiles",
-               "conv2d_fwd_bnrelu_in_config", "conv2d_fwd_head_ok"}
+               "conv2d_fwd_bnrelu_in_config", "conv2d_fwd_head_ok", "upsample2x_bwd_tiles"}
 
 _lib = None
 

@@ -63,6 +63,8 @@ def use(*nodes):
 FUSE = os.environ.get("UNETSEG_NO_FUSE", "0") != "1"
 #: the model's 1x1 head computed in the epilogue of the conv before it (UNETSEG_NO_HEAD_FUSE=1 disables)
 FUSE_HEAD = os.environ.get("UNETSEG_NO_HEAD_FUSE", "0") != "1"
+#: the ReLU backward of an upsample's input inside the upsample backward (UNETSEG_NO_UP_FUSE=1 disables)
+FUSE_UP = os.environ.get("UNETSEG_NO_UP_FUSE", "0") != "1"
 
 
 _WORKSPACES = {}
@@ -698,6 +700,18 @@ def upsample2x(ctx, x, align_corners):
 
     def bwd():
         if out.grad is None or not x.need_grad:
+            return
+        if (FUSE and FUSE_UP and ctx.dt == DT_BF16 and x.fuse is not None and x.fuse[0] == 1 and x.fuse[1] is X
+                and x.grad is None and x.uses == 1):
+            # x is a ReLU output consumed only here (unetUp conv2 -> next block's upsample): its
+            # backward mask and the producer conv's bias-gradient partials ride along
+            rows = lib.upsample2x_bwd_tiles(ctx.dt, N, H, W, C)
+            g = ctx.empty(N, H, W, C)
+            part = ctx.f32(rows, 2, C)
+            lib.upsample2x_bwd_relu(ctx.dt, P(out.grad), ldp(out.grad), N, H, W, C, int(align_corners), P(X),
+                                    ldp(X), P(g), ldp(g), P(part), rows, ctx.stream)
+            x.grad = g
+            x.fused = (part, rows)
             return
         g, acc = gbuf(ctx, x)
         lib.upsample2x_bwd(ctx.dt, P(out.grad), ldp(out.grad), N, H, W, C, int(align_corners), P(g), ldp(g), acc,
