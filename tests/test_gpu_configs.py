@@ -87,10 +87,15 @@ CASES = {
     "post2_ring128x128_5st_t9": ("post2", (8, 64, 64, 128, 0, 128, 3, 1), ["dgrad_post2:ring128x128_5st_t9"]),
     "post2_ring128x128_5st_t1": ("post2", (16, 32, 32, 256, 0, 1024, 1, 1), ["dgrad_post2:ring128x128_5st_t1"]),
     # stride-2 3x3: the four parity classes have 4 / 2 / 2 / 1 taps -> generic ring, ring_t1, ...
-    "post2_ring256x128_s2": ("post2", (16, 128, 128, 128, 0, 128, 3, 2), None),
+    "post2_ring256x128_s2": ("post2", (16, 128, 128, 128, 0, 128, 3, 2), ["dgrad_post2:multi128x128"] * 4),
     "post2_ring256x128_t9": ("post2", (16, 64, 64, 128, 0, 128, 3, 1), ["dgrad_post2:ring256x128_t9"]),
     "post2_ring256x128_t1": ("post2", (16, 64, 64, 128, 0, 512, 1, 1), ["dgrad_post2:ring256x128_t1"]),
-    "post2_ring64x128_s2": ("post2", (1, 32, 32, 512, 0, 512, 3, 2), None),
+    "post2_ring64x128_s2": ("post2", (1, 32, 32, 512, 0, 512, 3, 2), ["dgrad_post2:multi64x128"] * 4),
+    # stride-2 3x3 data gradients: the four parity classes in one launch (launch_tn_multi)
+    "dgrad_multi128x128_s2": ("dgrad", (16, 64, 64, 256, 0, 256, 3, 2), ["dgrad:multi128x128"] * 4),
+    "dgrad_multi64x128_s2": ("dgrad", (16, 32, 32, 512, 0, 512, 3, 2), ["dgrad:multi64x128"] * 4),
+    "dgrad_multi_ragged_s2": ("dgrad", (2, 17, 23, 128, 0, 192, 3, 2), None),
+    "post2_multi_ragged_s2": ("post2", (2, 17, 23, 128, 0, 192, 3, 2), None),
     "post2_ring64x128_t9": ("post2", (1, 32, 32, 256, 0, 256, 3, 1), ["dgrad_post2:ring64x128_t9"]),
     "post2_ring64x128_t1": ("post2", (1, 16, 16, 512, 0, 2048, 1, 1), ["dgrad_post2:ring64x128_t1"]),
     # ---- weight gradient (+ split-K reduce) ----

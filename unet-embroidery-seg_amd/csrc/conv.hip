@@ -993,6 +993,25 @@ UNETSEG_API int unetseg_conv2d_fwd_affine(int dtype, const void* x1, int c1, int
 
 // Data gradient.  dy: NHWC [n,p,q,cout] (pixel stride ldy); wt: dtype [cin][r][s][cout];
 // dx: NHWC [n,h,w,*] pixel stride ldx, written (or added to when accumulate).
+static int dgrad_classes(const void* dy, int ldy, int n, int p, int q, const void* wt, int cout, int cin, int r, int s,
+                         int stride, int pad, void* dx, int ldx, int h, int w, int ph, int pw, IgemmArgs& a);
+
+// Which parity classes of a stride-2 data gradient run as one merged launch (launch_tn_multi): the
+// classes with taps (a class no tap reaches only writes zeros and keeps its own launch), when at
+// least two of them share a fast tile.  in[i] marks them; returns the shared row tile or -1.
+static int merge_plan(const FastTNArgs* fs, int n, bool* in) {
+  FastTNArgs m[4];
+  int k = 0;
+  for (int i = 0; i < n; ++i) {
+    in[i] = fs[i].nr > 0;
+    if (in[i]) m[k++] = fs[i];
+  }
+  const int bm = tn_multi_tile_m(m, k);
+  if (bm < 0)
+    for (int i = 0; i < n; ++i) in[i] = false;
+  return bm;
+}
+
 UNETSEG_API int unetseg_conv2d_dgrad(int dtype, const void* dy, int ldy, int n, int p, int q, const void* wt,
                                      int cout, int cin, int r, int s, int stride, int pad, void* dx, int ldx,
                                      int h, int w, int accumulate, void* stream) {
@@ -1001,6 +1020,32 @@ UNETSEG_API int unetseg_conv2d_dgrad(int dtype, const void* dy, int ldy, int n, 
   US_CHECK_ARG(stride == 1 || stride == 2, "conv2d_dgrad: stride must be 1 or 2");
   US_CHECK_ARG(p == (h + 2 * pad - r) / stride + 1 && q == (w + 2 * pad - s) / stride + 1, "conv2d_dgrad: shape mismatch");
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == DT_BF16 && stride == 2) {
+    // the parity classes with taps as one launch when they share a fast tile (merge_plan)
+    FastTNArgs fs[4];
+    int ncls = 0;
+    bool fast = true;
+    for (int ph = 0; ph < 2 && fast; ++ph)
+      for (int pw = 0; pw < 2 && fast; ++pw) {
+        IgemmArgs a;
+        if (!dgrad_classes(dy, ldy, n, p, q, wt, cout, cin, r, s, stride, pad, dx, ldx, h, w, ph, pw, a)) continue;
+        if (a.M <= 0 || (a.nr == 0 && accumulate)) continue;
+        a.accumulate = accumulate;
+        fast = fast_tn_args(a, fs[ncls++]);
+      }
+    bool in[4];
+    if (fast && merge_plan(fs, ncls, in) > 0) {
+      FastTNArgs m[4];
+      int k = 0;
+      for (int i = 0; i < ncls; ++i) {
+        if (in[i]) m[k++] = fs[i];
+        else launch_tn_fast(fs[i], st);
+      }
+      US_CHECK_ARG(launch_tn_multi(m, k, st) == 0, "conv2d_dgrad: merged launch refused");
+      US_LAUNCH_CHECK("conv2d_dgrad (merged parity classes)");
+      return 0;
+    }
+  }
   for (int ph = 0; ph < stride; ++ph)
     for (int pw = 0; pw < stride; ++pw) {
       IgemmArgs a{};
@@ -1076,17 +1121,29 @@ UNETSEG_API int unetseg_conv2d_dgrad_post(int dtype, const void* dy, int ldy, in
       fs[ncls++] = f;
       total += tn_fast_post_rows(f);
     }
+  // parity classes merged into one launch share its row tile (their partial rows follow it)
+  bool in[4];
+  const int mbm = merge_plan(fs, ncls, in);
+  if (mbm > 0) {
+    total = 0;
+    for (int i = 0; i < ncls; ++i) total += in[i] ? ceil_div(fs[i].M, mbm) : tn_fast_post_rows(fs[i]);
+  }
   if (!part) return total;
   US_CHECK_ARG(dy && wt && dx && aux, "conv2d_dgrad_post: null pointer");
   US_CHECK_ARG(rows == total, "conv2d_dgrad_post: rows %d != %d", rows, total);
   US_CHECK_ARG(post == 1 || (psc && psh && pmean && pinv), "conv2d_dgrad_post: BN post needs its coefficients");
   hipStream_t st = (hipStream_t)stream;
   int off = 0;
+  FastTNArgs m[4];
+  int k = 0;
   for (int i = 0; i < ncls; ++i) {
     fs[i].ppart = part + (long)off * 2 * cin;
-    off += tn_fast_post_rows(fs[i]);
-    launch_tn_fast(fs[i], st);
+    const bool merged = mbm > 0 && in[i];
+    off += merged ? ceil_div(fs[i].M, mbm) : tn_fast_post_rows(fs[i]);
+    if (merged) m[k++] = fs[i];
+    else launch_tn_fast(fs[i], st);
   }
+  if (k > 0) US_CHECK_ARG(launch_tn_multi(m, k, st) == 0, "conv2d_dgrad_post: merged launch refused");
   US_LAUNCH_CHECK("conv2d_dgrad_post");
   return 0;
 }
@@ -1098,6 +1155,9 @@ UNETSEG_API int unetseg_conv2d_dgrad_config(int dtype, int ldy, int n, int p, in
                                             int stride, int pad, int ldx, int h, int w, int* cfg_out, int* taps_out) {
   US_CHECK_ARG(cfg_out && (stride == 1 || stride == 2), "conv2d_dgrad_config: bad args");
   int launched = 0;
+  FastTNArgs fs[4];
+  int idx[4], ncls = 0;
+  bool fast = dtype == DT_BF16 && stride == 2;
   for (int ph = 0; ph < stride; ++ph)
     for (int pw = 0; pw < stride; ++pw) {
       const int k = ph * stride + pw;
@@ -1109,7 +1169,19 @@ UNETSEG_API int unetseg_conv2d_dgrad_config(int dtype, int ldy, int n, int p, in
       if (a.M <= 0) continue;
       cfg_out[k] = tn_query(dtype, a, taps_out ? taps_out + k : nullptr);
       ++launched;
+      if (fast) {
+        idx[ncls] = k;
+        fast = fast_tn_args(a, fs[ncls++]);
+      }
     }
+  bool in[4];
+  const int bm = fast ? merge_plan(fs, ncls, in) : -1;
+  if (bm > 0)
+    for (int i = 0; i < ncls; ++i)
+      if (in[i]) {
+        cfg_out[idx[i]] = bm == 64 ? kCfgMulti64 : kCfgMulti128;
+        if (taps_out) taps_out[idx[i]] = 0;
+      }
   return launched;
 }
 

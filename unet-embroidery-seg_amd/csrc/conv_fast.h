@@ -85,13 +85,19 @@ struct HaloWgradArgs {
 };
 
 // kernel-configuration codes reported by the unetseg_conv2d_*_config queries (include/unetseg_hip.h)
-enum { kCfgHalo = 0, kCfgGeneric = 100 };  // 1..14: TN tile configurations of tn_config (conv_fast.hip)
+// 1..14: TN tile configurations of tn_config (conv_fast.hip); 17 / 18: stride-2 dgrad parity classes
+// merged into one launch on 128x128 / 64x128 register-staged tiles (launch_tn_multi)
+enum { kCfgHalo = 0, kCfgMulti128 = 17, kCfgMulti64 = 18, kCfgGeneric = 100 };
 enum { kWgHalo = 0, kWgFastRow64x256 = 1, kWgFastRow128 = 2, kWgFast64x256 = 3, kWgFast128 = 4, kWgGeneric = 5,
        kWgRing64x256 = 6, kWgRing128 = 7 };
 
 bool tn_fast_ok(const FastTNArgs& a);
 int tn_fast_config(const FastTNArgs& a, int* taps_out);  // kCfgHalo or a TN configuration 1..14
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st);
+// 2-4 independent GEMMs (stride-2 dgrad parity classes) in one launch: the shared row tile (64 /
+// 128), or -1 if they cannot be merged; launch_tn_multi returns -1 without launching in that case
+int tn_multi_tile_m(const FastTNArgs* fs, int n);
+int launch_tn_multi(const FastTNArgs* fs, int n, hipStream_t st);
 int tn_fast_tile_m(const FastTNArgs& a);
 int tn_fast_post_rows(const FastTNArgs& a);  // partial rows (ppart) a launch_tn_fast call writes
 int halo3_blocks(const FastTNArgs& a);

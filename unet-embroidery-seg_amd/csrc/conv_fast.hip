@@ -48,8 +48,9 @@ constexpr size_t kPreOff() {
 // on the 256x128 tile, which is what held its MFMA pipe at ~45 % busy).
 // PRE: the input prologue of FastTNArgs (x1 = BN input z, staged as relu(z*in_sc + in_sh) between the
 // global load and the LDS store); the per-channel coefficients sit in LDS after the tile stages.
-template <int BM, int BN, int NWM, int NWN, int ST, bool POST, int TAPS = 0, bool PRE = false>
-__global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN>())) void tn_fast_kernel(FastTNArgs a) {
+// The tile body: did = this block's linear id among gx * gy tiles (gy column tiles per row tile).
+template <int BM, int BN, int NWM, int NWN, int ST, bool POST, int TAPS, bool PRE>
+__device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did, const int gx, const int gy) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int WTM = BM / NWM, WTN = BN / NWN;
   constexpr int FP = WTM / 16, FC = WTN / 16;
@@ -67,11 +68,10 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
   // d % 8), each with its own L2.  Give every XCD a contiguous range of tiles, N tiles fastest, so
   // the N tiles of one row tile and the neighbouring row tiles (the 3x3 taps re-read them) share
   // one L2.  Bijective for any tile count.
-  const int ntiles = gridDim.x * gridDim.y;
-  const int did = blockIdx.x + gridDim.x * blockIdx.y;
+  const int ntiles = gx * gy;
   const int xq = ntiles >> 3, xr = ntiles & 7, xcd = did & 7;
   const int lin = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (did >> 3);
-  const int tile_m = lin / gridDim.y, tile_n = lin - tile_m * gridDim.y;
+  const int tile_m = lin / gy, tile_n = lin - tile_m * gy;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int kv = tid & 7, rb = tid >> 3;
   const int hw = a.hc * a.wc;
@@ -610,6 +610,30 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
   }
 }
 
+template <int BM, int BN, int NWM, int NWN, int ST, bool POST, int TAPS = 0, bool PRE = false>
+__global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN>())) void tn_fast_kernel(FastTNArgs a) {
+  tn_fast_body<BM, BN, NWM, NWN, ST, POST, TAPS, PRE>(a, blockIdx.x + gridDim.x * blockIdx.y, gridDim.x, gridDim.y);
+}
+
+// Several independent GEMMs of one configuration in one launch: the output-parity classes of a
+// stride-2 data gradient (conv.hip dgrad_classes; 4 / 2 / 2 / 1 taps, a few hundred tiles each),
+// which launched one after another left the chip mostly idle.  Blocks [start[k], start[k+1]) run
+// GEMM k as its own gx[k] x gy[k] grid.
+struct TNMulti {
+  FastTNArgs c[4];
+  int start[5];
+  int gx[4], gy[4];
+  int n;
+};
+
+template <int BM, int BN, int NWM, int NWN, int ST, bool POST>
+__global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN>())) void tn_multi_kernel(TNMulti m) {
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < m.n && b >= m.start[k + 1]) ++k;
+  tn_fast_body<BM, BN, NWM, NWN, ST, POST, 0, false>(m.c[k], b - m.start[k], m.gx[k], m.gy[k]);
+}
+
 // ------------------------------------------------------------------------------------------
 // wgrad: C[cout][(tap, c)] = sum_pix dY[pix][cout] * X[n][p*st+dh][q*st+dw][c];
 // tile BM couts x BN (tap,c) columns, K step = kWgBK consecutive output pixels.  Each thread
@@ -917,6 +941,32 @@ int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   return 0;
 }
 
+template <int BM, int BN, int NWM, int NWN, int ST, bool POST>
+int launch_tn_multi_cfg(const FastTNArgs* fs, int n, hipStream_t st) {
+  constexpr int NT = 64 * NWM * NWN;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_multi_kernel<BM, BN, NWM, NWN, ST, POST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPreOff<BM, BN, NWM, NWN, ST>());
+    attr = true;
+  }
+  TNMulti m{};
+  m.n = n;
+  int total = 0;
+  for (int k = 0; k < n; ++k) {
+    m.c[k] = fs[k];
+    m.c[k].t2d = 0;
+    m.gx[k] = ceil_div(fs[k].M, BM);
+    m.gy[k] = ceil_div(fs[k].Ng, BN);
+    m.start[k] = total;
+    total += m.gx[k] * m.gy[k];
+  }
+  m.start[n] = total;
+  constexpr size_t lds = kPreOff<BM, BN, NWM, NWN, ST>();
+  hipLaunchKernelGGL((tn_multi_kernel<BM, BN, NWM, NWN, ST, POST>), dim3(total), dim3(NT), lds, st, m);
+  return 0;
+}
+
 // Compile-time tap count for the LDS-DMA ring (0 = generic ring): 3x3 and 1x1 filters, when the
 // precomputed gather offsets (pixel index < 2^24, pbad * ldcb) fit the 24-bit multiply and 32 bits.
 static int tn_taps(const FastTNArgs& a) {
@@ -1036,6 +1086,36 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 14: return launch_tn_dma<256, 64, 4, 2, 13>(a, st);
     default: return a.post ? launch_tn_cfg<128, 128, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 3>(a, st);
   }
+}
+
+// Merged launch of 2-4 GEMMs (stride-2 data-gradient parity classes) on one register-staged tile:
+// 128x128 (or 64x128 when any class would take a 64-row tile).  Returns -1 (nothing launched) when
+// the classes cannot share one (input prologue, a halo class, more than 4).
+static bool tn_multi_off() {
+  static const bool off = getenv("UNETSEG_NO_TN_MULTI") != nullptr;
+  return off;
+}
+
+int tn_multi_tile_m(const FastTNArgs* fs, int n) {
+  if (tn_multi_off() || n < 2 || n > 4) return -1;
+  bool bm64 = false;
+  for (int k = 0; k < n; ++k) {
+    if (fs[k].in_sc || fs[k].M <= 0) return -1;
+    const int cfg = tn_config(fs[k]);
+    if (cfg == 0) return -1;
+    if (tn_cfg_bm(cfg) == 64) bm64 = true;
+  }
+  return bm64 ? 64 : 128;
+}
+
+int launch_tn_multi(const FastTNArgs* fs, int n, hipStream_t st) {
+  const int bm = tn_multi_tile_m(fs, n);
+  if (bm < 0) return -1;
+  const bool post = fs[0].post != 0;
+  if (bm == 64) return post ? launch_tn_multi_cfg<64, 128, 1, 4, 3, true>(fs, n, st)
+                            : launch_tn_multi_cfg<64, 128, 1, 4, 3, false>(fs, n, st);
+  return post ? launch_tn_multi_cfg<128, 128, 2, 2, 3, true>(fs, n, st)
+              : launch_tn_multi_cfg<128, 128, 2, 2, 3, false>(fs, n, st);
 }
 
 bool wgrad_fast_ok(const FastWgradArgs& a) {
