@@ -70,7 +70,6 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   uint4* hl = lds + WCH;                     // [2][HP][8]
   float* red = reinterpret_cast<float*>(hl + 2 * HCH);  // [NW][64]
   float* sbias = red + NW * 64;              // [64]
-  float* hwl = sbias + 64;                   // head: [HK][64] weights, then [HK] biases
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -86,7 +85,6 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   const unsigned hw_img = (unsigned)(a.OH * a.OW);
   const __amdgpu_buffer_rsrc_t rh = srd(HK ? (const void*)a.head_y : a.y,
                                         HK ? (unsigned)(a.M / (a.OH * a.OW)) * HK * hw_img * 4u : 0u);
-  if (HK && tid < HK * 65) hwl[tid] = tid < HK * 64 ? a.head_w[tid] : a.head_b[tid - HK * 64];
 
   if (kDyn && a.bias && tid < 64) sbias[tid] = a.bias[n0 + tid];
   // BN post-op coefficients of this block's 64 channels live in `red` (free in dgrad: no stats)
@@ -159,6 +157,16 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   // halo tap offsets (uniform): jt -> (dh, dw)
   const int dh0 = a.dh0, dhs = a.dhs, dw0 = a.dw0, dws = a.dws;
   const int j16 = lane & 15, kg = lane >> 4;
+  // fused head: this lane's 16 channels' head weights in registers (one block per CU: VGPRs are free)
+  float hwr[HK > 0 ? HK : 1][FC][4], hbr[HK > 0 ? HK : 1];
+#pragma unroll
+  for (int k = 0; k < HK; ++k) {
+    hbr[k] = a.head_b[k];
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) hwr[k][c][e] = a.head_w[k * 64 + c * 16 + kg * 4 + e];
+  }
   float breg[FC][4];  // this lane's 16 output channels' bias (compile-time flags only)
 #pragma unroll
   for (int c = 0; c < FC; ++c)
@@ -297,10 +305,10 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
 #pragma unroll
           for (int c = 0; c < FC; ++c)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) hs = fmaf(acc[c][p][e], hwl[k * 64 + c * 16 + kg * 4 + e], hs);
+            for (int e = 0; e < 4; ++e) hs = fmaf(acc[c][p][e], hwr[k][c][e], hs);
           hs += __shfl_xor(hs, 16);
           hs += __shfl_xor(hs, 32);
-          hs += hwl[HK * 64 + k];
+          hs += hbr[k];
           bstore32(rh, kg == 0 ? ((unsigned)(nb * HK + k) * hw_img + pix) * 4u : kOOB, hs);
         }
       }
@@ -542,8 +550,8 @@ __global__ __launch_bounds__(256) void halo3_wgrad_kernel(HaloWgradArgs a, int t
 
 template <int TH, int NW>
 size_t halo_lds_bytes(int head_k = 0) {
-  return (size_t)9 * 64 * 128 + 2 * (size_t)(TH + 2) * (HW_TW + 2) * 128 + NW * 64 * 4 + 64 * 4 +
-         (size_t)head_k * 65 * 4;
+  (void)head_k;
+  return (size_t)9 * 64 * 128 + 2 * (size_t)(TH + 2) * (HW_TW + 2) * 128 + NW * 64 * 4 + 64 * 4;
 }
 
 }  // namespace
