@@ -96,7 +96,8 @@ int unetseg_conv2d_fwd_affine(int dtype, const void* x1, int c1, int ldc1, const
  * (conv_fast.hip tn_config: 1 256x64, 2 256x128, 3 128x128, 4 128x128 one K step, 5 64x128,
  * 6 128x64, 7 256x128 LDS-DMA ring, 8 128x128 ring, 9 64x128 ring, 10 128x128 5-stage ring,
  * 11-14 other rings), 17 / 18 = the parity classes of a stride-2 data gradient merged into one launch
- * on 128x128 / 64x128 tiles, 100 = generic igemm kernel (fp32 / unaligned channels).  *taps_out = the
+ * on 128x128 / 64x128 tiles, 19 / 20 = short-K (2-4 steps) 128x128 / 128x64 tiles on one LDS stage,
+ * 100 = generic igemm kernel (fp32 / unaligned channels).  *taps_out = the
  * compile-time tap count of an LDS-DMA ring (9 or 1; 0 = generic ring or not a ring). */
 int unetseg_conv2d_fwd_config(int dtype, int c1, int ldc1, int c2, int ldc2, int n, int h, int w, int cout, int r,
                               int s, int stride, int pad, int* taps_out);

@@ -55,9 +55,12 @@ CASES = {
     "fwd_ring128x64_t9": ("fwd_relu", (1, 256, 256, 64, 128, 64, 3, 1), ["fwd:ring128x64_t9"]),  # up_concat1.conv1
     "fwd_ring64x128_t9": ("fwd_stats", (1, 64, 64, 256, 0, 256, 3, 2), ["fwd:ring64x128_t9"]),
     "fwd_ring64x128_t1": ("fwd_stats", (1, 16, 16, 2048, 0, 512, 1, 1), ["fwd:ring64x128_t1"]),
-    "fwd_tn128x128": ("fwd_all", (1, 64, 64, 128, 0, 512, 1, 1), ["fwd:tn128x128"]),
+    "fwd_tn128x128_1st": ("fwd_all", (1, 64, 64, 128, 0, 512, 1, 1), ["fwd:tn128x128_1st"]),
     "fwd_tn128x128_1step": ("fwd_stats", (1, 128, 128, 64, 0, 256, 1, 1), ["fwd:tn128x128_1step"]),
-    "fwd_tn128x64": ("fwd_stats", (1, 128, 128, 64, 0, 64, 1, 1), ["fwd:tn128x64"]),
+    "fwd_tn128x64": ("fwd_stats", (1, 32, 32, 512, 0, 64, 1, 1), ["fwd:tn128x64"]),
+    "fwd_tn128x64_1st": ("fwd_all", (16, 128, 128, 256, 0, 64, 1, 1), ["fwd:tn128x64_1st"]),        # layer1 conv1
+    "fwd_tn128x64_1st_ragged": ("fwd_stats", (3, 15, 17, 192, 0, 40, 1, 1), ["fwd:tn128x64_1st"]),
+    "fwd_tn128x64_1st_k64": ("fwd_stats", (1, 128, 128, 64, 0, 64, 1, 1), ["fwd:tn128x64_1st"]),
     "fwd_tn64x128": ("fwd_all", (1, 64, 64, 512, 0, 128, 1, 1), ["fwd:tn64x128"]),
     # generic kernel: the first conv of unet_plain / attention_unet (3 input channels padded to 8)
     "fwd_generic_cin8": ("fwd_stats", (2, 64, 64, 8, 0, 64, 3, 1), ["fwd:generic"]),
@@ -71,19 +74,25 @@ CASES = {
     "dgrad_ring128x64_t9": ("dgrad", (1, 256, 256, 64, 0, 128, 3, 1), ["dgrad:ring128x64_t9"]),  # attention down1
     "dgrad_ring64x128_t9": ("dgrad", (1, 32, 32, 256, 0, 256, 3, 1), ["dgrad:ring64x128_t9"]),
     "dgrad_ring64x128_t1": ("dgrad", (1, 16, 16, 512, 0, 2048, 1, 1), ["dgrad:ring64x128_t1"]),
-    "dgrad_tn128x128": ("dgrad", (1, 64, 64, 512, 0, 128, 1, 1), ["dgrad:tn128x128"]),
+    "dgrad_tn128x128_1st": ("dgrad", (1, 64, 64, 512, 0, 128, 1, 1), ["dgrad:tn128x128_1st"]),
+    "dgrad_tn128x128_1st_bench": ("dgrad", (16, 128, 128, 256, 0, 128, 1, 1), ["dgrad:tn128x128_1st"]),  # layer2 conv1
     "dgrad_tn128x128_s2": ("dgrad", (2, 64, 64, 256, 0, 512, 1, 2),
                            ["dgrad:tn64x128", "dgrad:tn128x128", "dgrad:tn128x128", "dgrad:tn128x128"]),
     "dgrad_tn128x128_1step": ("dgrad", (1, 128, 128, 256, 0, 64, 1, 1), ["dgrad:tn128x128_1step"]),
-    "dgrad_tn128x64": ("dgrad", (1, 128, 128, 64, 0, 64, 1, 1), ["dgrad:tn128x64"]),
+    "dgrad_tn128x64": ("dgrad", (1, 32, 32, 64, 0, 512, 1, 1), ["dgrad:tn128x64"]),
+    "dgrad_tn128x64_1st_k64": ("dgrad", (1, 128, 128, 64, 0, 64, 1, 1), ["dgrad:tn128x64_1st"]),
+    "dgrad_tn128x64_1st": ("dgrad", (16, 128, 128, 64, 0, 256, 1, 1), ["dgrad:tn128x64_1st"]),
+    "dgrad_tn128x128_1st_ragged": ("dgrad", (3, 15, 17, 136, 0, 192, 1, 1), ["dgrad:tn128x128_1st"]),
     # ---- data gradient with the producer's ReLU (post 1) / BN-ReLU (post 2) backward fused ----
     "post1_halo3": ("post1", (2, 64, 256, 64, 0, 64, 3, 1), ["dgrad_post1:halo3"]),
     "post1_ring256x128_t9": ("post1", (16, 32, 32, 512, 0, 512, 3, 1), ["dgrad_post1:ring256x128_t9"]),
     "post1_ring128x128_5st_t9": ("post1", (8, 64, 64, 128, 0, 128, 3, 1), ["dgrad_post1:ring128x128_5st_t9"]),
     "post2_halo3": ("post2", (1, 128, 128, 64, 0, 64, 3, 1), ["dgrad_post2:halo3"]),
-    "post2_tn128x128": ("post2", (1, 64, 64, 512, 0, 128, 1, 1), ["dgrad_post2:tn128x128"]),
+    "post2_tn128x128_1st": ("post2", (1, 64, 64, 512, 0, 128, 1, 1), ["dgrad_post2:tn128x128_1st"]),
     "post2_tn64x128": ("post2", (1, 64, 64, 128, 0, 512, 1, 1), ["dgrad_post2:tn64x128"]),
-    "post2_tn128x64": ("post2", (1, 128, 128, 64, 0, 64, 1, 1), ["dgrad_post2:tn128x64"]),
+    "post2_tn128x64": ("post2", (1, 32, 32, 64, 0, 512, 1, 1), ["dgrad_post2:tn128x64"]),
+    "post2_tn128x64_1st_k64": ("post2", (1, 128, 128, 64, 0, 64, 1, 1), ["dgrad_post2:tn128x64_1st"]),
+    "post2_tn128x64_1st": ("post2", (16, 128, 128, 64, 0, 256, 1, 1), ["dgrad_post2:tn128x64_1st"]),  # layer1 conv3
     "post2_ring128x128_5st_t9": ("post2", (8, 64, 64, 128, 0, 128, 3, 1), ["dgrad_post2:ring128x128_5st_t9"]),
     "post2_ring128x128_5st_t1": ("post2", (16, 32, 32, 256, 0, 1024, 1, 1), ["dgrad_post2:ring128x128_5st_t1"]),
     # stride-2 3x3: the four parity classes have 4 / 2 / 2 / 1 taps -> generic ring, ring_t1, ...
@@ -116,8 +125,8 @@ CASES = {
     "wgrad_ring64x256": ("wgrad", (16, 128, 128, 256, 0, 64, 1, 1), ["wgrad:wgrad_ring64x256", "reduce"]),
     # bottleneck conv3 reading bn2-ReLU on load (ops.bn(lazy=True), unetseg_conv2d_*_bnrelu_in)
     "bnin_tn128x128_1step": ("fwd_bnrelu_in", (16, 128, 128, 64, 0, 256, 1, 1), ["fwd_bnrelu_in:tn128x128_1step"]),
-    "bnin_tn128x128": ("fwd_bnrelu_in", (16, 64, 64, 128, 0, 512, 1, 1), ["fwd_bnrelu_in:tn128x128"]),
-    "bnin_tn128x128_k256": ("fwd_bnrelu_in", (16, 32, 32, 256, 0, 1024, 1, 1), ["fwd_bnrelu_in:tn128x128"]),
+    "bnin_tn128x128_1st": ("fwd_bnrelu_in", (16, 64, 64, 128, 0, 512, 1, 1), ["fwd_bnrelu_in:tn128x128_1st"]),
+    "bnin_tn128x128_1st_k256": ("fwd_bnrelu_in", (16, 32, 32, 256, 0, 1024, 1, 1), ["fwd_bnrelu_in:tn128x128_1st"]),
     "bnin_tn256x128": ("fwd_bnrelu_in", (16, 16, 16, 512, 0, 2048, 1, 1), ["fwd_bnrelu_in:tn256x128"]),
     "bnin_tn64x128": ("fwd_bnrelu_in", (1, 16, 16, 512, 0, 2048, 1, 1), ["fwd_bnrelu_in:tn64x128"]),
     "bnin_ragged": ("fwd_bnrelu_in", (1, 15, 17, 64, 0, 256, 1, 1), None),

@@ -29,14 +29,17 @@ namespace {
 // sets; only where the registers fit at two waves per SIMD)
 // waves per SIMD each configuration is sized for (LDS allows that many blocks per CU); caps the
 // register allocation so the two-step register prefetch cannot cost occupancy
-template <int BM, int BN, int NWM, int NWN>
-constexpr int tn_waves_per_simd() { return (BM == 64 || (BM == 128 && BN == 64)) ? 3 : 2; }
+// ST == 5 (short K on one LDS stage): 128x128 at three waves per SIMD, 128x64 at four
+template <int BM, int BN, int NWM, int NWN, int ST = 3>
+constexpr int tn_waves_per_simd() {
+  return ST == 5 ? (BN == 64 ? 4 : 3) : (BM == 64 || (BM == 128 && BN == 64)) ? 3 : 2;
+}
 
 // byte offset of the input-prologue coefficients in the TN kernel's dynamic LDS: after the operand
 // stages or the epilogue's transpose tiles + stats scratch, whichever is larger
 template <int BM, int BN, int NWM, int NWN, int ST>
 constexpr size_t kPreOff() {
-  constexpr size_t stages = (size_t)(ST == 1 ? 1 : ST >= 13 ? ST - 10 : 2) * (BM + BN) * 8 * 16;
+  constexpr size_t stages = (size_t)(ST == 1 || ST == 5 ? 1 : ST >= 13 ? ST - 10 : 2) * (BM + BN) * 8 * 16;
   constexpr size_t epi = (size_t)NWM * NWN * 64 * ((BN / NWN) * 2 + 16) + 2 * NWM * BN * 4;
   return ((stages > epi ? stages : epi) + 15) / 16 * 16;
 }
@@ -368,6 +371,26 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
       compute(0);
     }
     __syncthreads();
+  } else if (ST == 5) {
+    // short K (<= 4 steps) on ONE LDS stage: the next step's loads are in registers while this step
+    // computes; two barriers per step.  The single stage (32 / 24 KiB) and the one register set let
+    // 3-4 blocks share a CU, which is what hides the HBM latency of these memory-bound layers.
+    int kc0 = 0;
+    if (nsteps > 0) {
+      gload(ra0, rb0, kc0);
+      sstore(0, ra0, rb0, kc0);
+      __syncthreads();
+    }
+    for (int kt = 0; kt < nsteps; ++kt) {
+      const bool more = kt + 1 < nsteps;
+      if (more) gload(ra0, rb0, kc0);
+      compute(0);
+      __syncthreads();
+      if (more) {
+        sstore(0, ra0, rb0, kc0);
+        __syncthreads();
+      }
+    }
   } else if (ST == 2) {  // loads one step ahead (one register set)
     int kc0 = 0;
     if (nsteps > 0) {
@@ -611,7 +634,7 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
 }
 
 template <int BM, int BN, int NWM, int NWN, int ST, bool POST, int TAPS = 0, bool PRE = false>
-__global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN>())) void tn_fast_kernel(FastTNArgs a) {
+__global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN, ST>())) void tn_fast_kernel(FastTNArgs a) {
   tn_fast_body<BM, BN, NWM, NWN, ST, POST, TAPS, PRE>(a, blockIdx.x + gridDim.x * blockIdx.y, gridDim.x, gridDim.y);
 }
 
@@ -991,7 +1014,7 @@ static int launch_tn_dma(const FastTNArgs& a, hipStream_t st) {
   }
 }
 
-// TN configuration: 0 = halo, 1 = 256x64, 2 = 256x128, 3 = 128x128, 4 = 128x128 single stage
+// TN configuration: 0 = halo, 19 / 20 = short-K 128x128 / 128x64 on one LDS stage, 1 = 256x64, 2 = 256x128, 3 = 128x128, 4 = 128x128 single stage
 // (one K step: the prefetch stage would only cost occupancy), 5 = 64x128, 6 = 128x64;
 // 7-10: the same tiles on the LDS-DMA ring.  Measured (tools/gpu_cfg_sweep.sh): the 256x128 ring
 // (3 stages) beats the register-staged 256x128 by 3-8 % on every large layer; the 64x128 ring (4
@@ -999,13 +1022,17 @@ static int launch_tn_dma(const FastTNArgs& a, hipStream_t st) {
 static int tn_config(const FastTNArgs& a) {
   if (const char* e = getenv("UNETSEG_TN_CFG")) {  // experiments: force a configuration (1..14)
     const int c = atoi(e);
-    if (c >= 1 && c <= 14 && !(a.in_sc && c >= 7)) return c;
+    if (((c >= 1 && c <= 14) || c == 19 || c == 20) && !(a.in_sc && c >= 7 && c <= 14)) return c;
   }
   static const bool no_dma_env = getenv("UNETSEG_TN_NO_DMA") != nullptr;
   // the input prologue transforms registers between load and LDS store: register-staged tiles only
   const bool no_dma = no_dma_env || a.in_sc != nullptr;
   if (!a.in_sc && halo3_ok(a)) return 0;
   const int nsteps = a.nr * a.ns * (a.cin >> 6);
+  // short K (<= 4 steps: the bottleneck 1x1 layers, HBM-bound) on one LDS stage, 3-4 blocks per CU
+  // (128x128 with one step keeps its own single-step tile: as fast, fewer barriers)
+  static const bool no_short1 = getenv("UNETSEG_TN_NO_SHORT1") != nullptr;
+  if (!no_short1 && nsteps <= 4 && (nsteps >= 2 || a.Ng <= 64)) return a.Ng <= 64 ? 20 : 19;
   if (nsteps == 1 && a.Ng > 64) return 4;
   // 128x64 (two-step prefetch, 3 blocks/CU): 5-10 % over 256x64; deep 3x3 K on the 3-stage ring
   // with compile-time taps: ~8 % more (192->64 at 256x256: 390 -> 357 us)
@@ -1065,6 +1092,8 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
       case 5: return launch_tn_cfg<64, 128, 1, 4, 3, false, 0, true>(a, st);
       case 6: return launch_tn_cfg<128, 64, 2, 2, 3, false, 0, true>(a, st);
       case 3: return launch_tn_cfg<128, 128, 2, 2, 3, false, 0, true>(a, st);
+      case 19: return launch_tn_cfg<128, 128, 2, 2, 5, false, 0, true>(a, st);
+      case 20: return launch_tn_cfg<128, 64, 2, 2, 5, false, 0, true>(a, st);
       default: return -1;
     }
   }
@@ -1084,6 +1113,8 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 12: return launch_tn_dma<128, 64, 2, 2, 14>(a, st);
     case 13: return launch_tn_dma<128, 64, 2, 2, 13>(a, st);
     case 14: return launch_tn_dma<256, 64, 4, 2, 13>(a, st);
+    case 19: return a.post ? launch_tn_cfg<128, 128, 2, 2, 5, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 5>(a, st);
+    case 20: return a.post ? launch_tn_cfg<128, 64, 2, 2, 5, true>(a, st) : launch_tn_cfg<128, 64, 2, 2, 5>(a, st);
     default: return a.post ? launch_tn_cfg<128, 128, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 3>(a, st);
   }
 }
