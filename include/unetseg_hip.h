@@ -169,11 +169,19 @@ int unetseg_bn_eval_coeffs(int C, const float* gamma, const float* beta, const f
 int unetseg_bn_apply(int dtype, const void* y, int ldy, const float* sc, const float* sh, const void* r, int ldr,
                      const float* sc2, const float* sh2, int res_mode, int relu, void* out, int ldo, long M, int C,
                      void* stream);
+/* unetseg_bn_apply with relu = 1 that also writes the ReLU mask of `out` packed one byte per (pixel,
+ * 16-B channel vector): mbits[p * C/V + c/V] bit (c % V) = (stored out[p][c] > 0), V = 8 (bf16) / 4
+ * (fp32).  The backward below reads it (A = mbits, lda = 0) instead of the activation: the residual
+ * BN-add-ReLU of the ResNet bottleneck (model/resnet_backbone.py:66-76), 1/16 of the bytes. */
+int unetseg_bn_apply_mask(int dtype, const void* y, int ldy, const float* sc, const float* sh, const void* r, int ldr,
+                          const float* sc2, const float* sh2, int res_mode, void* out, int ldo, long M, int C,
+                          unsigned char* mbits, void* stream);
 /* partial-buffer geometry of the channel reductions below: returns G (row groups) */
 int unetseg_reduce_tiles(int dtype, long M, int C, int* tv_out, int* ppb_out);
 /* backward through [relu](BN(y1) [+ BN(y2)]): per-channel partials of dz and dz*xhat.  The ReLU
- * mask comes from the activation A, or (A == NULL, msc != NULL: no residual) is recomputed from y1
- * as fmaf(y1, msc, msh) > 0 -- the forward's BN scale/shift -- saving one tensor read. */
+ * mask comes from the activation A, from the packed mask of unetseg_bn_apply_mask (A = mbits with
+ * lda == 0), or (A == NULL, msc != NULL: no residual) is recomputed from y1 as fmaf(y1, msc, msh) > 0
+ * -- the forward's BN scale/shift -- saving one tensor read.  unetseg_bn_bwd_apply likewise. */
 int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const void* A, int lda, const float* msc,
                           const float* msh, const void* y1, int ld1, const float* mean1, const float* inv1,
                           const void* y2, int ld2, const float* mean2, const float* inv2, long M, int C, float* part,

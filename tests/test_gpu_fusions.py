@@ -132,3 +132,56 @@ def test_upsample_bwd_relu(N, H, W, C, align):
     ref = pref.double().sum(1)
     assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-5
     assert torch.allclose(got, dx.double().sum((0, 1, 2)), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,C,mode", [(16 * 128 * 128, 256, 1), (16 * 32 * 32, 1024, 2), (3 * 15 * 17, 64, 1)])
+def test_bn_mask_bits(M, C, mode):
+    """unetseg_bn_apply_mask (the residual BN-add-ReLU of the bottleneck, model/resnet_backbone.py:66-76):
+    the activation is bit-identical to unetseg_bn_apply, the packed bits are (out > 0), and the BN backward
+    reading the bits (lda = 0) is bit-identical to reading the activation"""
+    from unetseg_hip.lib import DT_BF16, lib
+    g = torch.Generator(device=DEV).manual_seed(M + C)
+    bf = torch.bfloat16
+    y = torch.randn(M, C, generator=g, device=DEV).to(bf)
+    r = torch.randn(M, C, generator=g, device=DEV).to(bf)
+    sc, sh = torch.rand(C, generator=g, device=DEV) + 0.5, torch.randn(C, generator=g, device=DEV) * 0.2
+    sc2, sh2 = torch.rand(C, generator=g, device=DEV) + 0.5, torch.randn(C, generator=g, device=DEV) * 0.2
+    m2 = (sc2.data_ptr(), sh2.data_ptr()) if mode == 2 else (0, 0)
+    a_ref = torch.empty(M, C, dtype=bf, device=DEV)
+    lib.bn_apply(DT_BF16, y.data_ptr(), C, sc.data_ptr(), sh.data_ptr(), r.data_ptr(), C, *m2, mode, 1,
+                 a_ref.data_ptr(), C, M, C, _st())
+    a = torch.empty_like(a_ref)
+    bits = torch.empty(M * C // 8, dtype=torch.uint8, device=DEV)
+    lib.bn_apply_mask(DT_BF16, y.data_ptr(), C, sc.data_ptr(), sh.data_ptr(), r.data_ptr(), C, *m2, mode,
+                      a.data_ptr(), C, M, C, bits.data_ptr(), _st())
+    torch.cuda.synchronize()
+    assert torch.equal(a.view(torch.int16), a_ref.view(torch.int16))
+    want = (a.float() > 0).view(M, C // 8, 8).to(torch.int32)
+    want = (want << torch.arange(8, device=DEV, dtype=torch.int32)).sum(-1).to(torch.uint8).view(-1)
+    assert torch.equal(bits, want)
+    # backward through the same BN with the mask from the activation vs from the bits
+    dA = torch.randn(M, C, generator=g, device=DEV).to(bf)
+    mean, inv = torch.randn(C, generator=g, device=DEV) * 0.1, torch.rand(C, generator=g, device=DEV) + 0.5
+    Gr = lib.reduce_tiles(DT_BF16, M, C, None, None)
+    outs = []
+    for src, lda in ((a, C), (bits, 0)):
+        part = torch.empty(3, C, Gr, device=DEV)
+        y2 = (r.data_ptr(), C, mean.data_ptr(), inv.data_ptr()) if mode == 2 else (0, 0, 0, 0)
+        lib.bn_bwd_reduce(DT_BF16, dA.data_ptr(), C, src.data_ptr(), lda, 0, 0, y.data_ptr(), C, mean.data_ptr(),
+                          inv.data_ptr(), *y2, M, C, part.data_ptr(), Gr, _st())
+        coef = torch.randn(6, C, generator=torch.Generator(device=DEV).manual_seed(1), device=DEV)
+        dy1 = torch.empty(M, C, dtype=bf, device=DEV)
+        dy2 = torch.empty(M, C, dtype=bf, device=DEV)
+        dz = torch.empty(M, C, dtype=bf, device=DEV)
+        yb = (r.data_ptr(), C, mean.data_ptr(), inv.data_ptr(), dy2.data_ptr(), C) if mode == 2 else (0, 0, 0, 0, 0, 0)
+        lib.bn_bwd_apply(DT_BF16, dA.data_ptr(), C, src.data_ptr(), lda, 0, 0, y.data_ptr(), C, mean.data_ptr(),
+                         inv.data_ptr(), dy1.data_ptr(), C, *yb, coef.data_ptr(), dz.data_ptr(), C, 0, M, C, _st())
+        torch.cuda.synchronize()
+        outs.append((part.clone(), dy1.clone(), dy2.clone() if mode == 2 else None, dz.clone()))
+    (p0, d0, e0, z0), (p1, d1, e1, z1) = outs
+    nq = 3 if mode == 2 else 2
+    assert torch.equal(p0[:nq], p1[:nq])
+    assert torch.equal(d0.view(torch.int16), d1.view(torch.int16))
+    assert torch.equal(z0.view(torch.int16), z1.view(torch.int16))
+    if mode == 2:
+        assert torch.equal(e0.view(torch.int16), e1.view(torch.int16))

@@ -86,10 +86,12 @@ __global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, con
 }
 
 // out = act(y*sc + sh + res); res: 0 none, 1 raw tensor r, 2 r*sc2 + sh2
+// mbits (may be NULL): the ReLU mask of `out` packed one byte per (pixel, V-channel vector), bit e =
+// (stored out[c0 + e] > 0), [M][C/V] -- the BN backward reads it instead of the whole activation
 template <typename T>
 __global__ void bn_apply_kernel(const T* y, int ldy, const float* sc, const float* sh, const T* r, int ldr,
                                 const float* sc2, const float* sh2, int res_mode, int relu, T* out, int ldo, long M,
-                                int C) {
+                                int C, uint8_t* mbits) {
   constexpr int V = VE<T>;
   const int cv = C / V;
   const long total = M * cv;
@@ -114,6 +116,12 @@ __global__ void bn_apply_kernel(const T* y, int ldy, const float* sc, const floa
       for (int e = 0; e < V; ++e) v[e] = fmaxf(v[e], 0.f);
     }
     store_vec(out + pix * ldo + c0, v);
+    if (mbits) {
+      unsigned b = 0u;
+#pragma unroll
+      for (int e = 0; e < V; ++e) b |= ((float)(T)v[e] > 0.f ? 1u : 0u) << e;
+      mbits[i] = (uint8_t)b;  // i == pix * cv + c0 / V
+    }
   }
 }
 
@@ -170,7 +178,8 @@ __device__ __forceinline__ void store_partials(float (&s)[NQ][V], int tv, int c0
 // BatchNorm backward, pass 1: per-(channel, pixel tile) partials of
 //   sum dz, sum dz*xhat1, sum dz*xhat2     where dz = dA * mask
 // MASK: 0 none, 1 (A > 0), 2 (y1*msc + msh > 0) -- the ReLU mask recomputed exactly as bn_apply
-// produced A.  Y2: second BN branch (downsample shortcut) present.
+// produced A, 3 the packed mask bn_apply wrote (A = mbits [M][C/V] bytes).  Y2: second BN branch
+// (downsample shortcut) present.
 template <typename T, int MASK, bool Y2>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dA, int ldd, const T* A, int lda,
                                                             const float* msc, const float* msh, const T* y1, int ld1,
@@ -196,11 +205,16 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dA, int ldd
     ms[e] = MASK == 2 ? msc[c0 + e] : 0.f;
     mh[e] = MASK == 2 ? msh[c0 + e] : 0.f;
   }
+  const uint8_t* mb = reinterpret_cast<const uint8_t*>(A);
+  const int cv = C / V;
   auto acc = [&](const uint4& rd, const uint4& rx, const uint4& ra, const uint4& r2) {
     float d[V], x[V];
     cvt16<T>(rd, d);
     cvt16<T>(rx, x);
-    if (MASK == 1) {
+    if (MASK == 3) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) d[e] = (ra.x >> e) & 1u ? d[e] : 0.f;
+    } else if (MASK == 1) {
       float a[V];
       cvt16<T>(ra, a);
 #pragma unroll
@@ -209,16 +223,18 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dA, int ldd
 #pragma unroll
       for (int e = 0; e < V; ++e) d[e] = fmaf(x[e], ms[e], mh[e]) > 0.f ? d[e] : 0.f;
     }
+    // explicit fmaf: the same rounding in every MASK / Y2 instantiation (the compiler's own
+    // contraction choices differed between them)
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       s[0][e] += d[e];
-      s[1][e] += d[e] * ((x[e] - m1[e]) * i1[e]);
+      s[1][e] = fmaf(d[e], (x[e] - m1[e]) * i1[e], s[1][e]);
     }
     if (Y2) {
       float x2[V];
       cvt16<T>(r2, x2);
 #pragma unroll
-      for (int e = 0; e < V; ++e) s[NQ - 1][e] += d[e] * ((x2[e] - m2v[e]) * i2v[e]);
+      for (int e = 0; e < V; ++e) s[NQ - 1][e] = fmaf(d[e], (x2[e] - m2v[e]) * i2v[e], s[NQ - 1][e]);
     }
   };
   long p = p0 + ty;
@@ -230,6 +246,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dA, int ldd
       rd[u] = *reinterpret_cast<const uint4*>(dA + q * ldd + c0);
       rx[u] = *reinterpret_cast<const uint4*>(y1 + q * ld1 + c0);
       if (MASK == 1) ra[u] = *reinterpret_cast<const uint4*>(A + q * lda + c0);
+      if (MASK == 3) ra[u].x = mb[q * cv + c0 / V];
       if (Y2) r2[u] = *reinterpret_cast<const uint4*>(y2 + q * ld2 + c0);
     }
 #pragma unroll
@@ -239,6 +256,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dA, int ldd
     uint4 rd = *reinterpret_cast<const uint4*>(dA + p * ldd + c0), ra = rd, r2 = rd;
     const uint4 rx = *reinterpret_cast<const uint4*>(y1 + p * ld1 + c0);
     if (MASK == 1) ra = *reinterpret_cast<const uint4*>(A + p * lda + c0);
+    if (MASK == 3) ra.x = mb[p * cv + c0 / V];
     if (Y2) r2 = *reinterpret_cast<const uint4*>(y2 + p * ld2 + c0);
     acc(rd, rx, ra, r2);
   }
@@ -310,11 +328,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dA, int ldd,
     ms[e] = MASK == 2 ? msc[c] : 0.f;
     mh[e] = MASK == 2 ? msh[c] : 0.f;
   }
+  const uint8_t* mb = reinterpret_cast<const uint8_t*>(A);
+  const int cv = C / V;
   auto one = [&](long q, const uint4& rd, const uint4& rx, const uint4& ra, const uint4& r2, const uint4& rz) {
     float d[V], x[V], o[V];
     cvt16<T>(rd, d);
     cvt16<T>(rx, x);
-    if (MASK == 1) {
+    if (MASK == 3) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) d[e] = (ra.x >> e) & 1u ? d[e] : 0.f;
+    } else if (MASK == 1) {
       float a[V];
       cvt16<T>(ra, a);
 #pragma unroll
@@ -350,6 +373,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dA, int ldd,
       rd[u] = *reinterpret_cast<const uint4*>(dA + q * ldd + c0);
       rx[u] = *reinterpret_cast<const uint4*>(y1 + q * ld1 + c0);
       if (MASK == 1) ra[u] = *reinterpret_cast<const uint4*>(A + q * lda + c0);
+      if (MASK == 3) ra[u].x = mb[q * cv + c0 / V];
       if (Y2) r2[u] = *reinterpret_cast<const uint4*>(y2 + q * ld2 + c0);
       if (DZ == 2) rz[u] = *reinterpret_cast<const uint4*>(dzout + q * ldz + c0);
     }
@@ -361,6 +385,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dA, int ldd,
     const uint4 rx = *reinterpret_cast<const uint4*>(y1 + p * ld1 + c0);
     uint4 ra = rd, r2 = rd, rz = rd;
     if (MASK == 1) ra = *reinterpret_cast<const uint4*>(A + p * lda + c0);
+    if (MASK == 3) ra.x = mb[p * cv + c0 / V];
     if (Y2) r2 = *reinterpret_cast<const uint4*>(y2 + p * ld2 + c0);
     if (DZ == 2) rz = *reinterpret_cast<const uint4*>(dzout + p * ldz + c0);
     one(p, rd, rx, ra, r2, rz);
@@ -1247,8 +1272,20 @@ UNETSEG_API int unetseg_bn_apply(int dtype, const void* y, int ldy, const float*
   CHECK_VEC(dtype, C, "bn_apply");
   DISPATCH_T(dtype, hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(M * C / VE<T>)), dim3(256), 0,
                                        (hipStream_t)stream, (const T*)y, ldy, sc, sh, (const T*)r, ldr, sc2, sh2,
-                                       res_mode, relu, (T*)out, ldo, M, C));
+                                       res_mode, relu, (T*)out, ldo, M, C, nullptr));
   US_LAUNCH_CHECK("bn_apply");
+  return 0;
+}
+
+UNETSEG_API int unetseg_bn_apply_mask(int dtype, const void* y, int ldy, const float* sc, const float* sh,
+                                      const void* r, int ldr, const float* sc2, const float* sh2, int res_mode,
+                                      void* out, int ldo, long M, int C, uint8_t* mbits, void* stream) {
+  CHECK_VEC(dtype, C, "bn_apply_mask");
+  US_CHECK_ARG(mbits != nullptr, "bn_apply_mask: mbits required");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(M * C / VE<T>)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)y, ldy, sc, sh, (const T*)r, ldr, sc2, sh2,
+                                       res_mode, 1, (T*)out, ldo, M, C, mbits));
+  US_LAUNCH_CHECK("bn_apply_mask");
   return 0;
 }
 
@@ -1283,18 +1320,20 @@ UNETSEG_API int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const 
   US_CHECK_ARG(g == G, "bn_bwd_reduce: G mismatch (%d vs %d)", G, g);
   const int V = dtype == DT_BF16 ? 8 : 4;
   dim3 grid(G, C / V / tv);
-  const int mask = A ? 1 : (msc ? 2 : 0);
+  const int mask = A ? (lda == 0 ? 3 : 1) : (msc ? 2 : 0);
   hipStream_t st = (hipStream_t)stream;
 #define BN_RED_LAUNCH(MK, Y2)                                                                                     \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MK, Y2>), grid, dim3(256), 0, st, (const T*)dA, ldd, (const T*)A, lda, \
                      msc, msh, (const T*)y1, ld1, mean1, inv1, (const T*)y2, ld2, mean2, inv2, M, C, tv, ppb, part, G)
   DISPATCH_T(dtype, {
     if (y2) {
-      if (mask == 1) BN_RED_LAUNCH(1, true);
+      if (mask == 3) BN_RED_LAUNCH(3, true);
+      else if (mask == 1) BN_RED_LAUNCH(1, true);
       else if (mask == 2) BN_RED_LAUNCH(2, true);
       else BN_RED_LAUNCH(0, true);
     } else {
-      if (mask == 1) BN_RED_LAUNCH(1, false);
+      if (mask == 3) BN_RED_LAUNCH(3, false);
+      else if (mask == 1) BN_RED_LAUNCH(1, false);
       else if (mask == 2) BN_RED_LAUNCH(2, false);
       else BN_RED_LAUNCH(0, false);
     }
@@ -1324,7 +1363,7 @@ UNETSEG_API int unetseg_bn_bwd_apply(int dtype, const void* dA, int ldd, const v
   const int G = unetseg_reduce_tiles(dtype, M, C, &tv, &ppb);
   const int V = dtype == DT_BF16 ? 8 : 4;
   dim3 grid(G, C / V / tv);
-  const int mask = A ? 1 : (msc ? 2 : 0);
+  const int mask = A ? (lda == 0 ? 3 : 1) : (msc ? 2 : 0);
   const int dzm = dzout ? (dz_acc ? 2 : 1) : 0;
   hipStream_t st = (hipStream_t)stream;
 #define BN_APP_LAUNCH(MK, Y2, DZ)                                                                                  \
@@ -1339,11 +1378,13 @@ UNETSEG_API int unetseg_bn_bwd_apply(int dtype, const void* dA, int ldd, const v
   } while (0)
   DISPATCH_T(dtype, {
     if (y2) {
-      if (mask == 1) BN_APP_DZ(1, true);
+      if (mask == 3) BN_APP_DZ(3, true);
+      else if (mask == 1) BN_APP_DZ(1, true);
       else if (mask == 2) BN_APP_DZ(2, true);
       else BN_APP_DZ(0, true);
     } else {
-      if (mask == 1) BN_APP_DZ(1, false);
+      if (mask == 3) BN_APP_DZ(3, false);
+      else if (mask == 1) BN_APP_DZ(1, false);
       else if (mask == 2) BN_APP_DZ(2, false);
       else BN_APP_DZ(0, false);
     }

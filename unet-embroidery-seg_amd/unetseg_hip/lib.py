@@ -47,6 +47,7 @@ SIGNATURES = {
     "unetseg_bn_finalize": (I, [P, I, I, L, I, P, P, P, P, P, F, F, P, P, P, P, P]),
     "unetseg_bn_eval_coeffs": (I, [I, P, P, P, P, F, P, P, P]),
     "unetseg_bn_apply": (I, [I, P, I, P, P, P, I, P, P, I, I, P, I, L, I, P]),
+    "unetseg_bn_apply_mask": (I, [I, P, I, P, P, P, I, P, P, I, P, I, L, I, P, P]),
     "unetseg_reduce_tiles": (I, [I, L, I, P, P]),
     "unetseg_bn_bwd_reduce": (I, [I, P, I, P, I, P, P, P, I, P, P, P, I, P, P, L, I, P, I, P]),
     "unetseg_bn_bwd_finalize": (I, [P, I, I, L, I, P, P, P, P, P, P, P, P, P, P]),

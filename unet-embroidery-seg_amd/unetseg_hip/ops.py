@@ -562,6 +562,9 @@ def _bn_coeffs(ctx, bn, st, M, tile=None):
     return s
 
 
+#: residual BN-add-ReLU stores a packed ReLU mask for its backward (UNETSEG_NO_MASK_BITS=1: read the activation)
+MASK_BITS = os.environ.get("UNETSEG_NO_MASK_BITS", "0") != "1"
+
 #: BN-ReLU applied by the consuming 1x1 conv on load instead of a separate pass (UNETSEG_NO_BN_PROLOGUE=1: off)
 BN_PROLOGUE = os.environ.get("UNETSEG_NO_BN_PROLOGUE", "0") != "1"
 
@@ -594,9 +597,17 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None, lazy=False):
     elif res_bn is not None:
         mode, R = 2, res_bn[0].data
         s2 = _bn_coeffs(ctx, res_bn[2], res_bn[1], M)
+    mbits = None
     if lazy and BN_PROLOGUE and relu and mode == 0 and ctx.training and ctx.dt == DT_BF16:
         out = Node(Y)
         out.lazy = s1
+    elif MASK_BITS and relu and mode != 0 and ctx.training and ctx.dt == DT_BF16:
+        # residual BN-add-ReLU: the backward reads the packed ReLU mask (1/16 of the activation)
+        a = ctx.empty(N, H, W, C)
+        mbits = torch.empty(M * (C // 8), dtype=torch.uint8, device=ctx.device)
+        lib.bn_apply_mask(ctx.dt, P(Y), ldp(Y), P(s1.sc), P(s1.sh), P(R), ldp(R), P(s2.sc if s2 else None),
+                          P(s2.sh if s2 else None), mode, P(a), C, M, C, P(mbits), ctx.stream)
+        out = Node(a)
     else:
         a = ctx.empty(N, H, W, C)
         lib.bn_apply(ctx.dt, P(Y), ldp(Y), P(s1.sc), P(s1.sh), P(R), ldp(R), P(s2.sc if s2 else None),
@@ -631,8 +642,11 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None, lazy=False):
         # plain BN-ReLU: the mask is recomputed from y (no read of the activation)
         plain = relu and res is None and res_bn is None
         mA = 0 if (plain or not relu) else P(out.data)
+        lda = C
+        if mbits is not None:  # the packed mask written by the forward (lda 0 flags it)
+            mA, lda = P(mbits), 0
         msc, msh = (P(s1.sc), P(s1.sh)) if plain else (0, 0)
-        lib.bn_bwd_reduce(ctx.dt, P(dA), ldp(dA), mA, C, msc, msh, P(Y), ldp(Y), P(s1.mean), P(s1.inv),
+        lib.bn_bwd_reduce(ctx.dt, P(dA), ldp(dA), mA, lda, msc, msh, P(Y), ldp(Y), P(s1.mean), P(s1.inv),
                           P(Y2), ldp(Y2), P(s2.mean if s2 else None), P(s2.inv if s2 else None), M, C, P(part), Gr,
                           ctx.stream)
         coef = ctx.f32(6, C)
@@ -653,7 +667,7 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None, lazy=False):
         dz, dzacc = None, 0
         if res is not None and res.need_grad:
             dz, dzacc = gbuf(ctx, res)
-        lib.bn_bwd_apply(ctx.dt, P(dA), ldp(dA), mA, C, msc, msh, P(Y), ldp(Y), P(s1.mean), P(s1.inv),
+        lib.bn_bwd_apply(ctx.dt, P(dA), ldp(dA), mA, lda, msc, msh, P(Y), ldp(Y), P(s1.mean), P(s1.inv),
                          P(dy1), ldp(dy1), P(Y2), ldp(Y2), P(s2.mean if s2 else None), P(s2.inv if s2 else None),
                          P(dy2), ldp(dy2), P(coef), P(dz), ldp(dz), dzacc, M, C, ctx.stream)
 
