@@ -408,22 +408,25 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
 // read serves all 9 taps.  Partials go to slab[slot] in the natural [cout][tap*cin + c] layout of
 // the split-K reduce.
 // ------------------------------------------------------------------------------------------
-template <int TH>
-__global__ __launch_bounds__(256) void halo3_wgrad_kernel(HaloWgradArgs a, int tiles_w, int tiles_h, int n_sp,
-                                                          int G_per) {
-  constexpr int NW = 4;
+// NW = 8: two waves per SIMD -- wave w owns input channels 16 (w % 4) .. of the 9 taps for output
+// channels 32 (w / 4) .. 32 (w / 4) + 31 (the X fragments are read by both halves; the single wave per
+// SIMD of NW = 4 left the MFMA pipe idle while its own LDS reads were in flight).
+template <int TH, int NW>
+__global__ __launch_bounds__(64 * NW) void halo3_wgrad_kernel(HaloWgradArgs a, int tiles_w, int tiles_h, int n_sp,
+                                                              int G_per) {
   constexpr int TP = TH * HW_TW;              // output pixels per tile
   constexpr int HP = (TH + 2) * (HW_TW + 2);  // halo pixels
   constexpr int DCH = TP * 8, HCH = HP * 8;   // 16-B chunks per stage part
   constexpr int DI = DCH / (64 * NW);         // dY DMA instructions per wave
   constexpr int HI = (HCH + 64 * NW - 1) / (64 * NW);
   constexpr int STG = DCH + HCH;              // uint4 per stage
-  constexpr int FM = 4, FN = 9;
+  constexpr int FM = NW == 8 ? 2 : 4, FN = 9;
   static_assert(DCH % (64 * NW) == 0, "tile shape");
   extern __shared__ __attribute__((aligned(16))) uint4 lds[];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wid & 3, wm = NW == 8 ? wid >> 2 : 0;  // input-channel group, output-channel half
   const int mtiles = a.Cout >> 6;
   const int grp = blockIdx.x / G_per, slot = blockIdx.x % G_per;
   const int mt = grp % mtiles, ct = grp / mtiles;
@@ -500,9 +503,9 @@ __global__ __launch_bounds__(256) void halo3_wgrad_kernel(HaloWgradArgs a, int t
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
 #pragma unroll
-    for (int i = 0; i < FM; ++i) pa[i][k] = lane_off(8 * g + qq + 4 * k, i * 2 + (pp >> 1));
+    for (int i = 0; i < FM; ++i) pa[i][k] = lane_off(8 * g + qq + 4 * k, (wm * FM + i) * 2 + (pp >> 1));
 #pragma unroll
-    for (int r = 0; r < 16; ++r) pb[r][k] = lane_off(r + 8 * g + qq + 4 * k, wid * 2 + (pp >> 1));
+    for (int r = 0; r < 16; ++r) pb[r][k] = lane_off(r + 8 * g + qq + 4 * k, wc * 2 + (pp >> 1));
   }
   auto tr2 = [&](const char* base, unsigned o0, unsigned o1) -> bf16x8 {
     s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + o0));
@@ -542,9 +545,9 @@ __global__ __launch_bounds__(256) void halo3_wgrad_kernel(HaloWgradArgs a, int t
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int m = mt * 64 + i * 16 + g * 4 + e;
+      const int m = mt * 64 + (wm * FM + i) * 16 + g * 4 + e;
 #pragma unroll
-      for (int j = 0; j < FN; ++j) ws[(long)m * Ng + (long)j * a.cin + ct * 64 + wid * 16 + i16] = acc[i][j][e];
+      for (int j = 0; j < FN; ++j) ws[(long)m * Ng + (long)j * a.cin + ct * 64 + wc * 16 + i16] = acc[i][j][e];
     }
 }
 
@@ -667,13 +670,20 @@ int launch_halo3_wgrad(const HaloWgradArgs& a, int G_per, hipStream_t st) {
   const int n_sp = a.N * tiles_h * tiles_w;
   const int groups = (a.Cout / 64) * (a.cin / 64);
   const size_t lds = 2 * ((size_t)TH * HW_TW + (size_t)(TH + 2) * (HW_TW + 2)) * 128;
+  static const bool w4 = getenv("UNETSEG_HALO_WG_W4") != nullptr;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_wgrad_kernel<TH>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_wgrad_kernel<TH, 8>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_wgrad_kernel<TH, 4>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((halo3_wgrad_kernel<TH>), dim3(groups * G_per), dim3(256), lds, st, a, tiles_w, tiles_h, n_sp,
-                     G_per);
+  if (w4)
+    hipLaunchKernelGGL((halo3_wgrad_kernel<TH, 4>), dim3(groups * G_per), dim3(256), lds, st, a, tiles_w, tiles_h,
+                       n_sp, G_per);
+  else
+    hipLaunchKernelGGL((halo3_wgrad_kernel<TH, 8>), dim3(groups * G_per), dim3(512), lds, st, a, tiles_w, tiles_h,
+                       n_sp, G_per);
   return 0;
 }
