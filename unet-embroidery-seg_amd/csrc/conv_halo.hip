@@ -642,7 +642,8 @@ bool halo3_wgrad_ok(const HaloWgradArgs& a) {
 
 // Blocks per (cout, cin) group: one persistent block per CU at a time (152 KiB LDS), so the
 // makespan is ceil(groups*G / 256) rounds of ceil(n_sp / G) tiles, plus the split-K reduce that
-// reads G slabs.  Pick the G that minimises that estimate (tile ~2 us, reduce ~4 TB/s).
+// reads G slabs.  Pick the G that minimises that estimate (tile ~1 us with 8 waves, reduce ~4 TB/s;
+// A/B against the 4-wave kernel's 2 us: +0.3-0.9 %).
 int halo3_wgrad_splits(const HaloWgradArgs& a) {
   const int groups = (a.Cout / 64) * (a.cin / 64);
   const int n_sp = a.N * (a.H / 8) * (a.W / HW_TW);
@@ -652,10 +653,12 @@ int halo3_wgrad_splits(const HaloWgradArgs& a) {
   // with the weight gradients on their own stream the makespan matters less than the slab traffic
   // the reduce adds beside the compute stream: UNETSEG_HALO_WG_MAXG caps G (experiments)
   static const int maxg = getenv("UNETSEG_HALO_WG_MAXG") ? atoi(getenv("UNETSEG_HALO_WG_MAXG")) : 512;
+  // seconds per (8 x 32)-pixel tile of one block (the makespan model; UNETSEG_HALO_WG_TILE_US overrides)
+  static const double tile_s = (getenv("UNETSEG_HALO_WG_TILE_US") ? atof(getenv("UNETSEG_HALO_WG_TILE_US")) : 1.0) * 1e-6;
   for (int g = 1; g <= maxg && g <= n_sp; ++g) {
     if (slab * g > 768.0 * (1 << 20)) break;  // workspace cap
     const double rounds = (double)((groups * g + 255) / 256);
-    const double t = rounds * ((n_sp + g - 1) / g) * 2e-6 + slab * g / 4e12;
+    const double t = rounds * ((n_sp + g - 1) / g) * tile_s + slab * g / 4e12;
     if (t < best_t * 0.999) {
       best_t = t;
       best = g;
