@@ -229,9 +229,10 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
       const int row = rb + RSTEP * i;
       uint4 v = ra[i];
       if constexpr (PRE) {  // == bn_apply: (bf16) relu(fmaf(z, sc, sh))
-        bf16* e8 = reinterpret_cast<bf16*>(&v);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) e8[e] = (bf16)fmaxf(fmaf((float)e8[e], psc[e], psh[e]), 0.f);
+        v.x = bnrelu_pair(v.x, (f32x2){psc[0], psc[1]}, (f32x2){psh[0], psh[1]});
+        v.y = bnrelu_pair(v.y, (f32x2){psc[2], psc[3]}, (f32x2){psh[2], psh[3]});
+        v.z = bnrelu_pair(v.z, (f32x2){psc[4], psc[5]}, (f32x2){psh[4], psh[5]});
+        v.w = bnrelu_pair(v.w, (f32x2){psc[6], psc[7]}, (f32x2){psh[6], psh[7]});
       }
       L[row * 8 + swz8(row, kv)] = v;
     }

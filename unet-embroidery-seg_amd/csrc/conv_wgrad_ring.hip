@@ -182,11 +182,17 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_ring_kernel(FastWgradArg
     for (int i = 0; i < FM; ++i) af[i] = trpair(toffA[i][0], toffA[i][1]);
 #pragma unroll
     for (int j = 0; j < FN; ++j) bfr[j] = trpair(toffB[j][0], toffB[j][1]);
-    if constexpr (PRE) {  // == bn_apply: (bf16) relu(fmaf(z, sc, sh))
+    if constexpr (PRE) {  // == bn_apply: (bf16) relu(fmaf(z, sc, sh)); one channel per fragment
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) bfr[j][e] = (bf16)fmaxf(fmaf((float)bfr[j][e], pre_sc[j], pre_sh[j]), 0.f);
+      for (int j = 0; j < FN; ++j) {
+        uint4 u = __builtin_bit_cast(uint4, bfr[j]);
+        const f32x2 sc2 = {pre_sc[j], pre_sc[j]}, sh2 = {pre_sh[j], pre_sh[j]};
+        u.x = bnrelu_pair(u.x, sc2, sh2);
+        u.y = bnrelu_pair(u.y, sc2, sh2);
+        u.z = bnrelu_pair(u.z, sc2, sh2);
+        u.w = bnrelu_pair(u.w, sc2, sh2);
+        bfr[j] = __builtin_bit_cast(bf16x8, u);
+      }
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i)

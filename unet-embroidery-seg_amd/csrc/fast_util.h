@@ -16,6 +16,22 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
 }
 __device__ __forceinline__ int swz8(int row, int ch) { return ch ^ ((row >> 1) & 7); }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// BN-ReLU input prologue on one packed bf16 pair: (bf16) relu(fmaf(z, sc, sh)), bn_apply's expression
+// and rounding, as unpack + one packed fma (v_pk_fma_f32) + round-to-nearest-even pack + ReLU as a
+// signed 16-bit max on the bf16 bit patterns (a negative bf16 is a negative int16; -0 becomes +0) --
+// 3 VALU per pair fewer than the scalar form, which bound the prologue variants' VALU issue.
+__device__ __forceinline__ unsigned bnrelu_pair(unsigned v, f32x2 sc, f32x2 sh) {
+  const f32x2 z = {__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)};
+  const f32x2 r = __builtin_elementwise_fma(z, sc, sh);
+  i16x2 b = __builtin_bit_cast(i16x2, __builtin_convertvector(r, bf16x2));  // one v_cvt_pk_bf16_f32
+  b = __builtin_elementwise_max(b, (i16x2){0, 0});
+  return __builtin_bit_cast(unsigned, b);
+}
+
 // LDS-DMA of 16 B per lane (64 lanes -> 1 KiB contiguous at lds_byte): issued in inline asm so
 // hipcc neither tracks it (no conservative vmcnt(0) before every ds_read) nor reuses M0 (saved and
 // restored inside the statement).  Completion is counted by the caller's explicit vmcnt.
