@@ -16,6 +16,7 @@ import numpy as np
 import torch
 
 from .lib import DT_BF16, DT_F32, lib
+from .lib import dgrad_config as _dgrad_config
 
 BN_TILE = 128  # == unetseg_conv_tile_m(): M tile of the conv kernel, hence of its BN partials
 
@@ -272,6 +273,16 @@ def pack_input(ctx, x, cpad=8):
 PAD_K = os.environ.get("UNETSEG_NO_PADK", "0") != "1"
 
 
+def _dgrad_launches(ctx, ldy, N, Pq, Qq, K, C, R, S, stride, pad, H, W):
+    """kernel launches of one data-gradient call (probe bookkeeping only): one per parity class,
+    the classes merged into one launch (configs multi*) counting once"""
+    if stride == 1 or PROBE is None:
+        return stride * stride
+    cfgs = _dgrad_config(ctx.dt, ldy, N, Pq, Qq, K, C, R, S, stride, pad, C, H, W)
+    merged = sum(1 for c in cfgs if c.startswith("multi"))
+    return len(cfgs) - merged + (1 if merged else 0)
+
+
 def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
     """y = conv(cat[x1, x2]) (+bias if the conv has one, ReLU).  Stride/padding come from the
     Conv2d container.  out: an NHWC view (pixel stride >= K) to write y into, e.g. a channel slice
@@ -404,12 +415,14 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
         elif x2 is None:
             if x1.need_grad and not _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
                 g, acc = gbuf(ctx, x1)
-                with _probe("igemm_tn", flops, stride * stride, ("dgrad",) + desc):
+                with _probe("igemm_tn", flops, _dgrad_launches(ctx, ldp(dY), N, Pq, Qq, K, C1, R, S, stride, pad, H, W),
+                            ("dgrad",) + desc):
                     lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, R, S, stride, pad, P(g),
                                      ldp(g), H, W, acc, ctx.stream)
         elif x1.need_grad or x2.need_grad:
             g = ctx.empty(N, H, W, cin)
-            with _probe("igemm_tn", flops, stride * stride, ("dgrad",) + desc):
+            with _probe("igemm_tn", flops, _dgrad_launches(ctx, ldp(dY), N, Pq, Qq, K, cin, R, S, stride, pad, H, W),
+                        ("dgrad",) + desc):
                 lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, cin, R, S, stride, pad, P(g), cin,
                                  H, W, 0, ctx.stream)
             give_grad(ctx, x1, g[..., :C1])
@@ -470,7 +483,8 @@ def _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
         return False
     g = ctx.empty(N, H, W, C1)
     part = ctx.f32(rows, 2, C1)
-    with _probe("igemm_tn", flops, stride * stride, (f"dgrad_post{kind}",) + desc):
+    with _probe("igemm_tn", flops, _dgrad_launches(ctx, ldp(dY), N, Pq, Qq, K, C1, R, S, stride, pad, H, W),
+                (f"dgrad_post{kind}",) + desc):
         rc = lib.conv2d_dgrad_post(*args, P(g), C1, H, W, kind, P(aux), ldp(aux), *coeffs, P(part), rows, ctx.stream)
     if rc != 0:
         raise RuntimeError(f"unetseg_conv2d_dgrad_post failed ({rc}): {lib_last_error()}")
