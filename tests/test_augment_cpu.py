@@ -129,10 +129,45 @@ def test_pack_batch_layout(tmp_path):
     assert b.src.size == sum(s.image.size for s in samples)
     assert list(b.desc[:, D_NW]) == [s.nw for s in samples]
     assert b.desc[0, D_SRC] == 0 and b.desc[1, D_SRC] == samples[0].image.size
-    with pytest.raises(TypeError):
-        hf_unet_dataset_collate(samples)
+    # the reference's one-argument collate_fn (hf_dataloader.py:183): settings ride on the samples
+    b1 = hf_unet_dataset_collate(samples)
+    assert b1.input_shape == (48, 40) and b1.num_classes == 4 and not b1.binary
+    np.testing.assert_array_equal(b1.tables, b.tables)
+    np.testing.assert_array_equal(b1.desc, b.desc)
+    assert len(b1) == 3 and b1.batch_size == 4  # unpacks as (images, pngs, seg_labels)
     b2 = hf_unet_dataset_collate(samples, [48, 40], 4, "multiclass")
     np.testing.assert_array_equal(b2.tables, b.tables)
+
+
+def test_reference_dataloader_contract(tmp_path):
+    """DataLoader(ds, collate_fn=hf_unet_dataset_collate, pin_memory=True, num_workers=2) as
+    train.py:140-162 builds it: the one-argument collate runs in the workers, the pinning hook is
+    RawBatch.pin_memory, and a batch unpacks into 3 (binary / multiclass) or 4 (multitask) items."""
+    from torch.utils.data import DataLoader
+    make_dataset(str(tmp_path), "full", "train", n=5, seed=8)
+    for cls_label, n_items in ((False, 3), (True, 4)):
+        ds = HFUnetDataset(str(tmp_path), [32, 32], 2, split="train", config="full", task="binary",
+                           return_cls_label=cls_label)
+        dl = DataLoader(ds, batch_size=2, shuffle=False, num_workers=2, collate_fn=hf_unet_dataset_collate,
+                        drop_last=False)
+        batches = list(dl)
+        assert [b.batch_size for b in batches] == [2, 2, 1]
+        assert all(len(b) == n_items and b.binary and b.input_shape == (32, 32) for b in batches)
+        assert callable(getattr(batches[0], "pin_memory", None))  # DataLoader(pin_memory=True)'s hook
+
+
+def test_dataset_memory_mapped(tmp_path):
+    """rows stay in the (memory-mapped) Arrow tables; nothing is materialised per row at
+    construction"""
+    make_dataset(str(tmp_path), "full", "train", n=6, seed=9)
+    ds = HFUnetDataset(str(tmp_path), [32, 32], 2, split="train", config="full")
+    assert len(ds) == 6 and not hasattr(ds, "images")
+    assert all(t.num_rows > 0 for t in ds._tables)
+    np.random.seed(3)
+    s = ds[-1]
+    assert s.input_shape == (32, 32) and s.num_classes == 2 and s.task == "multiclass"
+    with pytest.raises(IndexError):
+        ds[6]
 
 
 def test_augment_rejects_bad_descriptor_before_launch(tmp_path):

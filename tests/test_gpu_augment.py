@@ -137,3 +137,39 @@ def test_train_val_on_parquet(tmp_path, task, model, loss):
     m = val.val(val.parse_args(common + vloss + ["--weights", os.path.join(exp, "weights", "best.pth")]))
     key = "Mean IoU" if task == "multiclass" else "IoU"
     assert 0.0 <= float(m[key]) <= 1.0
+
+
+@pytest.mark.parametrize("cls_label", [False, True])
+def test_reference_loop_contract(tmp_path, cls_label):
+    """the reference's own loader + loop code shape (train.py:140-162, utils/train_and_eval.py:203-207):
+    DataLoader(ds, collate_fn=hf_unet_dataset_collate, pin_memory=True, workers) and
+    ``imgs, pngs, labels = batch; imgs = imgs.to(device)`` -- the batch is the collated tensors,
+    identical to the oracle's restatement of get_random_data + the reference collate; the single
+    item unpacks as the reference's ``(jpg, png, seg_labels[, cls])``"""
+    from utils.hf_dataloader import hf_unet_dataset_collate
+    make_dataset(str(tmp_path), "full", "train", n=5, seed=13)
+    ds = HFUnetDataset(str(tmp_path), [64, 64], 2, split="train", config="full", task="binary",
+                       return_cls_label=cls_label)
+    loader = torch.utils.data.DataLoader(ds, batch_size=2, shuffle=False, num_workers=2, pin_memory=True,
+                                         collate_fn=hf_unet_dataset_collate, drop_last=False)
+    seen = 0
+    for batch in loader:
+        if cls_label:
+            imgs, pngs, labels, cls = batch
+        else:
+            imgs, pngs, labels = batch
+        imgs, pngs, labels = imgs.to("cuda"), pngs.to("cuda"), labels.to("cuda")
+        B = imgs.shape[0]
+        assert imgs.shape == (B, 3, 64, 64) and pngs.dtype == torch.int64 and labels.shape == (B, 64, 64, 3)
+        # replay the worker's draws: samples are re-drawn with the same seeded RNG below
+        seen += B
+    assert seen == 5
+    np.random.seed(21)
+    samples = [ds[i] for i in range(5)]
+    b = hf_unet_dataset_collate(samples)
+    _check(ds, samples, tuple(b))
+    np.random.seed(22)
+    s = ds[3]
+    item = tuple(s)
+    assert len(item) == (4 if cls_label else 3)
+    _check(ds, [s], tuple(torch.from_numpy(np.asarray(v))[None] for v in item[:3]))

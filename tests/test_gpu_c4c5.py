@@ -1,0 +1,410 @@
+"""GPU: the attention-gate kernels and the attention_unet / unet_plain models at the BASELINE
+workloads (C1: unet_plain 128x128 B=2; C4: attention_unet 512x512 B=8).
+
+The pixel tile of the narrow 1x1 kernels (psi conv forward with its BN statistics, ``attn_bwd2``)
+depends on the pixel count M (``pw_tile``, csrc/elem.hip: 2048 halved while a launch would have
+fewer than 512 blocks), so the four gates of attention_unet at 512x512 B=8 each run their own tile:
+
+    gate (model/unet_attention.py:38-55)   M = 8 x H x W   Cs / Cg / Ci      tile
+    up4 (512^2)                            2,097,152       64 / 128 / 32     2048
+    up3 (256^2)                              524,288       128 / 256 / 64    1024
+    up2 (128^2)                              131,072       256 / 512 / 128    256
+    up1 (64^2)                                32,768       512 / 1024 / 256   128
+
+``test_attention_gate_kernels_c4`` runs each kernel of the gate in bf16 (the product precision) at
+those shapes against float64 arithmetic on the same operands; ``test_attention_gate_op_c4_fp32``
+runs the whole gate (theta/phi convs + BNs, ReLU, psi + BN + sigmoid, gating; forward and backward)
+in fp32 against a float64 torch restatement of model/unet_attention.py:30-35.  The model-level
+tests run one full train step of attention_unet at C4 and unet_plain at C1.
+
+Tolerances (stated per check below): fp32 sums of n products within n * 2^-24 of the sum of their
+magnitudes (bounded here by 2e-5 of it); a bf16 store within half an ulp (2^-8 relative, as
+tests/test_gpu_configs.py); merged statistics 1e-5 relative.
+"""
+import contextlib
+import io
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+# (N, H, Cs, Cg, Ci, expected pw tile) -- the four gates of attention_unet at 512x512, B=8
+C4_GATES = [(8, 512, 64, 128, 32, 2048), (8, 256, 128, 256, 64, 1024), (8, 128, 256, 512, 128, 256),
+            (8, 64, 512, 1024, 256, 128)]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from unetseg_hip import load
+    load()
+
+
+def _st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _P(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _bf16_ok(out, ref, what, extra=None):
+    """out (a bf16 store) within half an ulp of ref (+ an absolute allowance for the fp32 error of
+    the value before rounding)"""
+    out, ref = out.double(), ref.double()
+    bound = 2.0 ** -8 * ref.abs() + 1e-6 * ref.abs().max()
+    if extra is not None:
+        bound = bound + extra
+    err = (out - ref).abs()
+    bad = int((err > bound).sum())
+    assert bad == 0, f"{what}: {bad} elements out of bound (max err {err.max().item():.3e})"
+
+
+def _merge(part, tile, M):
+    """merge per-tile (sum, M2-about-the-tile-mean) partials [G][2] -> (sum, M2) in float64"""
+    G = part.shape[0]
+    p = part.double()
+    cnt = torch.full((G,), float(tile), dtype=torch.float64, device=part.device)
+    cnt[-1] = M - tile * (G - 1)
+    tot = p[:, 0].sum()
+    mean = tot / M
+    m2 = (p[:, 1] + cnt * (p[:, 0] / cnt - mean) ** 2).sum()
+    return tot, m2
+
+
+@pytest.mark.parametrize("N,H,Cs,Cg,Ci,tile", C4_GATES)
+def test_attention_gate_kernels_c4(N, H, Cs, Cg, Ci, tile):
+    from unetseg_hip.lib import DT_BF16, lib
+    M = N * H * H
+    assert lib.pw_small_tile(M) == tile, (M, lib.pw_small_tile(M))
+    G = lib.pw_small_tiles(M)
+    g = torch.Generator(device=DEV).manual_seed(M + Ci)
+    st = _st()
+    bf = torch.bfloat16
+    # ---- psi forward: psi = f . w + b (fp32 planar), BN partials of psi per tile ----
+    f = torch.relu(torch.randn(M, Ci, generator=g, device=DEV)).to(bf)  # f = ReLU output (zeros included)
+    w = torch.randn(Ci, generator=g, device=DEV) / math.sqrt(Ci)
+    b = torch.randn(1, generator=g, device=DEV) * 0.1
+    psi = torch.empty(M, dtype=torch.float32, device=DEV)
+    part = torch.empty(G, 2, dtype=torch.float32, device=DEV)
+    lib.pw_small_fwd(DT_BF16, _P(f), Ci, M, M, Ci, 1, _P(w), _P(b), _P(psi), _P(part), st)
+    f64, w64 = f.double(), w.double()
+    ref = f64 @ w64 + b.double()
+    mag = f64.abs() @ w64.abs() + b.double().abs()
+    err = (psi.double() - ref).abs()
+    assert bool((err <= 2e-5 * mag + 1e-7).all()), f"psi: max err {err.max().item():.3e}"
+    tot, m2 = _merge(part, tile, M)
+    pk = psi.double()
+    torch.testing.assert_close(tot, pk.sum(), rtol=1e-5, atol=1e-5 * pk.abs().sum().item())
+    torch.testing.assert_close(m2 / M, pk.var(unbiased=False), rtol=1e-5, atol=1e-9)
+    # ---- apply: alpha = sigmoid(psi*sc + sh), gated = skip * alpha (bf16) ----
+    mean = (pk.mean()).float().reshape(1)
+    inv = (1.0 / torch.sqrt(pk.var(unbiased=False) + 1e-5)).float().reshape(1)
+    sc = (inv * 1.3).contiguous()
+    sh = (0.2 - mean * sc).contiguous()
+    skip = torch.randn(M, Cs, generator=g, device=DEV).to(bf)
+    alpha = torch.empty(M, dtype=torch.float32, device=DEV)
+    gated = torch.empty(M, Cs, dtype=bf, device=DEV)
+    lib.attn_apply(DT_BF16, _P(skip), Cs, _P(psi), _P(sc), _P(sh), _P(alpha), _P(gated), Cs, M, Cs, st)
+    a64 = torch.sigmoid(pk * sc.double() + sh.double())
+    torch.testing.assert_close(alpha.double(), a64, rtol=2e-6, atol=1e-7)
+    _bf16_ok(gated, skip.double() * alpha.double()[:, None], "gated")
+    # ---- backward 1: dskip (+)= dg * alpha, dpsibn = (dg . skip) alpha (1 - alpha), partials ----
+    dg = torch.randn(M, Cs, generator=g, device=DEV).to(bf)
+    G1 = lib.attn_bwd1_tiles(M)
+    dpsibn = torch.empty(M, dtype=torch.float32, device=DEV)
+    p1 = torch.empty(2, G1, dtype=torch.float32, device=DEV)
+    ds = torch.empty(M, Cs, dtype=bf, device=DEV)
+    lib.attn_bwd1(DT_BF16, _P(dg), Cs, _P(skip), Cs, _P(alpha), _P(psi), _P(mean), _P(inv), _P(ds), Cs, 0,
+                  _P(dpsibn), M, Cs, _P(p1), st)
+    al = alpha.double()
+    _bf16_ok(ds, dg.double() * al[:, None], "dskip")
+    dot = (dg.double() * skip.double()).sum(1)
+    dmag = (dg.double() * skip.double()).abs().sum(1)
+    ref = dot * al * (1 - al)
+    err = (dpsibn.double() - ref).abs()
+    assert bool((err <= 2e-5 * dmag * al * (1 - al) + 1e-12).all()), f"dpsibn: max err {err.max().item():.3e}"
+    dk = dpsibn.double()
+    xh = (pk - mean.double()) * inv.double()
+    torch.testing.assert_close(p1[0].double().sum(), dk.sum(), rtol=1e-5, atol=1e-5 * dk.abs().sum().item())
+    torch.testing.assert_close(p1[1].double().sum(), (dk * xh).sum(), rtol=1e-5,
+                               atol=1e-5 * (dk * xh).abs().sum().item())
+    # accumulate onto an existing skip gradient (the skip is also read by the theta conv)
+    old = torch.randn(M, Cs, generator=g, device=DEV).to(bf)
+    ds.copy_(old)
+    lib.attn_bwd1(DT_BF16, _P(dg), Cs, _P(skip), Cs, _P(alpha), _P(psi), _P(mean), _P(inv), _P(ds), Cs, 1,
+                  _P(dpsibn), M, Cs, _P(p1), st)
+    _bf16_ok(ds, dg.double() * al[:, None] + old.double(), "dskip accumulated",
+             extra=1e-6 * (dg.double().abs() + old.double().abs()))
+    # ---- backward 2: dpsi from the BN backward coefficients, dz_f = dpsi w (f > 0), dW / db partials ----
+    coef = torch.tensor([1.7, 0.05, -0.3, 0, 0, 0], dtype=torch.float32, device=DEV)
+    dzf = torch.empty(M, Ci, dtype=bf, device=DEV)
+    pw = torch.empty(Ci, G, dtype=torch.float32, device=DEV)
+    pb = torch.empty(1, G, dtype=torch.float32, device=DEV)
+    lib.attn_bwd2(DT_BF16, _P(dpsibn), _P(psi), _P(mean), _P(inv), _P(coef), _P(f), Ci, _P(w), _P(dzf), Ci, M, Ci,
+                  _P(pw), _P(pb), st)
+    c0, c1, c2 = (float(v) for v in coef[:3].tolist())
+    xh32 = ((psi - mean) * inv).double()
+    dp = c0 * (dk - c1 - xh32 * c2)
+    dp_tol = 1e-6 * abs(c0) * (dk.abs() + abs(c1) + (xh32 * c2).abs())
+    ref = torch.where(f64 > 0, dp[:, None] * w64[None, :], torch.zeros_like(f64))
+    _bf16_ok(dzf, ref, "dz_f", extra=dp_tol[:, None] * w64.abs()[None, :])
+    assert bool((dzf.double()[f64 <= 0] == 0).all())
+    sw = (dp[:, None] * f64).sum(0)
+    swm = (dp.abs()[:, None] * f64).sum(0)
+    err = (pw.double().sum(1) - sw).abs()
+    assert bool((err <= 2e-4 * swm + 1e-3 * dp_tol.sum()).all()), f"dW_psi: max err {err.max().item():.3e}"
+    torch.testing.assert_close(pb.double().sum(), dp.sum(), rtol=1e-4, atol=2e-4 * dp.abs().sum().item())
+
+
+@pytest.mark.parametrize("N,H,Cs,Cg,Ci,tile", C4_GATES)
+def test_attention_gate_op_c4_fp32(N, H, Cs, Cg, Ci, tile):
+    """ops.attention_gate (the whole gate, training mode) in fp32 at the C4 gate shapes against a
+    float64 torch restatement of model/unet_attention.py:30-35: output within 1e-4 of its max,
+    input gradients 1e-4 (away from the ReLU's fp32 rounding edge, see below), every parameter
+    gradient 1e-3 relative to its max or 2x the error of torch's own fp32 run of the same code (the psi
+    bias, in front of a batch-statistics BN, has an exactly zero gradient)."""
+    from model.unet_attention import AttentionGate
+    from unetseg_hip import ops
+    from unetseg_hip.lib import DT_F32
+    g = torch.Generator(device=DEV).manual_seed(N * H + Cs)
+    gm = AttentionGate(Cg, Cs, Ci)
+    for p in gm.parameters():
+        p.data = torch.randn(p.shape, generator=torch.Generator().manual_seed(p.numel())) * (0.3 if p.dim() > 1 else 0.2)
+    for bnm in (gm.theta[1], gm.phi[1], gm.psi[1]):
+        bnm.weight.data += 1.0
+    gm = gm.to(DEV)
+    ref_params = {n: p.data.clone() for n, p in gm.named_parameters()}
+    for p in gm.parameters():
+        p.grad = torch.zeros_like(p)
+    ctx = ops.Ctx(DT_F32, True, True, torch.device(DEV))
+    for conv in (gm.theta[0], gm.phi[0]):
+        conv._pc = ops.PackedConv(conv)
+        conv._pc.pack(ctx, True)
+    skip = torch.randn(N, H, H, Cs, generator=g, device=DEV)
+    gate = torch.randn(N, H, H, Cg, generator=g, device=DEV)
+    sn, gn = ops.Node(skip.clone()), ops.Node(gate.clone())
+    out = ops.attention_gate(ctx, sn, gn, gm, gm.theta[0]._pc, gm.phi[0]._pc)
+    dout = torch.randn(N, H, H, Cs, generator=g, device=DEV)
+    out.grad = dout.clone()
+    ctx.backward()
+    torch.cuda.synchronize()
+
+    def reference(dt):
+        rp = {n: v.detach().to(dt).clone().requires_grad_(True) for n, v in ref_params.items()}
+        sr, gr = skip.to(dt).requires_grad_(True), gate.to(dt).requires_grad_(True)
+
+        def conv1x1(x, wname, bname=None):  # NHWC
+            y = x @ rp[wname].reshape(rp[wname].shape[0], -1).t()
+            return y + rp[bname] if bname else y
+
+        def bn(x, pre):  # training-mode BN over N, H, W (channels last)
+            m = x.mean((0, 1, 2))
+            v = x.var((0, 1, 2), unbiased=False)
+            return (x - m) / torch.sqrt(v + 1e-5) * rp[pre + ".weight"] + rp[pre + ".bias"]
+
+        th, ph = conv1x1(sr, "theta.0.weight"), conv1x1(gr, "phi.0.weight")
+        pre = bn(th, "theta.1") + bn(ph, "phi.1")
+        f = torch.relu(pre)
+        f.retain_grad()
+        psi_lin = conv1x1(f, "psi.0.weight", "psi.0.bias")
+        psi_lin.retain_grad()
+        ref = sr * torch.sigmoid(bn(psi_lin, "psi.1"))
+        ref.backward(dout.to(dt))
+        # per-channel BN scales gamma / sigma of theta and phi (what a ReLU flip's gradient passes through)
+        scl = {k: (rp[k + ".1.weight"] / torch.sqrt(t.var((0, 1, 2), unbiased=False) + 1e-5)).detach().abs()
+               for k, t in (("theta", th), ("phi", ph))}
+        return (ref.detach(), sr.grad, gr.grad, {n: v.grad for n, v in rp.items()}, pre.detach(), psi_lin.grad,
+                f.grad, scl)
+
+    ref, dsr, dgr, pgr, pre, dpsi, df, scl = reference(torch.float64)
+    pgr32 = reference(torch.float32)[3]  # torch's own fp32 error, the scale for the parameters
+
+    def rel(a, b, keep=None):
+        d = (a.double() - b.double()).abs()
+        if keep is not None:
+            d = d[keep]
+        return float(d.max() / (b.double().abs().max() + 1e-30))
+
+    assert rel(out.data, ref) < 1e-4
+    # a pixel whose ReLU input sum(theta, phi) is within fp32 rounding of 0 may take the other side of
+    # the ReLU in any fp32 computation (torch's own fp32 run flips 1-3 of them at these shapes: an
+    # O(1) change of that pixel's input gradients); every other pixel is held to 1e-4
+    edge = (pre.abs() < 4e-6 * pre.abs().max()).any(-1)
+    assert int(edge.sum()) <= 8 + pre.numel() // 10000, int(edge.sum())
+    keep = ~edge
+    assert rel(sn.grad, dsr, keep) < 1e-4
+    assert rel(gn.grad, dgr, keep) < 1e-4
+    # parameter gradients sum over every pixel, the ReLU-edge ones included: 1e-3 (or 2x torch's own fp32
+    # error where that is larger) plus what flipping every edge element could change: sum over edge
+    # (pixel, channel k) of |dL/df| x BN scale_k x max|conv input| (theta / phi weights), |dL/df| x
+    # max(1, |xhat|) (their BN parameters)
+    emask = (pre.abs() < 4e-6 * pre.abs().max()).double()
+    flip = emask * df.abs()                                       # [N, H, W, Ci]
+    xin = {"theta": skip.abs().amax(-1), "phi": gate.abs().amax(-1)}
+    allow = {}
+    for k in ("theta", "phi"):
+        allow[f"{k}.0.weight"] = float((flip * scl[k] * xin[k][..., None].double()).sum())
+        allow[f"{k}.1.weight"] = allow[f"{k}.1.bias"] = float(flip.sum() * max(1.0, float(pre.abs().max())))
+    for n, p in gm.named_parameters():
+        if n == "psi.0.bias":  # exactly 0: an fp32 sum of M terms that cancel, held to 1e-5 of sum |term|
+            assert p.grad.abs().max().item() <= 1e-5 * dpsi.abs().sum().item()
+            continue
+        scale = pgr[n].double().abs().max().item()
+        bound = max(1e-3, 2 * rel(pgr32[n], pgr[n])) + allow.get(n, 0.0) / scale
+        assert rel(p.grad, pgr[n]) < bound, (n, rel(p.grad, pgr[n]), rel(pgr32[n], pgr[n]), bound)
+
+
+# ------------------------------------------------------------------------------------------------
+# model level
+# ------------------------------------------------------------------------------------------------
+@contextlib.contextmanager
+def _torch_exact():
+    prev = (torch.backends.cudnn.enabled, torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32)
+    torch.backends.cudnn.enabled = False
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    try:
+        yield
+    finally:
+        (torch.backends.cudnn.enabled, torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32) = prev
+
+
+def _hip(name, state, dtype):
+    from model.model_factory import build_model
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = build_model(name, num_classes=2)
+    m.load_state_dict(state)
+    m = m.to(DEV).train()
+    m.compute_dtype = dtype
+    for p in m.parameters():
+        p.grad = None
+    return m
+
+
+def _err(a, b):
+    d = (a.double() - b.double()).abs()
+    return d.max().item(), d.mean().item()
+
+
+def _rel_l2(a, b):
+    n = b.double().norm().item()
+    return (a.double() - b.double()).norm().item() / n if n > 0 else 0.0
+
+
+#: HIP bf16 vs the bf16-storage emulation, as a fraction of the reference's own bf16-autocast
+#: deviation from fp32 (max and mean |d logit|); measured values in DESIGN.md section 4
+EMU_FRAC = 0.45
+
+
+def test_attention_unet_train_step_512_b8_bf16():
+    """C4 at its workload: attention_unet, 512x512, B=8, bf16, fwd + Lovasz + bwd against three oracle
+    runs in torch on the GPU (f32 / the reference's bf16 autocast / the bf16-storage emulation of the
+    HIP path's rounding points, oracle/ref_cpu.py Ctx.bf16_storage).  Logits: HIP-vs-emu within
+    EMU_FRAC of amp-vs-f32 (max and mean); HIP-vs-f32 no worse than 1.5x amp-vs-f32; loss within 2x
+    amp's deviation + 1e-3 relative; gradients: median relative L2 over tensors no worse than 1.5x
+    amp's, and every tensor that bf16 storage moves by < 5 % held individually (1.5x amp + 1e-3)."""
+    from oracle import ref_cpu
+    from oracle.weights import make_torch_state
+    from unetseg_hip.losses import binary_segmentation_loss
+    from utils.synthetic import make_batch
+    name = "attention_unet"
+    state = make_torch_state(ref_cpu.model_spec(name, num_classes=2))
+    x, y = make_batch(8, 512, seed=41)
+    xd, yd = x.to(DEV), y.to(DEV)
+    m = _hip(name, state, "bf16")
+    out = m(xd)
+    loss = binary_segmentation_loss(out, yd, "lovasz_hinge")
+    loss.backward()
+    torch.cuda.synchronize()
+    hip_out = out.detach().float()
+    hip_grads = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+    hip_loss = loss.item()
+    del m, out, loss
+    torch.cuda.empty_cache()
+    runs = {}
+    for tag, kw in (("f32", {}), ("amp", dict(autocast_bf16=True)), ("emu", dict(bf16_storage=True))):
+        params, buffers = ref_cpu.split_state(state)
+        params = {k: v.to(DEV).detach().requires_grad_(True) for k, v in params.items()}
+        buffers = {k: v.to(DEV) for k, v in buffers.items()}
+        with _torch_exact():
+            l_, o_, g_ = ref_cpu.train_step(name, params, buffers, xd, yd, "lovasz_hinge", **kw)
+        runs[tag] = (l_.item(), o_.float(), g_)
+        del params, buffers
+        torch.cuda.empty_cache()
+    f32 = runs["f32"]
+    e_emu, e_f32, e_amp = _err(hip_out, runs["emu"][1]), _err(hip_out, f32[1]), _err(runs["amp"][1], f32[1])
+    gh = sorted(_rel_l2(hip_grads[k], v) for k, v in f32[2].items())
+    ga = sorted(_rel_l2(runs["amp"][2][k], v) for k, v in f32[2].items())
+    ge = sorted(_rel_l2(hip_grads[k], v) for k, v in runs["emu"][2].items())
+    print(f"\nattention_unet 512 B=8: max|logit| {f32[1].abs().max().item():.3f}  hip-emu {e_emu[0]:.3e}/{e_emu[1]:.3e}"
+          f"  hip-f32 {e_f32[0]:.3e}/{e_f32[1]:.3e}  amp-f32 {e_amp[0]:.3e}/{e_amp[1]:.3e}")
+    print(f"loss hip {hip_loss:.6f} f32 {f32[0]:.6f} amp {runs['amp'][0]:.6f} emu {runs['emu'][0]:.6f}")
+    print(f"grad rel L2 median/max: hip-f32 {gh[len(gh) // 2]:.3e}/{gh[-1]:.3e} amp-f32 {ga[len(ga) // 2]:.3e}/"
+          f"{ga[-1]:.3e} hip-emu {ge[len(ge) // 2]:.3e}/{ge[-1]:.3e}")
+    assert e_emu[0] <= EMU_FRAC * e_amp[0] and e_emu[1] <= EMU_FRAC * e_amp[1], (e_emu, e_amp)
+    assert e_f32[0] <= 1.5 * e_amp[0] and e_f32[1] <= 1.5 * e_amp[1], (e_f32, e_amp)
+    assert abs(hip_loss - f32[0]) <= 2 * abs(runs["amp"][0] - f32[0]) + 1e-3 * abs(f32[0])
+    assert gh[len(gh) // 2] <= 1.5 * ga[len(ga) // 2], (gh[len(gh) // 2], ga[len(ga) // 2])
+    well = 0
+    for k, v in f32[2].items():
+        ra = _rel_l2(runs["amp"][2][k], v)
+        if v.double().norm().item() > 0 and ra < 0.05:
+            well += 1
+            rh = _rel_l2(hip_grads[k], v)
+            assert rh <= 1.5 * ra + 1e-3, (k, rh, ra)
+    print(f"well-conditioned gradient tensors checked individually: {well}")
+    assert well >= 10
+
+
+def test_unet_plain_128_b2_golden(golden_dir):
+    """C1 (unet_plain, 128x128, batch 2) on the HIP path against the reference's own outputs for
+    that exact workload (tests/golden/model_unet_plain.npz, oracle/gen_golden.py):
+      fp32: train-mode logits within 1e-3 (north_star), Lovasz / BCE losses 1e-4 relative, every
+      parameter-gradient norm within 2 % (test_gpu_round2.py's bound), running statistics 1e-4, and
+      eval-mode logits (with the updated running statistics) within 1e-3;
+      bf16 (the product kernels): logits no further from the reference's fp32 logits than 1.5x the
+      reference's own CPU bf16-autocast output (``out_bf16``) is, max and mean."""
+    from oracle import ref_cpu
+    from oracle.weights import make_torch_state
+    from unetseg_hip.losses import binary_segmentation_loss
+    d = np.load(os.path.join(golden_dir, "model_unet_plain.npz"))
+    x, y = torch.from_numpy(d["x"]).to(DEV), torch.from_numpy(d["y"]).to(DEV)
+    assert tuple(x.shape) == (2, 3, 128, 128)
+    state = make_torch_state(ref_cpu.model_spec("unet_plain", num_classes=2))
+    m = _hip("unet_plain", state, "fp32")
+    out = m(x)
+    loss = binary_segmentation_loss(out, y, "lovasz_hinge")
+    loss.backward()
+    assert np.abs(out.detach().cpu().numpy() - d["out"]).max() < 1e-3
+    assert abs(loss.item() - d["loss"][0]) < 1e-4 * abs(d["loss"][0])
+    bce = binary_segmentation_loss(out.detach(), y, "bce")
+    assert abs(bce.item() - d["loss"][1]) < 1e-4 * abs(d["loss"][1])
+    named = dict(m.named_parameters())
+    bad = [(n, float(named[n].grad.double().norm()), r) for n, r in zip(d["grad_names"], d["grad_norms"])
+           if abs(float(named[n].grad.double().norm()) - r) > 2e-2 * r + 1e-5]
+    assert not bad, bad[:5]
+    bufs = dict(m.named_buffers())
+    for k in d.files:
+        if k.startswith("state::"):
+            np.testing.assert_allclose(bufs[k[7:]].cpu().numpy(), d[k], rtol=1e-4, atol=1e-5)
+    m.eval()
+    with torch.no_grad():
+        ev = m(x)
+    assert np.abs(ev.cpu().numpy() - d["eval_out"]).max() < 1e-3
+    # bf16 product kernels at the same workload
+    mb = _hip("unet_plain", state, "bf16")
+    with torch.no_grad():
+        ob = mb(x).float().cpu()
+    ref = torch.from_numpy(d["out"])
+    e_hip, e_ref = _err(ob, ref), _err(torch.from_numpy(d["out_bf16"]), ref)
+    print(f"\nunet_plain 128 B=2 bf16: hip-f32 {e_hip[0]:.3e}/{e_hip[1]:.3e}  ref autocast-f32 {e_ref[0]:.3e}/{e_ref[1]:.3e}")
+    assert e_hip[0] <= 1.5 * e_ref[0] and e_hip[1] <= 1.5 * e_ref[1], (e_hip, e_ref)

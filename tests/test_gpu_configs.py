@@ -14,8 +14,9 @@ Tolerances (stated here):
     <= 2^-8 relative, plus fp32 accumulation noise near zero);
   * fp32 weight gradient: |dw - ref| <= 1e-3 |ref| + 2e-5 max|ref|;
   * BN partial statistics / fused backward partials: 1e-4 relative after merging the row tiles.
-``test_bench_configs_covered`` runs one real benchmark step (unet_resnet50 512x512 B=16) with the
-probe on and asserts every configuration it launched appears in CASES.
+``test_bench_configs_covered`` runs one real training step of each BASELINE GPU configuration
+(unet_resnet50 512x512 B=16, attention_unet and multitask_unet 512x512 B=8) with the probe on and
+asserts every configuration it launched appears in CASES.
 Shapes follow the reference layers (model/resnet_backbone.py:35-115, model/unet_resnet.py:7-42,70-78).
 """
 import math
@@ -62,6 +63,8 @@ CASES = {
     "fwd_tn128x64_1st_ragged": ("fwd_stats", (3, 15, 17, 192, 0, 40, 1, 1), ["fwd:tn128x64_1st"]),
     "fwd_tn128x64_1st_k64": ("fwd_stats", (1, 128, 128, 64, 0, 64, 1, 1), ["fwd:tn128x64_1st"]),
     "fwd_tn64x128": ("fwd_all", (1, 64, 64, 512, 0, 128, 1, 1), ["fwd:tn64x128"]),
+    # batch 8 (attention_unet / multitask_unet, BASELINE C4 / C5): layer2 conv1 512 -> 128 at 64^2
+    "fwd_tn128x128": ("fwd_all", (8, 64, 64, 512, 0, 128, 1, 1), ["fwd:tn128x128"]),
     # generic kernel: the first conv of unet_plain / attention_unet (3 input channels padded to 8)
     "fwd_generic_cin8": ("fwd_stats", (2, 64, 64, 8, 0, 64, 3, 1), ["fwd:generic"]),
     # ---- data gradient (plain / accumulated) ----
@@ -89,6 +92,8 @@ CASES = {
     "post1_ring128x128_5st_t9": ("post1", (8, 64, 64, 128, 0, 128, 3, 1), ["dgrad_post1:ring128x128_5st_t9"]),
     "post2_halo3": ("post2", (1, 128, 128, 64, 0, 64, 3, 1), ["dgrad_post2:halo3"]),
     "post2_tn128x128_1st": ("post2", (1, 64, 64, 512, 0, 128, 1, 1), ["dgrad_post2:tn128x128_1st"]),
+    # batch 8: layer2 conv3 (128 -> 512 at 64^2), its data gradient with bn2-ReLU's backward fused
+    "post2_tn128x128": ("post2", (8, 64, 64, 128, 0, 512, 1, 1), ["dgrad_post2:tn128x128"]),
     "post2_tn64x128": ("post2", (1, 64, 64, 128, 0, 512, 1, 1), ["dgrad_post2:tn64x128"]),
     "post2_tn128x64": ("post2", (1, 32, 32, 64, 0, 512, 1, 1), ["dgrad_post2:tn128x64"]),
     "post2_tn128x64_1st_k64": ("post2", (1, 128, 128, 64, 0, 64, 1, 1), ["dgrad_post2:tn128x64_1st"]),
@@ -129,6 +134,8 @@ CASES = {
     "bnin_tn128x128_1st_k256": ("fwd_bnrelu_in", (16, 32, 32, 256, 0, 1024, 1, 1), ["fwd_bnrelu_in:tn128x128_1st"]),
     "bnin_tn256x128": ("fwd_bnrelu_in", (16, 16, 16, 512, 0, 2048, 1, 1), ["fwd_bnrelu_in:tn256x128"]),
     "bnin_tn64x128": ("fwd_bnrelu_in", (1, 16, 16, 512, 0, 2048, 1, 1), ["fwd_bnrelu_in:tn64x128"]),
+    # batch 8: layer4 conv3 (512 -> 2048 at 16^2) reading bn2-ReLU on load
+    "bnin_tn128x128": ("fwd_bnrelu_in", (8, 16, 16, 512, 0, 2048, 1, 1), ["fwd_bnrelu_in:tn128x128"]),
     "bnin_ragged": ("fwd_bnrelu_in", (1, 15, 17, 64, 0, 256, 1, 1), None),
     "bnin_wgrad_ring_r16": ("wgrad_bnrelu_in", (16, 128, 128, 64, 0, 256, 1, 1), ["wgrad_bnrelu_in:wgrad_ring128", "reduce"]),
     "bnin_wgrad_ring_r4": ("wgrad_bnrelu_in", (1, 64, 64, 128, 0, 512, 1, 1), ["wgrad_bnrelu_in:wgrad_ring128", "reduce"]),
@@ -434,27 +441,34 @@ def test_stem_bench_size(N, H):
     assert (err <= 1e-3 * dref.abs() + 2e-5 * m).all(), err.max().item()
 
 
-def test_bench_configs_covered():
-    """One real benchmark step (unet_resnet50, 512x512, B=16, bf16, Lovasz + Adam) with the probe
-    on: every kernel configuration it launches must be exercised by a case above."""
+@pytest.mark.parametrize("model_name,batch", [("unet_resnet50", 16), ("attention_unet", 8), ("multitask_unet", 8)])
+def test_bench_configs_covered(model_name, batch):
+    """One real training step of each BASELINE GPU configuration (C2/C3: unet_resnet50 512x512 B=16,
+    Lovasz + Adam; C4: attention_unet 512x512 B=8; C5: multitask_unet 512x512 B=8, BCE + CE) with the
+    probe on: every kernel configuration it launches must be exercised by a case above."""
     import contextlib
     import io
 
     from model.model_factory import create_model
     from unetseg_hip import introspect, ops
     from unetseg_hip.arena import FusedAdam
-    from unetseg_hip.losses import binary_segmentation_loss
+    from unetseg_hip.losses import binary_segmentation_loss, multitask_loss
     from utils.synthetic import make_batch
+    multitask = model_name == "multitask_unet"
     with contextlib.redirect_stdout(io.StringIO()):
-        model = create_model("unet_resnet50", num_classes=2, weights="").to(DEV).train()
+        model = create_model(model_name, num_classes=1 if multitask else 2, weights="").to(DEV).train()
     model.compute_dtype = "bf16"
     opt = FusedAdam(model, lr=1e-4)
-    x, y = make_batch(16, 512, seed=7)
-    x, y = x.to(DEV), y.to(DEV)
+    x, y, c = make_batch(batch, 512, seed=7, with_cls=True)
+    x, y, c = x.to(DEV), y.to(DEV), c.to(DEV)
     ops.PROBE = []
     try:
         opt.zero_grad()
-        loss = binary_segmentation_loss(model(x), y, "lovasz_hinge")
+        if multitask:
+            seg, cls = model(x)
+            loss = multitask_loss(seg, cls, y, c, 1.0, "bce")[0]
+        else:
+            loss = binary_segmentation_loss(model(x), y, "lovasz_hinge")
         loss.backward()
         opt.step()
         torch.cuda.synchronize()
@@ -463,7 +477,10 @@ def test_bench_configs_covered():
             used.update(introspect.call_configs(rec[5]))
     finally:
         ops.PROBE = None
+    del model, opt
+    torch.cuda.empty_cache()
     assert np.isfinite(loss.item())
+    used.discard(None)
     stem = {"stem_fwd:tn128x64", "stem_wgrad:wgrad_ring64x256"}  # test_stem_bench_size
     missing = sorted(used - covered_keys() - stem)
-    assert not missing, f"bench configurations without a parity case: {missing}"
+    assert not missing, f"{model_name} B={batch}: configurations without a parity case: {missing}"

@@ -6,6 +6,10 @@ the production path: HipModel's tape, ``ops.OVERLAP`` (weight gradients on the s
 ``param_done`` ordering, ``GradBuckets._issue`` enqueuing each bucket's AVG all-reduce on the side
 stream after it waits for the compute stream, and the fused Adam over the flat arena.
 
+Cases: unet_resnet50 fp32 64x64 B=2 (small), and the BASELINE multi-GPU steps at their per-GPU
+workload in bf16 -- unet_resnet50 512x512 B=16 (C3) and multitask_unet 512x512 B=8 (C5, whose cls
+head reports its four parameters to the buckets after the decoder's).  Two ranks at ~25 GB each.
+
 Checked: after one DP step the arena gradient on both ranks equals the mean of the two
 ranks' local (single-process) gradients, and the parameters after Adam are bitwise identical across
 ranks and equal to a single-process Adam update with that mean gradient.  Also: buffers are
@@ -29,7 +33,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, model_name, q):
+def _worker(rank, world, port, model_name, q, dtype="fp32", batch=2, size=64):
     import contextlib
     import io
     import sys
@@ -45,7 +49,7 @@ def _worker(rank, world, port, model_name, q):
         from unetseg_hip import ops
         from unetseg_hip.arena import FusedAdam
         from unetseg_hip.ddp import GradBuckets, init_from_env
-        from unetseg_hip.losses import binary_segmentation_loss
+        from unetseg_hip.losses import binary_segmentation_loss, multitask_loss
         from utils.synthetic import make_batch
 
         assert ops.OVERLAP
@@ -53,19 +57,27 @@ def _worker(rank, world, port, model_name, q):
         dev = torch.device("cuda", 0)
         torch.cuda.set_stream(torch.cuda.Stream(dev))
         with contextlib.redirect_stdout(io.StringIO()):
-            m = build_model(model_name, num_classes=2)
-        state = make_torch_state(ref_cpu.model_spec(model_name, num_classes=2))
+            kw = dict(num_classes=1) if model_name == "multitask_unet" else dict(num_classes=2)
+        m = build_model(model_name, **kw)
+        state = make_torch_state(ref_cpu.model_spec(model_name, **kw))
         if rank == 1:  # rank 1 starts from different weights and buffers: the wrap broadcasts rank 0's
             state = {k: (v + 0.25 if v.is_floating_point() else v) for k, v in state.items()}
         m.load_state_dict(state)
         m = m.to(dev).train()
-        m.compute_dtype = "fp32"
-        x, y = make_batch(2, 64, seed=1234 + 100000 * rank)
-        x, y = x.to(dev), y.to(dev)
+        m.compute_dtype = dtype
+        multitask = model_name == "multitask_unet"
+        x, y, c = make_batch(batch, size, seed=1234 + 100000 * rank, with_cls=True)
+        x, y, c = x.to(dev), y.to(dev), c.to(dev)
+        if multitask:  # a fixed per-rank dropout keep-mask: the local and the DP pass draw the same
+            m.dropout_mask = (torch.rand(batch, 512, generator=torch.Generator().manual_seed(77 + rank)) >= 0.5).float()
 
         def fwd_bwd():
             m._flat_grad.zero_()
-            loss = binary_segmentation_loss(m(x), y, "lovasz_hinge")
+            if multitask:  # seg BCE + 1.0 x CE (train.py:213-219 defaults), the bench's C5 step
+                seg, cls = m(x)
+                loss = multitask_loss(seg, cls, y, c, 1.0, "bce")[0]
+            else:
+                loss = binary_segmentation_loss(m(x), y, "lovasz_hinge")
             loss.backward()
             torch.cuda.synchronize()
             return loss.item()
@@ -112,9 +124,13 @@ def _worker(rank, world, port, model_name, q):
         sys.exit(1)
 
 
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("model_name", ["unet_resnet50"])
-def test_dp2_one_gpu_hip_model(model_name):
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("model_name,dtype,batch,size", [
+    ("unet_resnet50", "fp32", 2, 64),
+    ("unet_resnet50", "bf16", 16, 512),    # C3's per-GPU step: the bench dtype, batch and size
+    ("multitask_unet", "bf16", 8, 512),    # C5's per-GPU step (seg BCE + CE, the cls head's buckets)
+])
+def test_dp2_one_gpu_hip_model(model_name, dtype, batch, size):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import numpy as np
@@ -122,13 +138,13 @@ def test_dp2_one_gpu_hip_model(model_name):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, model_name, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, model_name, q, dtype, batch, size)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
     try:
         for _ in range(2):
-            item = q.get(timeout=240)
+            item = q.get(timeout=540)
             assert not isinstance(item[1], str), item[1]
             res[item[0]] = item[1:]
     finally:

@@ -41,8 +41,11 @@ import torch
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
-EMU_FRAC = 0.5
+EMU_FRAC = 0.45
 AMP_FACTOR = 1.5
+#: fp32 step at the benchmark size: every gradient tensor (encoder included) within this relative L2 of
+#: the oracle's fp32 run, or 4x that run's own distance from float64 where that is larger
+FP32_GRAD_REL = 2e-3
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -143,9 +146,14 @@ def test_eval_forward_512_bf16():
     assert int(flip.sum()) == 0
 
 
-def test_train_step_512_b16_bf16():
-    """train-mode fwd + Lovasz + bwd at the benchmark configuration (B=16, 512^2): logits, loss,
-    every parameter gradient and the BN running statistics"""
+@pytest.mark.parametrize("loss_name", ["lovasz_hinge", "bce"])
+def test_train_step_512_b16_bf16(loss_name):
+    """train-mode fwd + loss + bwd at the benchmark configuration (B=16, 512^2): logits, loss,
+    every parameter gradient and the BN running statistics, with the benchmark's Lovasz hinge and with
+    BCE.  BCE is smooth (no sort-order discontinuity), yet the encoder's gradients move as much under
+    bf16 storage as with Lovasz (measured: amp-vs-f32 median 1.06 for both): the ill-conditioning is
+    the BN-ResNet backward at this init, not the loss; every tensor is held at full size in fp32 by
+    test_train_step_512_b16_fp32_every_tensor."""
     from oracle import ref_cpu
     from unetseg_hip.losses import binary_segmentation_loss
     from utils.synthetic import make_batch
@@ -155,7 +163,7 @@ def test_train_step_512_b16_bf16():
     for p in m.parameters():
         p.grad = None
     out = m(x.to(DEV))
-    loss = binary_segmentation_loss(out, y.to(DEV), "lovasz_hinge")
+    loss = binary_segmentation_loss(out, y.to(DEV), loss_name)
     loss.backward()
     torch.cuda.synchronize()
     hip_out = out.detach().float()
@@ -166,7 +174,7 @@ def test_train_step_512_b16_bf16():
     for tag, kw in (("f32", {}), ("amp", dict(autocast_bf16=True)), ("emu", dict(bf16_storage=True))):
         params, buffers = _oracle(state)
         with _torch_exact():
-            l_, o_, g_ = ref_cpu.train_step("unet_resnet50", params, buffers, xd, yd, "lovasz_hinge", **kw)
+            l_, o_, g_ = ref_cpu.train_step("unet_resnet50", params, buffers, xd, yd, loss_name, **kw)
         runs[tag] = (l_.item(), o_.float(), g_, buffers)
         torch.cuda.empty_cache()
     f32 = runs["f32"]
@@ -221,6 +229,9 @@ def test_train_step_512_b16_bf16():
             assert rh <= AMP_FACTOR * ra + 1e-3, (k, rh, ra)
     print(f"well-conditioned gradient tensors checked individually: {well}")
     assert well >= 10
+    worst = sorted(((hip_grads[k].double() - v.double()).norm().item() / max(v.double().norm().item(), 1e-30), k)
+                   for k, v in runs["emu"][2].items() if v.double().norm().item() > 0)
+    print("hip-emu per tensor, worst 4: " + ", ".join(f"{k} {r:.3e}" for r, k in worst[-4:]))
     # BN running statistics after the step (bn_finalize over 16 x H x W pixels per channel)
     for k, v in runs["emu"][3].items():
         if k.endswith(("running_mean", "running_var")):
@@ -228,3 +239,67 @@ def test_train_step_512_b16_bf16():
             assert (hb - v.double()).abs().max().item() <= 2e-2 * v.double().abs().max().item() + 1e-4, k
         elif k.endswith("num_batches_tracked"):
             assert int(hip_bufs[k]) == int(v)
+
+
+def test_train_step_512_b16_fp32_every_tensor():
+    """The HIP path in fp32 (compute_dtype="fp32": the same op graph, fused BN / ReLU backward
+    epilogues, side-stream weight gradients, fused Lovasz) at the benchmark size, B=16, 512^2, against
+    the oracle's fp32 and float64 runs in torch on the GPU: EVERY gradient tensor, the encoder's
+    included, within FP32_GRAD_REL relative L2 of the fp32 oracle (or 4x the fp32 oracle's own
+    distance from float64, where the problem's conditioning makes that larger); logits within 1e-3
+    (north_star); loss 1e-5 relative; running statistics 1e-4.  The bf16 product kernels of every
+    configuration this step runs are held per launch in tests/test_gpu_configs.py."""
+    from oracle import ref_cpu
+    from unetseg_hip.losses import binary_segmentation_loss
+    from utils.synthetic import make_batch
+    x, y = make_batch(16, 512, seed=37)
+    xd, yd = x.to(DEV), y.to(DEV)
+    state = _state()
+    m = _hip_model(state, train=True)
+    m.compute_dtype = "fp32"
+    for p in m.parameters():
+        p.grad = None
+    out = m(xd)
+    loss = binary_segmentation_loss(out, yd, "lovasz_hinge")
+    loss.backward()
+    torch.cuda.synchronize()
+    hip_out = out.detach().float()
+    hip_grads = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+    hip_bufs = {k: b.detach().clone() for k, b in m.named_buffers()}
+    hip_loss = loss.item()
+    del m, out, loss
+    torch.cuda.empty_cache()
+    runs = {}
+    for tag, dt in (("f32", torch.float32), ("f64", torch.float64)):
+        params, buffers = _oracle(state)
+        params = {k: v.detach().to(dt).requires_grad_(True) for k, v in params.items()}
+        buffers = {k: (v.to(dt) if v.is_floating_point() else v) for k, v in buffers.items()}
+        with _torch_exact():
+            l_, o_, g_ = ref_cpu.train_step("unet_resnet50", params, buffers, xd.to(dt), yd, "lovasz_hinge")
+        runs[tag] = (l_.item(), o_, g_, buffers)
+        del params
+        torch.cuda.empty_cache()
+    f32, f64 = runs["f32"], runs["f64"]
+    e_out = (hip_out.double() - f32[1].double()).abs().max().item()
+    rows = []
+    for k, v in f32[2].items():
+        n = v.double().norm().item()
+        if n == 0:
+            continue
+        r_hip = (hip_grads[k].double() - v.double()).norm().item() / n
+        n64 = f64[2][k].norm().item()
+        r_ref = (v.double() - f64[2][k]).norm().item() / max(n64, 1e-300)
+        rows.append((r_hip, r_ref, k))
+    rows.sort()
+    print(f"\nfp32 512 B=16: max|logit| {f32[1].abs().max().item():.3f} hip-f32 max|d| {e_out:.3e} "
+          f"loss hip {hip_loss:.7f} f32 {f32[0]:.7f} f64 {f64[0]:.7f}")
+    print(f"grad rel L2 hip-f32: median {rows[len(rows) // 2][0]:.3e} max {rows[-1][0]:.3e} ({rows[-1][2]}); "
+          f"f32-f64 max {max(r[1] for r in rows):.3e}")
+    assert e_out < 1e-3, e_out
+    assert abs(hip_loss - f32[0]) <= 1e-5 * abs(f32[0]) + 1e-6
+    bad = [(k, rh, rr) for rh, rr, k in rows if rh > max(FP32_GRAD_REL, 4 * rr)]
+    assert not bad, bad[:8]
+    for k, v in f32[3].items():
+        if k.endswith(("running_mean", "running_var")):
+            hb, vb = hip_bufs[k].double(), v.double()
+            assert (hb - vb).abs().max().item() <= 1e-4 * vb.abs().max().item() + 1e-6, k

@@ -8,18 +8,27 @@ Here the split is at the pixel work:
     image / mask with PIL exactly as the reference (``.convert("RGB")`` / ``.convert("L")``) and
     draws the augmentation parameters with ``np.random`` in the reference's order
     (hf_dataloader.py:135-166), so a seeded run makes the same draws.  It returns a ``RawSample``.
-  * ``hf_unet_dataset_collate`` packs a list of ``RawSample`` into one ``RawBatch``: the uint8
-    pixels back to back plus the per-sample descriptors and tables (utils/augment_tables.py).
+  * ``hf_unet_dataset_collate(batch)`` -- the reference's one-argument collate_fn -- packs a list of
+    ``RawSample`` (each carries its dataset's input_shape / num_classes / task) into one ``RawBatch``:
+    the uint8 pixels back to back plus the per-sample descriptors and tables
+    (utils/augment_tables.py).
   * ``RawBatch.to_device`` (main process) uploads the bytes and runs ``unetseg_augment_batch``
     (csrc/augment.hip): resize, flip, paste, HSV jitter, /255, label handling and one-hot for the
     whole batch, writing the collated ``(images, pngs, seg_labels[, cls_labels])`` the reference's
-    collate returns, already on the GPU.  ``DeviceLoader`` wraps a DataLoader and does this one
-    batch ahead on a side stream.
+    collate returns, already on the GPU.  A ``RawBatch`` also unpacks like the reference's tuple
+    (``imgs, pngs, labels = batch``: the device path runs on first access, and ``.to(device)`` on
+    the results is then a no-op), so a reference training loop over
+    ``DataLoader(ds, collate_fn=hf_unet_dataset_collate, pin_memory=True)`` runs unchanged.
+    ``DeviceLoader`` wraps a DataLoader and does the device work one batch ahead on a side stream.
+  * ``ds[i]`` is a ``RawSample``; unpacking it (``jpg, png, seg_labels = ds[i]``) gives the
+    reference's item as numpy (one-sample device batch), as does ``ds.get(i)``.
 The geometric part is bit-exact with Pillow; the HSV jitter follows OpenCV's 8-bit algorithm
 (parity unpinned: cv2 is not installed here, see oracle/augment_ref.py).
 
 Dataset layout (convert_and_upload.py:60-90): ``{data_dir}/{config}/{split}/data.parquet`` with
-columns image / mask (HF Image structs: bytes + path), label, filename, subset.
+columns image / mask (HF Image structs: bytes + path), label, filename, subset.  The parquet files are
+memory-mapped Arrow tables (as ``datasets.load_dataset`` keeps them); a row is materialised only in
+``__getitem__``, so forked DataLoader workers share the mapping instead of copying Python objects.
 """
 from __future__ import annotations
 
@@ -73,7 +82,9 @@ def _open_image(cell, base_dir):
 
 @dataclass
 class RawSample:
-    """one decoded sample and its drawn augmentation (picklable: crosses DataLoader workers)"""
+    """one decoded sample and its drawn augmentation (picklable: crosses DataLoader workers), with the
+    dataset settings the one-argument collate needs.  Unpacks as the reference's item
+    ``(jpg, png, seg_labels[, cls_label])`` (numpy, through a one-sample device batch)."""
     image: np.ndarray  # uint8 [ih][iw][3]
     mask: np.ndarray  # uint8 [mh][mw]
     nw: int
@@ -83,6 +94,22 @@ class RawSample:
     flip: bool
     r: np.ndarray | None  # HSV factors (training) or None (validation letterbox)
     cls_label: int | None = None
+    input_shape: tuple | None = None
+    num_classes: int | None = None
+    task: str = "multiclass"
+
+    def reference_item(self, device="cuda"):
+        """hf_dataloader.py:67-105's return value: jpg fp32 [3,H,W], png int64 [H,W], seg_labels fp32
+        [H,W,C+1] (numpy) [, cls_label int]"""
+        if self.input_shape is None:
+            raise TypeError("RawSample without dataset settings (input_shape / num_classes / task)")
+        out = pack_batch([self], self.input_shape, self.num_classes, self.task).to_device(device)
+        torch.cuda.synchronize()
+        vals = [t[0].cpu().numpy() for t in out[:3]]
+        return (*vals, int(out[3][0])) if len(out) == 4 else tuple(vals)
+
+    def __iter__(self):
+        return iter(self.reference_item())
 
 
 class HFUnetDataset(torch.utils.data.Dataset):
@@ -101,20 +128,35 @@ class HFUnetDataset(torch.utils.data.Dataset):
         self.return_cls_label = return_cls_label
         self.files = find_split_files(data_dir, config, split)
         self.base_dir = os.path.join(data_dir, config)
-        tables = [pq.read_table(f) for f in self.files]
-        cols = set(tables[0].column_names)
-        missing = {"image", "mask"} - cols
-        if missing:
-            raise ValueError(f"{self.files[0]}: missing columns {sorted(missing)}")
-        self.images, self.masks, self.labels = [], [], []
-        for t in tables:
-            self.images += t.column("image").to_pylist()
-            self.masks += t.column("mask").to_pylist()
-            self.labels += t.column("label").to_pylist() if "label" in cols else ["unknown"] * t.num_rows
-        self.length = len(self.images)
+        # memory-mapped Arrow tables (only the columns read); rows are decoded on access
+        self._tables = []
+        for f in self.files:
+            names = pq.read_schema(f).names
+            missing = {"image", "mask"} - set(names)
+            if missing:
+                raise ValueError(f"{f}: missing columns {sorted(missing)}")
+            cols = [c for c in ("image", "mask", "label") if c in names]
+            self._tables.append(pq.read_table(f, columns=cols, memory_map=True))
+        self._starts = np.cumsum([0] + [t.num_rows for t in self._tables])
+        self.length = int(self._starts[-1])
 
     def __len__(self):
         return self.length
+
+    def _row(self, index):
+        """(table, row) of a global index (negative indices as a list)"""
+        if index < 0:
+            index += self.length
+        if not 0 <= index < self.length:
+            raise IndexError(index)
+        k = int(np.searchsorted(self._starts, index, side="right")) - 1
+        return self._tables[k], int(index - self._starts[k])
+
+    def _cell(self, column, index):
+        t, r = self._row(index)
+        if column not in t.column_names:
+            return None
+        return t.column(column)[r].as_py()
 
     @staticmethod
     def rand(a=0, b=1):
@@ -146,27 +188,26 @@ class HFUnetDataset(torch.utils.data.Dataset):
 
     def cls_label_of(self, index):
         """hf_dataloader.py:94-103"""
-        name = self.labels[index] or "unknown"
+        name = self._cell("label", index) or "unknown"
         for cname, idx in self.CLASS_TO_IDX.items():
             if name.startswith(cname):
                 return idx
         return 0
 
     def __getitem__(self, index) -> RawSample:
-        jpg = _open_image(self.images[index], self.base_dir).convert("RGB")
-        png = _open_image(self.masks[index], self.base_dir).convert("L")
+        jpg = _open_image(self._cell("image", index), self.base_dir).convert("RGB")
+        png = _open_image(self._cell("mask", index), self.base_dir).convert("L")
         iw, ih = jpg.size
         p = self.draw(iw, ih, random=self.augmentation)
         return RawSample(image=np.asarray(jpg, np.uint8), mask=np.asarray(png, np.uint8),
-                         cls_label=self.cls_label_of(index) if self.return_cls_label else None, **p)
+                         cls_label=self.cls_label_of(index) if self.return_cls_label else None,
+                         input_shape=tuple(int(v) for v in self.input_shape), num_classes=int(self.num_classes),
+                         task=self.task, **p)
 
     def get(self, index, device="cuda"):
         """the reference's item (jpg fp32 [3,H,W], png int64 [H,W], seg_labels fp32 [H,W,C+1][, cls]) as
         numpy, produced through the device path (one-sample batch)"""
-        out = hf_unet_dataset_collate([self[index]], self.input_shape, self.num_classes, self.task).to_device(device)
-        torch.cuda.synchronize()
-        vals = [t[0].cpu().numpy() for t in out[:3]]
-        return (*vals, int(out[3][0])) if len(out) == 4 else tuple(vals)
+        return self[index].reference_item(device)
 
 
 @dataclass
@@ -183,8 +224,10 @@ class RawBatch:
     binary: bool
     cls_labels: np.ndarray | None = None
     pinned: dict = field(default_factory=dict)
+    _tensors: tuple | None = None
 
-    def __len__(self):
+    @property
+    def batch_size(self):
         return self.desc.shape[0]
 
     def pin(self):
@@ -193,6 +236,27 @@ class RawBatch:
             for k in ("src", "msk", "tables", "desc"):
                 self.pinned[k] = torch.from_numpy(getattr(self, k)).pin_memory()
         return self
+
+    def pin_memory(self, device=None):
+        """DataLoader(pin_memory=True) calls this on every batch (torch.utils.data._utils.pin_memory)"""
+        return self.pin()
+
+    # -- the reference collate's tuple (hf_dataloader.py:205-213): (images, pngs, seg_labels[, cls]) --
+    def tensors(self, device=None):
+        """the collated tensors on `device` (default: the current HIP device); computed once"""
+        if self._tensors is None:
+            dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+            self._tensors = self.to_device(dev)
+        return self._tensors
+
+    def __len__(self):
+        return 4 if self.cls_labels is not None else 3
+
+    def __iter__(self):
+        return iter(self.tensors())
+
+    def __getitem__(self, i):
+        return self.tensors()[i]
 
     def to_device(self, device="cuda", stream=None, onehot=True):
         """run the device augmentation; returns (images, pngs, seg_labels[, cls_labels]) on `device`"""
@@ -203,7 +267,7 @@ class RawBatch:
             raise RuntimeError("the device augmentation needs a GPU (no CPU fallback)")
         stream = stream or torch.cuda.current_stream(device)
         self.pin()
-        B = len(self)
+        B = self.batch_size
         H, W = int(self.input_shape[0]), int(self.input_shape[1])
         with torch.cuda.stream(stream):
             dev = {k: v.to(device, non_blocking=True) for k, v in self.pinned.items()}
@@ -228,8 +292,14 @@ class RawBatch:
         return out
 
 
-def pack_batch(samples, input_shape, num_classes, task="multiclass"):
-    """list[RawSample] -> RawBatch (descriptors + tables per utils/augment_tables.py)"""
+def pack_batch(samples, input_shape=None, num_classes=None, task=None):
+    """list[RawSample] -> RawBatch (descriptors + tables per utils/augment_tables.py).  The settings
+    default to the ones the samples carry (HFUnetDataset.__getitem__)."""
+    if samples and input_shape is None:
+        input_shape, num_classes, task = samples[0].input_shape, samples[0].num_classes, task or samples[0].task
+    if input_shape is None or num_classes is None:
+        raise TypeError("pack_batch needs input_shape / num_classes (or samples that carry them)")
+    task = task or "multiclass"
     B = len(samples)
     desc = np.zeros((B, AUG_DESC), np.int64)
     srcs, msks, tabs = [], [], []
@@ -278,13 +348,11 @@ class _Collate:
         return pack_batch(batch, *self.args)
 
 
-def hf_unet_dataset_collate(batch, input_shape=None, num_classes=None, task="multiclass"):
-    """hf_dataloader.py:183-213.  With a dataset's settings: ``hf_unet_dataset_collate(batch, ...)``
-    or ``make_collate(dataset)`` as the DataLoader's collate_fn.  Returns a RawBatch; the tensors the
-    reference's collate returns come from ``RawBatch.to_device`` / ``DeviceLoader``."""
-    if input_shape is None:
-        raise TypeError("hf_unet_dataset_collate needs the dataset's input_shape / num_classes / task here: "
-                        "use make_collate(dataset) as the DataLoader's collate_fn")
+def hf_unet_dataset_collate(batch, input_shape=None, num_classes=None, task=None):
+    """hf_dataloader.py:183-213, the reference's one-argument collate_fn: the settings come from the
+    samples (HFUnetDataset stores them in each RawSample) unless given.  Returns a RawBatch, which
+    unpacks as the reference's ``(images, pngs, seg_labels[, cls_labels])`` on the current HIP device
+    (``RawBatch.tensors``), or feeds ``DeviceLoader`` / ``RawBatch.to_device``."""
     return pack_batch(batch, input_shape, num_classes, task)
 
 
@@ -294,7 +362,9 @@ def make_collate(dataset: HFUnetDataset):
 
 class DeviceLoader:
     """iterate a DataLoader of RawBatch as the reference's collated tensors on `device`; batch i+1 is
-    uploaded and augmented on a side stream while the caller computes on batch i"""
+    uploaded and augmented on a side stream while the caller computes on batch i.  onehot=False skips
+    the fp32 one-hot seg_labels (B x H x W x (C+1): 50 MB at 512^2, B=16, C=2) and yields None in its
+    slot -- the binary and multitask loops never read it (utils/train_and_eval.py:203-207)."""
 
     def __init__(self, loader, device="cuda", onehot=True):
         self.loader, self.device, self.onehot = loader, torch.device(device), onehot
