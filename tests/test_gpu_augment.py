@@ -133,6 +133,9 @@ def test_train_val_on_parquet(tmp_path, task, model, loss):
     summ = json.load(open(os.path.join(exp, "summary.json")))
     assert len(summ["train_losses"]) == 2 and all(v == v and v > 0 for v in summ["train_losses"])
     assert summ["test_metrics"] is not None
+    if task == "binary":  # --export-vis (default on, train.py:580-585): 2x2 grids of the test split
+        grids = sorted(f for f in os.listdir(os.path.join(exp, "vis")) if f.endswith("_grid.png"))
+        assert len(grids) == 2 and Image.open(os.path.join(exp, "vis", grids[0])).size == (128, 128)
     vloss = [] if task == "multiclass" else ["--loss", loss if loss != "ce" else "bce"]
     m = val.val(val.parse_args(common + vloss + ["--weights", os.path.join(exp, "weights", "best.pth")]))
     key = "Mean IoU" if task == "multiclass" else "IoU"

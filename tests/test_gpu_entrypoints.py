@@ -40,7 +40,7 @@ def test_train_and_val_entrypoints(tmp_path, task, model, loss):
     hist = json.load(open(os.path.join(exp, "val_metrics_history.json")))
     assert len(hist) == 2 and 0.0 <= hist[-1]["IoU"] <= 1.0
     vargs = val.parse_args(["--weights", os.path.join(exp, "weights", "best.pth"), "--task", task, "--model", model,
-                            "--input-size", "64", "--synthetic-test", "2"])
+                            "--input-size", "64", "--data-path", "synthetic", "--synthetic-test", "2"])
     m = val.val(vargs)
     assert 0.0 <= m["IoU"] <= 1.0
 

@@ -14,6 +14,26 @@ def test_train_cli_defaults_match_reference():
     assert train.parse_args(["--pos-weight", ""]).pos_weight is None
 
 
+def test_val_cli_defaults_match_reference():
+    """val.py:158-187: every flag of the reference with its default (ce / focal accepted by --loss)"""
+    import val
+
+    a = val.parse_args([])
+    assert (a.data_path, a.data_config, a.weights, a.task, a.model, a.loss) == (
+        "./hf_datasets/merged_dataset_v2", "no-ai", "weights/unet_resnet_voc.pth", "binary", "unet_resnet50",
+        "lovasz_hinge")
+    assert (a.num_classes, a.input_size, a.cache_dir, a.device) == (4, 512, ".hf-cache/datasets", "cuda")
+    for loss in ("bce", "lovasz_hinge", "ce", "focal"):
+        assert val.parse_args(["--loss", loss]).loss == loss
+
+
+def test_train_export_vis_default_matches_reference():
+    import train
+
+    assert train.parse_args([]).export_vis is True  # train.py:580-585
+    assert train.parse_args(["--no-export-vis"]).export_vis is False
+
+
 def test_optimizer_and_schedule_match_reference():
     """get_optimizer_and_lr: lr clamps to 1e-4 for any batch size; warm-cos epoch 0 = 1e-5."""
     import train

@@ -26,6 +26,13 @@ void unetseg_set_error(const char* fmt, ...);
     }                                      \
   } while (0)
 
+// shared argument checks of the C ABI's launching entry points (exercised by tests/asan/cabi_asan.cpp)
+#define US_CHECK_DTYPE(dt, name) \
+  US_CHECK_ARG((dt) == DT_F32 || (dt) == DT_BF16, "%s: bad dtype %d (0 = fp32, 1 = bf16)", name, (int)(dt))
+#define US_CHECK_CONV_GEOM(name, n, h, w, r, s, stride, pad)                                                   \
+  US_CHECK_ARG((n) >= 0 && (h) >= 0 && (w) >= 0 && (r) >= 1 && (s) >= 1 && (stride) >= 1 && (pad) >= 0,       \
+               "%s: bad geometry n=%d h=%d w=%d r=%d s=%d stride=%d pad=%d", name, n, h, w, r, s, stride, pad)
+
 #define US_LAUNCH_CHECK(name)                                                        \
   do {                                                                               \
     hipError_t _e = hipGetLastError();                                               \

@@ -861,6 +861,8 @@ UNETSEG_API int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, 
                                    int pad, const float* bias, int relu, void* y, int ldy, float* stats,
                                    void* stream) {
   US_CHECK_ARG(x1 && wk && y, "conv2d_fwd: null pointer");
+  US_CHECK_CONV_GEOM("conv2d_fwd", n, h, w, r, s, stride, pad);
+  US_CHECK_ARG(cout > 0 && ldc1 >= c1 && (c2 == 0 || ldc2 >= c2), "conv2d_fwd: pixel strides below the channel counts");
   US_CHECK_ARG((c1 + c2) % 8 == 0 && c1 % 8 == 0, "conv2d_fwd: channels must be multiples of 8 (c1=%d c2=%d)", c1, c2);
   US_CHECK_ARG(c2 == 0 || x2, "conv2d_fwd: c2>0 needs x2");
   US_CHECK_ARG(ldc1 % 8 == 0 && (c2 == 0 || ldc2 % 8 == 0) && ldy >= cout, "conv2d_fwd: bad strides");
@@ -981,6 +983,9 @@ UNETSEG_API int unetseg_conv2d_fwd_affine(int dtype, const void* x1, int c1, int
                                           int stride, int pad, const float* escale, const float* bias, int relu,
                                           void* y, int ldy, void* stream) {
   US_CHECK_ARG(x1 && wk && y && escale && bias, "conv2d_fwd_affine: null pointer");
+  US_CHECK_DTYPE(dtype, "conv2d_fwd_affine");
+  US_CHECK_CONV_GEOM("conv2d_fwd_affine", n, h, w, r, s, stride, pad);
+  US_CHECK_ARG(cout > 0 && ldc1 >= c1 && (c2 == 0 || ldc2 >= c2) && ldy >= cout, "conv2d_fwd_affine: bad strides");
   US_CHECK_ARG((c1 + c2) % 8 == 0 && c1 % 8 == 0, "conv2d_fwd_affine: channels must be multiples of 8");
   US_CHECK_ARG(c2 == 0 || x2, "conv2d_fwd_affine: c2>0 needs x2");
   US_CHECK_ARG(ldc1 % 8 == 0 && (c2 == 0 || ldc2 % 8 == 0) && ldy >= cout, "conv2d_fwd_affine: bad strides");
@@ -1016,6 +1021,9 @@ UNETSEG_API int unetseg_conv2d_dgrad(int dtype, const void* dy, int ldy, int n, 
                                      int cout, int cin, int r, int s, int stride, int pad, void* dx, int ldx,
                                      int h, int w, int accumulate, void* stream) {
   US_CHECK_ARG(dy && wt && dx, "conv2d_dgrad: null pointer");
+  US_CHECK_DTYPE(dtype, "conv2d_dgrad");
+  US_CHECK_CONV_GEOM("conv2d_dgrad", n, h, w, r, s, stride, pad);
+  US_CHECK_ARG(cin > 0 && cout > 0 && ldy >= cout && ldx >= cin, "conv2d_dgrad: bad channel counts / strides");
   US_CHECK_ARG(cout % 8 == 0 && ldy % 8 == 0, "conv2d_dgrad: cout/ldy must be multiples of 8");
   US_CHECK_ARG(stride == 1 || stride == 2, "conv2d_dgrad: stride must be 1 or 2");
   US_CHECK_ARG(p == (h + 2 * pad - r) / stride + 1 && q == (w + 2 * pad - s) / stride + 1, "conv2d_dgrad: shape mismatch");
@@ -1236,6 +1244,10 @@ UNETSEG_API int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1
                                      int stride, int pad, float* ws, size_t ws_bytes, float* dw, int dw_c,
                                      int accumulate, void* stream) {
   US_CHECK_ARG(x1 && dy && ws && dw, "conv2d_wgrad: null pointer");
+  US_CHECK_DTYPE(dtype, "conv2d_wgrad");
+  US_CHECK_CONV_GEOM("conv2d_wgrad", n, h, w, r, s, stride, pad);
+  US_CHECK_ARG(cout > 0 && ldc1 >= c1 && (c2 == 0 || ldc2 >= c2) && ldy >= cout && dw_c >= c1 + c2,
+               "conv2d_wgrad: bad channel counts / strides");
   US_CHECK_ARG((c1 + c2) % 8 == 0 && c1 % 8 == 0 && cout % 8 == 0 && ldy % 8 == 0, "conv2d_wgrad: channel counts must be multiples of 8");
   const int p = (h + 2 * pad - r) / stride + 1, q = (w + 2 * pad - s) / stride + 1;
   const int bkw = dtype == DT_BF16 ? 32 : 16;

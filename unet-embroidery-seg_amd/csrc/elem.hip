@@ -1282,8 +1282,12 @@ inline int pow2_le(int v, int cap) {
     }                                     \
   } while (0)
 
-#define CHECK_VEC(dtype, C, name) \
-  US_CHECK_ARG((C) % ((dtype) == DT_BF16 ? 8 : 4) == 0, "%s: channels (%d) must be a multiple of the 16-B vector", name, (int)(C))
+#define CHECK_VEC(dtype, C, name)                                                                               \
+  do {                                                                                                          \
+    US_CHECK_DTYPE(dtype, name);                                                                                \
+    US_CHECK_ARG((C) > 0 && (C) % ((dtype) == DT_BF16 ? 8 : 4) == 0,                                            \
+                 "%s: channels (%d) must be a positive multiple of the 16-B vector", name, (int)(C));           \
+  } while (0)
 
 UNETSEG_API int unetseg_bn_finalize(const float* part, int C, int G, long M, int tile, const float* gamma,
                                     const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
@@ -1316,6 +1320,10 @@ UNETSEG_API int unetseg_bn_apply(int dtype, const void* y, int ldy, const float*
                                  int ldr, const float* sc2, const float* sh2, int res_mode, int relu, void* out,
                                  int ldo, long M, int C, void* stream) {
   CHECK_VEC(dtype, C, "bn_apply");
+  US_CHECK_ARG(y && sc && sh && out && M >= 0, "bn_apply: null pointer or negative M");
+  US_CHECK_ARG(res_mode >= 0 && res_mode <= 2, "bn_apply: res_mode %d (0 none, 1 identity, 2 BN'd residual)", res_mode);
+  US_CHECK_ARG(res_mode == 0 || r, "bn_apply: res_mode %d needs the residual", res_mode);
+  US_CHECK_ARG(res_mode != 2 || (sc2 && sh2), "bn_apply: res_mode 2 needs the residual's BN coefficients");
   DISPATCH_T(dtype, hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(M * C / VE<T>)), dim3(256), 0,
                                        (hipStream_t)stream, (const T*)y, ldy, sc, sh, (const T*)r, ldr, sc2, sh2,
                                        res_mode, relu, (T*)out, ldo, M, C, nullptr));
@@ -1338,6 +1346,10 @@ UNETSEG_API int unetseg_bn_apply_mask(int dtype, const void* y, int ldy, const f
 // geometry of the channel-reduction kernels (also used by the host to size partial buffers)
 UNETSEG_API int unetseg_reduce_tiles(int dtype, long M, int C, int* tv_out, int* ppb_out) {
   const int V = dtype == DT_BF16 ? 8 : 4;
+  if (C <= 0 || C % V != 0 || M < 0) {  // no 16-B channel vectors: no reduction geometry (host ASan driver)
+    unetseg_set_error("reduce_tiles: C=%d must be a positive multiple of %d", C, V);
+    return -1;
+  }
   const int cv = C / V;
   const int tv = pow2_le(cv, 64);
   const int rows = 256 / tv;
@@ -1361,6 +1373,7 @@ UNETSEG_API int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const 
                                       const float* inv1, const void* y2, int ld2, const float* mean2,
                                       const float* inv2, long M, int C, float* part, int G, void* stream) {
   CHECK_VEC(dtype, C, "bn_bwd_reduce");
+  US_CHECK_ARG(dA && y1 && mean1 && inv1 && part && M >= 0, "bn_bwd_reduce: null pointer or negative M");
   int tv, ppb;
   const int g = unetseg_reduce_tiles(dtype, M, C, &tv, &ppb);
   US_CHECK_ARG(g == G, "bn_bwd_reduce: G mismatch (%d vs %d)", G, g);
@@ -1392,6 +1405,9 @@ UNETSEG_API int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const 
 UNETSEG_API int unetseg_bn_bwd_finalize(const float* part, int C, int G, long M, int nbranch, const float* g1,
                                         const float* inv1, float* dg1, float* db1, const float* g2, const float* inv2,
                                         float* dg2, float* db2, float* coef, void* stream) {
+  US_CHECK_ARG(nbranch == 1 || nbranch == 2, "bn_bwd_finalize: nbranch %d must be 1 or 2", nbranch);
+  US_CHECK_ARG(part && g1 && inv1 && coef && C > 0 && G > 0 && M > 0, "bn_bwd_finalize: bad args");
+  US_CHECK_ARG(nbranch == 1 || (g2 && inv2), "bn_bwd_finalize: the second branch needs its gamma / invstd");
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, C, G, M, nbranch, g1,
                      inv1, dg1, db1, g2, inv2, dg2, db2, coef);
   US_LAUNCH_CHECK("bn_bwd_finalize");
@@ -1480,6 +1496,9 @@ UNETSEG_API int unetseg_maxpool_fwd(int dtype, const void* x, int ldx, int n, in
                                     int ceil_mode, void* y, int ldy, uint8_t* idx, int* p_out, int* q_out,
                                     void* stream) {
   CHECK_VEC(dtype, c, "maxpool_fwd");
+  US_CHECK_ARG(x && y && idx, "maxpool_fwd: null pointer");
+  US_CHECK_ARG(k >= 1 && k <= 16 && s >= 1 && n >= 0 && h >= k && w >= k, "maxpool_fwd: bad window k=%d s=%d on %dx%d", k,
+               s, h, w);
   int p = ceil_mode ? (h - k + s - 1) / s + 1 : (h - k) / s + 1;
   int q = ceil_mode ? (w - k + s - 1) / s + 1 : (w - k) / s + 1;
   if (ceil_mode) {  // last window must start inside the input (ATen pooling_output_shape)
@@ -1500,6 +1519,7 @@ UNETSEG_API int unetseg_maxpool_bwd(int dtype, const void* dy, int ldy, const ui
                                     int c, int k, int s, int p, int q, void* dx, int ldx, int accumulate,
                                     void* stream) {
   CHECK_VEC(dtype, c, "maxpool_bwd");
+  US_CHECK_ARG(dy && idx && dx && k >= 1 && s >= 1 && n >= 0 && h >= 0 && w >= 0, "maxpool_bwd: bad args");
   DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for((long)n * h * w * c / VE<T>)), dim3(256),
                                        0, (hipStream_t)stream, (const T*)dy, ldy, idx, n, h, w, c, k, s, p, q, (T*)dx,
                                        ldx, accumulate));
@@ -1510,6 +1530,7 @@ UNETSEG_API int unetseg_maxpool_bwd(int dtype, const void* dy, int ldy, const ui
 UNETSEG_API int unetseg_upsample2x_fwd(int dtype, const void* x, int ldx, int n, int h, int w, int c,
                                        int align_corners, void* y, int ldy, void* stream) {
   CHECK_VEC(dtype, c, "upsample_fwd");
+  US_CHECK_ARG(x && y && n >= 0 && h >= 0 && w >= 0, "upsample_fwd: null pointer or negative size");
   DISPATCH_T(dtype, hipLaunchKernelGGL(upsample_fwd_kernel<T>,
                                        dim3(ceil_div(2 * w * (c / VE<T>), 256), ceil_div(n * 2 * h, up_rows_pb())),
                                        dim3(256), 0, (hipStream_t)stream, (const T*)x, ldx, n, h, w, c, align_corners,
@@ -1521,6 +1542,7 @@ UNETSEG_API int unetseg_upsample2x_fwd(int dtype, const void* x, int ldx, int n,
 UNETSEG_API int unetseg_upsample2x_bwd(int dtype, const void* dy, int ldy, int n, int h, int w, int c,
                                        int align_corners, void* dx, int ldx, int accumulate, void* stream) {
   CHECK_VEC(dtype, c, "upsample_bwd");
+  US_CHECK_ARG(dy && dx && n >= 0 && h >= 0 && w >= 0, "upsample_bwd: null pointer or negative size");
 #define UP_BWD(R)                                                                                            \
   hipLaunchKernelGGL((upsample_bwd_kernel<T, R>), dim3(ceil_div(w * (c / VE<T>), 256), ceil_div(n * h, R)), dim3(256), \
                      0, (hipStream_t)stream, (const T*)dy, ldy, n, h, w, c, align_corners, (T*)dx, ldx, accumulate)
@@ -1558,7 +1580,9 @@ UNETSEG_API int unetseg_upsample2x_bwd_relu(int dtype, const void* dy, int ldy, 
 
 UNETSEG_API int unetseg_pack_input(int dtype, const float* x, int n, int c, int h, int w, int cpad, void* y,
                                    void* stream) {
-  US_CHECK_ARG(cpad >= c, "pack_input: cpad < c");
+  US_CHECK_DTYPE(dtype, "pack_input");
+  US_CHECK_ARG(x && y, "pack_input: null pointer");
+  US_CHECK_ARG(cpad >= c && c > 0 && n >= 0 && h >= 0 && w >= 0, "pack_input: bad sizes (c=%d cpad=%d)", c, cpad);
   DISPATCH_T(dtype, hipLaunchKernelGGL(pack_input_kernel<T>, dim3(grid_for((long)n * h * w)), dim3(256), 0,
                                        (hipStream_t)stream, x, n, c, h, w, cpad, (T*)y));
   US_LAUNCH_CHECK("pack_input");
@@ -1714,6 +1738,7 @@ UNETSEG_API int unetseg_attn_bwd2(int dtype, const float* dpsibn, const float* p
 
 UNETSEG_API int unetseg_add(int dtype, const void* x, int ldx, void* out, int ldo, long M, int c, void* stream) {
   CHECK_VEC(dtype, c, "add");
+  US_CHECK_ARG(x && out && M >= 0 && ldx >= c && ldo >= c, "add: bad args");
   DISPATCH_T(dtype, hipLaunchKernelGGL(add_kernel<T>, dim3(grid_for(M * c / VE<T>)), dim3(256), 0, (hipStream_t)stream,
                                        (const T*)x, ldx, (T*)out, ldo, M, c));
   US_LAUNCH_CHECK("add");

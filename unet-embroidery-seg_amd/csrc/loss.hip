@@ -652,6 +652,9 @@ UNETSEG_API size_t unetseg_bce_workspace(int B, long P) { return (size_t)grid_fo
 // BCE-with-logits mean loss; gz (may be NULL) = dloss/dz (already /count); pos_weight fp32 scalar or NULL
 UNETSEG_API int unetseg_bce_fwd(const float* out, int nch, const int64_t* tgt, int B, long P, const float* pos_weight,
                                 void* ws, size_t ws_bytes, float* gz, float* loss, void* stream) {
+  US_CHECK_ARG(out && tgt && ws && gz && loss, "bce_fwd: null pointer");
+  US_CHECK_ARG(nch == 1 || nch == 2, "bce_fwd: nch %d must be 1 or 2", nch);
+  US_CHECK_ARG(B > 0 && P > 0, "bce_fwd: empty batch");
   US_CHECK_ARG(ws_bytes >= unetseg_bce_workspace(B, P), "bce_fwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   const int G = grid_for((long)B * P);
@@ -684,6 +687,7 @@ UNETSEG_API int unetseg_confusion(const float* out, int nch, const int64_t* tgt,
 
 UNETSEG_API int unetseg_adam(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
                              float eps, float wd, int step, const float* grad_scale, void* stream) {
+  US_CHECK_ARG(p && g && m && v && n >= 0, "adam: null pointer or negative size");
   US_CHECK_ARG(step >= 1, "adam: step must be >= 1");
   const double bc1 = 1.0 - pow((double)beta1, step);
   const double bc2 = 1.0 - pow((double)beta2, step);
@@ -705,6 +709,8 @@ UNETSEG_API int unetseg_adam_dev(float* p, const float* g, float* m, float* v, l
 }
 
 UNETSEG_API int unetseg_gap_fwd(int dtype, const void* x, int ldx, int B, int HW, int C, float* g, void* stream) {
+  US_CHECK_DTYPE(dtype, "gap_fwd");
+  US_CHECK_ARG(x && g && B > 0 && HW > 0 && C > 0 && ldx >= C, "gap_fwd: bad args");
   if (dtype == DT_BF16)
     hipLaunchKernelGGL(gap_kernel<bf16>, dim3(ceil_div(B * C, 256)), dim3(256), 0, (hipStream_t)stream, (const bf16*)x,
                        ldx, B, HW, C, g);
@@ -717,6 +723,8 @@ UNETSEG_API int unetseg_gap_fwd(int dtype, const void* x, int ldx, int B, int HW
 
 UNETSEG_API int unetseg_gap_bwd(int dtype, const float* dg, int B, int HW, int C, void* dx, int ldx, int accumulate,
                                 void* stream) {
+  US_CHECK_DTYPE(dtype, "gap_bwd");
+  US_CHECK_ARG(dg && dx && B > 0 && HW > 0 && C > 0 && ldx >= C, "gap_bwd: bad args");
   const long n = (long)B * HW * C;
   if (dtype == DT_BF16)
     hipLaunchKernelGGL(gap_bwd_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dg, B, HW, C,
@@ -731,6 +739,8 @@ UNETSEG_API int unetseg_gap_bwd(int dtype, const float* dg, int B, int HW, int C
 UNETSEG_API int unetseg_linear_fwd(const float* x, const float* W, const float* bias, int B, int I, int O, int act,
                                    float p_drop, unsigned long long seed, const float* mask_in, float* mask_out,
                                    float* pre, float* y, void* stream) {
+  US_CHECK_ARG(x && W && y && B > 0 && I > 0 && O > 0, "linear_fwd: null pointer or empty shape");
+  US_CHECK_ARG(act >= 0 && act <= 2 && (act != 2 || p_drop < 1.f), "linear_fwd: act %d / p_drop %g", act, p_drop);
   const long threads = (long)B * O * 64;
   hipLaunchKernelGGL(linear_fwd_kernel, dim3(ceil_div(threads, 256)), dim3(256), 0, (hipStream_t)stream, x, W, bias, B,
                      I, O, act, p_drop, seed, mask_in, mask_out, pre, y);
@@ -742,6 +752,9 @@ UNETSEG_API int unetseg_linear_fwd(const float* x, const float* W, const float* 
 UNETSEG_API int unetseg_linear_bwd(const float* dy, const float* pre, const float* mask, float p_drop, int act,
                                    const float* x, const float* W, int B, int I, int O, float* dx, float* dW, float* db,
                                    float* scratch, void* stream) {
+  US_CHECK_ARG(dy && x && W && dW && db && scratch && B > 0 && I > 0 && O > 0, "linear_bwd: null pointer or empty shape");
+  US_CHECK_ARG(act >= 0 && act <= 2 && (act == 0 || pre) && (act != 2 || (mask && p_drop < 1.f)),
+               "linear_bwd: act %d needs pre (and the dropout mask)", act);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(linear_act_bwd_kernel, dim3(ceil_div(B * O, 256)), dim3(256), 0, st, dy, pre, mask, p_drop, act, B,
                      O, scratch);
@@ -753,6 +766,7 @@ UNETSEG_API int unetseg_linear_bwd(const float* dy, const float* pre, const floa
 
 UNETSEG_API int unetseg_ce_fwd(const float* logits, const int64_t* tgt, int B, int K, float* loss, float* dlog,
                                void* stream) {
+  US_CHECK_ARG(logits && tgt && loss && dlog && B > 0 && K > 0, "ce_fwd: null pointer or empty shape");
   hipLaunchKernelGGL(ce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, tgt, B, K, loss, dlog);
   US_LAUNCH_CHECK("ce_fwd");
   return 0;

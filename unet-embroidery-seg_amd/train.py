@@ -12,7 +12,8 @@ multitask.  Differences, all deliberate:
     synthetic embroidery-like generator;
   * launched under torchrun (WORLD_SIZE > 1) it trains data-parallel over RCCL: rank r takes every
     W-th image, gradients are bucket-averaged during backward (unetseg_hip.ddp.GradBuckets);
-  * plots / visual exports (matplotlib, cv2) are out of scope.
+  * the test-split visual export (utils/vis_export.py) needs an HF dataset, as the reference's does;
+    plots (matplotlib) are out of scope.
 """
 from __future__ import annotations
 
@@ -39,6 +40,7 @@ from model.unet_training import get_lr_scheduler, lovasz_hinge_loss, set_optimiz
 from unetseg_hip.arena import FusedAdam  # noqa: E402
 from unetseg_hip.ddp import GradBuckets, init_from_env, local_device  # noqa: E402
 from utils.hf_dataloader import DeviceLoader, HFUnetDataset, make_collate  # noqa: E402
+from utils.vis_export import export_binary_visuals  # noqa: E402
 from utils.synthetic import SyntheticSegDataset, collate  # noqa: E402
 from utils.train_and_eval import (  # noqa: E402
     evaluate,
@@ -241,6 +243,14 @@ def train(args):
                                                ignore_index=None, max_batches=mtest)
             with open(os.path.join(exp_folder, "test_metrics.json"), "w", encoding="utf-8") as f:
                 json.dump(test_metrics, f, ensure_ascii=False, indent=2)
+            # fixed-sample visual export of the test split (train.py:476-486; HF datasets only)
+            if args.task in ("binary", "multitask") and args.export_vis and isinstance(test_ds, HFUnetDataset):
+                try:
+                    export_binary_visuals(model=model, hf_unet_dataset=test_ds, out_dir=os.path.join(exp_folder, "vis"),
+                                          input_shape=[args.input_size] * 2, device=device, num_samples=args.vis_num,
+                                          seed=args.vis_seed)
+                except Exception as e:  # the reference reports and continues (train.py:487-488)
+                    print(f"[WARN] Skip test evaluation: {e}")
         with open(os.path.join(exp_folder, "val_metrics_history.json"), "w", encoding="utf-8") as f:
             json.dump(history, f, ensure_ascii=False, indent=2)
         fields = ["epoch"] + [k for k in (history[0] if history else {})]
@@ -284,7 +294,7 @@ def parse_args(argv=None):
     p.add_argument("--amp", action=argparse.BooleanOptionalAction, default=True)
     p.add_argument("--seed", default=11, type=int)
     p.add_argument("--cache-dir", default=".hf-cache/datasets")
-    p.add_argument("--export-vis", action=argparse.BooleanOptionalAction, default=False)
+    p.add_argument("--export-vis", action=argparse.BooleanOptionalAction, default=True)
     p.add_argument("--vis-num", default=8, type=int)
     p.add_argument("--vis-seed", default=0, type=int)
     p.add_argument("--max-train-batches", default=0, type=int)

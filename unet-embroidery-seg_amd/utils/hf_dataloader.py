@@ -135,7 +135,7 @@ class HFUnetDataset(torch.utils.data.Dataset):
             missing = {"image", "mask"} - set(names)
             if missing:
                 raise ValueError(f"{f}: missing columns {sorted(missing)}")
-            cols = [c for c in ("image", "mask", "label") if c in names]
+            cols = [c for c in ("image", "mask", "label", "filename") if c in names]
             self._tables.append(pq.read_table(f, columns=cols, memory_map=True))
         self._starts = np.cumsum([0] + [t.num_rows for t in self._tables])
         self.length = int(self._starts[-1])

@@ -95,12 +95,15 @@ def val(args):
 
 def parse_args(argv=None):
     p = argparse.ArgumentParser(description="U-Net evaluation on the MI355X HIP path")
-    p.add_argument("--weights", required=True)
-    p.add_argument("--data-path", default="synthetic")
+    p.add_argument("--data-path", default="./hf_datasets/merged_dataset_v2",
+                   help="HF parquet dataset directory, or 'synthetic' (the seeded synthetic test split)")
     p.add_argument("--data-config", default="no-ai", choices=["full", "no-ai", "sam3"])
+    p.add_argument("--weights", default="weights/unet_resnet_voc.pth")
     p.add_argument("--task", default="binary", choices=["binary", "multiclass", "multitask"])
     p.add_argument("--model", default="unet_resnet50", choices=sorted(SUPPORTED_MODELS.keys()))
-    p.add_argument("--loss", default="lovasz_hinge", choices=["bce", "lovasz_hinge"])
+    # val.py:176: ce / focal are accepted; the binary evaluation then refuses them as the reference's
+    # binary_segmentation_loss does (ValueError "Unsupported loss_name")
+    p.add_argument("--loss", default="lovasz_hinge", choices=["bce", "lovasz_hinge", "ce", "focal"])
     p.add_argument("--num-classes", default=4, type=int)
     p.add_argument("--device", default="cuda")
     p.add_argument("--input-size", default=512, type=int)
