@@ -4,8 +4,12 @@
   targets of -100 are ignored (mean over the others, zero gradient rows); any other class outside
   [0, K) gives a NaN loss and gradient instead of an out-of-range read;
 * float segmentation targets (MultiTaskLoss passes seg_targets.float(), unet_multitask.py:131) are
-  accepted when they are 0/1 and refused otherwise (the kernels take 0/1 labels; BCE would take soft
-  labels as given).
+  accepted when they are 0/1; a soft label (BCE would take it as given, the kernels take 0/1 labels)
+  turns the seg loss and its gradient into NaN on the device -- no host sync (ADVICE round 2);
+* binary_segmentation_loss reads float targets as (targets == 1), the reference's own mapping
+  (utils/train_and_eval.py:163);
+* the multiclass CE / Focal treat a target outside [0, C) other than ignore_index the way
+  nn.CrossEntropyLoss refuses it: NaN loss and gradient.
 """
 import pytest
 import torch
@@ -51,5 +55,35 @@ def test_float_seg_targets():
     _, _, _, sl_f, _ = _mt(ct, t01)
     _, _, _, sl_i, _ = _mt(ct, t01.long())
     torch.testing.assert_close(sl_f, sl_i)
-    with pytest.raises(ValueError, match="0/1"):
-        _mt(ct, t01 * 0.7)
+    seg, _, _, sl, cl = _mt(ct, t01 * 0.7)
+    assert torch.isnan(sl).item() and torch.isnan(seg.grad).all().item() and torch.isfinite(cl).item()
+
+
+def test_binary_loss_float_targets_as_reference():
+    from unetseg_hip.losses import binary_segmentation_loss
+    g = torch.Generator(device=DEV).manual_seed(5)
+    out = torch.randn(2, 2, 16, 16, generator=g, device=DEV)
+    t = torch.randint(0, 3, (2, 16, 16), generator=g, device=DEV).float() * 0.75  # 0, 0.75, 1.5: only ==1 is fg
+    t[0, :4] = 1.0
+    for kind in ("bce", "lovasz_hinge"):
+        a = binary_segmentation_loss(out, t, kind)
+        b = binary_segmentation_loss(out, (t == 1).long(), kind)
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("fn", ["ce", "focal"])
+def test_multiclass_out_of_range_target_is_nan(fn):
+    from model.unet_training import CE_Loss, Focal_Loss
+    g = torch.Generator(device=DEV).manual_seed(6)
+    x = torch.randn(2, 4, 8, 8, generator=g, device=DEV, requires_grad=True)
+    t = torch.randint(0, 4, (2, 8, 8), generator=g, device=DEV)
+    w = torch.ones(4, device=DEV)
+    f = CE_Loss if fn == "ce" else Focal_Loss
+    ok = f(x, t, w, num_classes=4)           # ignore_index = num_classes = 4: fine
+    t2 = t.clone()
+    t2[0, 0, 0] = 4                           # the ignore label
+    assert torch.isfinite(f(x, t2, w, num_classes=4)).item()
+    t2[1, 2, 3] = 7                           # neither a class nor the ignore label
+    bad = f(x, t2, w, num_classes=4)
+    bad.backward()
+    assert torch.isfinite(ok).item() and torch.isnan(bad).item() and torch.isnan(x.grad).all().item()

@@ -1246,7 +1246,8 @@ UNETSEG_API int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1
   US_CHECK_ARG(x1 && dy && ws && dw, "conv2d_wgrad: null pointer");
   US_CHECK_DTYPE(dtype, "conv2d_wgrad");
   US_CHECK_CONV_GEOM("conv2d_wgrad", n, h, w, r, s, stride, pad);
-  US_CHECK_ARG(cout > 0 && ldc1 >= c1 && (c2 == 0 || ldc2 >= c2) && ldy >= cout && dw_c >= c1 + c2,
+  // dw_c <= cin: the padded input channels of the first conv (3 -> 8) have no weight columns
+  US_CHECK_ARG(cout > 0 && ldc1 >= c1 && (c2 == 0 || ldc2 >= c2) && ldy >= cout && dw_c > 0 && dw_c <= c1 + c2,
                "conv2d_wgrad: bad channel counts / strides");
   US_CHECK_ARG((c1 + c2) % 8 == 0 && c1 % 8 == 0 && cout % 8 == 0 && ldy % 8 == 0, "conv2d_wgrad: channel counts must be multiples of 8");
   const int p = (h + 2 * pad - r) / stride + 1, q = (w + 2 * pad - s) / stride + 1;

@@ -1581,8 +1581,8 @@ UNETSEG_API int unetseg_upsample2x_bwd_relu(int dtype, const void* dy, int ldy, 
 UNETSEG_API int unetseg_pack_input(int dtype, const float* x, int n, int c, int h, int w, int cpad, void* y,
                                    void* stream) {
   US_CHECK_DTYPE(dtype, "pack_input");
+  US_CHECK_ARG(cpad >= c && c > 0 && n >= 0 && h >= 0 && w >= 0, "pack_input: bad sizes (c=%d, cpad=%d < c?)", c, cpad);
   US_CHECK_ARG(x && y, "pack_input: null pointer");
-  US_CHECK_ARG(cpad >= c && c > 0 && n >= 0 && h >= 0 && w >= 0, "pack_input: bad sizes (c=%d cpad=%d)", c, cpad);
   DISPATCH_T(dtype, hipLaunchKernelGGL(pack_input_kernel<T>, dim3(grid_for((long)n * h * w)), dim3(256), 0,
                                        (hipStream_t)stream, x, n, c, h, w, cpad, (T*)y));
   US_LAUNCH_CHECK("pack_input");

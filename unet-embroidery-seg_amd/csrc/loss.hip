@@ -652,7 +652,7 @@ UNETSEG_API size_t unetseg_bce_workspace(int B, long P) { return (size_t)grid_fo
 // BCE-with-logits mean loss; gz (may be NULL) = dloss/dz (already /count); pos_weight fp32 scalar or NULL
 UNETSEG_API int unetseg_bce_fwd(const float* out, int nch, const int64_t* tgt, int B, long P, const float* pos_weight,
                                 void* ws, size_t ws_bytes, float* gz, float* loss, void* stream) {
-  US_CHECK_ARG(out && tgt && ws && gz && loss, "bce_fwd: null pointer");
+  US_CHECK_ARG(out && tgt && ws && loss, "bce_fwd: null pointer");  // gz may be NULL (no gradient)
   US_CHECK_ARG(nch == 1 || nch == 2, "bce_fwd: nch %d must be 1 or 2", nch);
   US_CHECK_ARG(B > 0 && P > 0, "bce_fwd: empty batch");
   US_CHECK_ARG(ws_bytes >= unetseg_bce_workspace(B, P), "bce_fwd: workspace too small");

@@ -171,6 +171,12 @@ __global__ __launch_bounds__(256) void mc_loss_partial_kernel(McArgs a, float* p
     const float nll = valid ? lse - xt : 0.f;
     acc_wnll += wt * nll;
     acc_w += wt;
+    if (a.tgt && a.focal != 2 && t != a.ignore && !valid) {
+      // a target that is neither a class nor ignore_index: nn.CrossEntropyLoss (the reference's CE_Loss
+      // / Focal_Loss, model/unet_training.py:9-59) refuses it; here loss and gradient become NaN
+      acc_w += __builtin_nanf("");
+      acc_f += __builtin_nanf("");
+    }
     if (a.focal == 1) {
       const float logpt = -(wt * nll);
       const float pt = expf(logpt);
@@ -223,8 +229,9 @@ __global__ void mc_loss_finalize_kernel(McArgs a, const float* part, int G, floa
   const double n = (double)a.B * (double)a.P;
   const double main = a.focal == 2 ? 0.0 : a.focal == 1 ? s[2] / n : s[0] / s[1];
   double dice = 0.0;
+  const bool bad = s[1] != s[1];  // an invalid target poisoned the weight sum (partial kernel)
   coef[0] = s[1];
-  coef[1] = n;
+  coef[1] = bad ? s[1] : n;
   if (a.dice_t) {
     const double b2 = (double)a.beta * a.beta;
     double mean = 0.0;
@@ -238,8 +245,8 @@ __global__ void mc_loss_finalize_kernel(McArgs a, const float* part, int G, floa
     }
     dice = 1.0 - mean / a.C;
   }
-  loss[0] = (float)(main + dice);
-  loss[1] = (float)main;
+  loss[0] = (float)(bad ? s[1] : main + dice);
+  loss[1] = (float)(bad ? s[1] : main);
   loss[2] = (float)dice;
 }
 
@@ -249,6 +256,7 @@ __global__ __launch_bounds__(256) void mc_loss_bwd_kernel(McArgs a, const double
   const long total = (long)a.B * a.P;
   const float g = gscale ? gscale[0] : 1.f;
   const float inv_w = (float)(1.0 / coef[0]), inv_n = (float)(1.0 / coef[1]);
+  const float poison = 0.f * inv_n;  // NaN when an invalid target poisoned the sums, else 0
   const double b2 = (double)a.beta * a.beta;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     float x[kMaxC], lse;
@@ -280,7 +288,7 @@ __global__ __launch_bounds__(256) void mc_loss_bwd_kernel(McArgs a, const double
     }
     float d[kMaxC];
 #pragma unroll
-    for (int c = 0; c < kMaxC; ++c) d[c] = k * (pr[c] - (c == t ? 1.f : 0.f));
+    for (int c = 0; c < kMaxC; ++c) d[c] = k * (pr[c] - (c == t ? 1.f : 0.f)) + poison;
     if (a.dice_t) {
       const float* tt = a.dice_t + i * a.ct;
       float gp[kMaxC], dot = 0.f;

@@ -18,18 +18,33 @@ def _stream(dev):
     return torch.cuda.current_stream(dev).cuda_stream
 
 
-def _prep(outputs, targets):
+def _prep(outputs, targets, ignore_index=None):
+    """-> (fp32 outputs, int64 targets, soft): float targets are mapped the way the reference reads
+    them, (targets == 1) (utils/train_and_eval.py:163, binary_segmentation_loss; ignore_index kept);
+    `soft` is a device bool, True when some float target is neither 0 nor 1 -- MultiTaskLoss
+    (model/unet_multitask.py:131) feeds seg_targets.float() straight to BCE, where such a soft label
+    would count as given and the 0/1 kernels cannot represent it: that loss is poisoned to NaN on the
+    device (_poison) instead of a host check, so no call syncs the stream."""
     if not outputs.is_cuda:
         raise RuntimeError("HIP losses need device tensors")
     out = outputs.detach().float().contiguous()
-    if targets.is_floating_point():
-        # MultiTaskLoss passes seg_targets.float() (model/unet_multitask.py:131) to BCE, which would
-        # take soft labels as given; the kernels take 0/1 labels, so anything else is refused rather
-        # than silently binarised (a host check: float targets only come from that path)
-        if bool(((targets != 0) & (targets != 1)).any()):
-            raise ValueError("float segmentation targets must be 0/1 (soft labels are not supported)")
-    tgt = targets.detach().to(torch.int64).contiguous()
-    return out, tgt
+    soft = None
+    t = targets.detach()
+    if t.is_floating_point():
+        soft = ((t != 0) & (t != 1)).any()
+        tgt = (t == 1).to(torch.int64)
+        if ignore_index is not None:
+            tgt = torch.where(t == ignore_index, torch.full_like(tgt, int(ignore_index)), tgt)
+        return out, tgt.contiguous(), soft
+    return out, t.to(torch.int64).contiguous(), soft
+
+
+def _poison(soft, *ts):
+    """NaN-fill ts in place where `soft` (device bool) is set (no host sync)"""
+    if soft is not None:
+        for t in ts:
+            if t is not None:
+                t.masked_fill_(soft, float("nan"))
 
 
 def _seg_forward(kind, out, nch, tgt, B, Pn, pos_weight, need_grad, ignore_index=None):
@@ -73,7 +88,7 @@ def _seg_forward(kind, out, nch, tgt, B, Pn, pos_weight, need_grad, ignore_index
 class _SegLossFn(torch.autograd.Function):
     @staticmethod
     def forward(fctx, outputs, targets, kind, pos_weight, ignore_index=None):
-        out, tgt = _prep(outputs, targets)
+        out, tgt, _ = _prep(outputs, targets, ignore_index)
         B, nch = out.shape[0], out.shape[1]
         Pn = out[0, 0].numel()
         loss, gz = _seg_forward(kind, out, nch, tgt, B, Pn, pos_weight, outputs.requires_grad, ignore_index)
@@ -112,11 +127,13 @@ def seg_loss_1ch(logits, targets, kind):
 class _MultiTaskFn(torch.autograd.Function):
     @staticmethod
     def forward(fctx, seg, cls, seg_t, cls_t, w, kind):
-        out, tgt = _prep(seg, seg_t)
+        out, tgt, soft = _prep(seg, seg_t)
         B = out.shape[0]
         Pn = out[0].numel()
         dev = out.device
         seg_loss, gz = _seg_forward(kind, out, 1, tgt, B, Pn, None, True)
+        if kind == "bce":
+            _poison(soft, seg_loss, gz)
         c = cls.detach().float().contiguous()
         ct = cls_t.detach().to(device=dev, dtype=torch.int64).contiguous()
         cls_loss = torch.empty((), dtype=torch.float32, device=dev)
@@ -160,7 +177,7 @@ def binary_confusion(outputs, targets, conf=None, ignore_index=None):
     """device uint64[4] (+)= (tp, fp, fn, tn).  outputs [B,2,H,W] (argmax, tie -> 0) or [B,1,H,W]
     (sigmoid > 0.5); pixels whose target is ignore_index are skipped.  No host sync: callers read
     the counters once per split."""
-    out, tgt = _prep(outputs, targets)
+    out, tgt, _ = _prep(outputs, targets, ignore_index)
     B, nch = out.shape[0], out.shape[1]
     Pn = out[0, 0].numel()
     if conf is None:

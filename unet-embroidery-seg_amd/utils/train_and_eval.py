@@ -3,8 +3,12 @@
 confusion-matrix metrics) and multitask.
 
 Same signatures, return values and metric definitions as the reference; the losses and the
-confusion counts run on fused HIP kernels and the per-iteration host syncs are reduced to one
-``loss.item()``.
+confusion counts run on fused HIP kernels.  The reference prints every iteration's ``loss.item()``
+(a host sync that drains the launch queue each step); here the progress line carries the same
+columns but shows the PREVIOUS iteration's loss, read from a pinned copy whose event has completed
+while the current step is already queued (``_LaggedLoss``), so the GPU never idles for the print;
+the epoch's loss sums accumulate on the device (the same fp64 sum of the same fp32 values) and are
+read once per epoch.
 """
 import time
 
@@ -21,6 +25,57 @@ class LogColor:
     RED = "\033[1;31m"
     RESET = "\033[0m"
     BLUE = "\033[1;34m"
+
+
+class _LaggedLoss:
+    """the previous step's scalar loss on the host without draining the queue: push() enqueues a
+    non-blocking copy of this step's loss into a pinned buffer (two, alternating) and returns the
+    value of the step before it, whose copy is complete by the time the current step is queued"""
+
+    def __init__(self):
+        self.bufs = None
+        self.pending = None
+        self.i = 0
+
+    def push(self, loss):
+        t = loss.detach().float().reshape(())
+        if not t.is_cuda:
+            return float(t)
+        if self.bufs is None:
+            self.bufs = [torch.empty((), dtype=torch.float32, pin_memory=True) for _ in range(2)]
+        buf = self.bufs[self.i]
+        self.i ^= 1
+        buf.copy_(t, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        prev, self.pending = self.pending, (buf, ev)
+        if prev is None:
+            return None
+        prev[1].synchronize()
+        return float(prev[0])
+
+    def flush(self):
+        if self.pending is None:
+            return None
+        self.pending[1].synchronize()
+        v = float(self.pending[0])
+        self.pending = None
+        return v
+
+
+def _progress(epoch, train_epoch, it, n, gpu_used, lv, lr, size, header):
+    """the reference's column-aligned progress line (train_and_eval.py:233-257, 373-401); lv: the
+    loss printed (the previous iteration's; the epoch's first iteration prints its own at the end)"""
+    if header:
+        print(f"{LogColor.GREEN}Epoch{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}data_num{LogColor.RESET}{' ' * 12}"
+              f"{LogColor.YELLOW}GPU Mem{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}Loss{LogColor.RESET}{' ' * 12}"
+              f"{LogColor.YELLOW}LR{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}Image_size{LogColor.RESET}{' ' * 12}")
+    if lv is None:
+        return
+    e, b, g, ls, r = f"{epoch + 1}/{train_epoch}", f"{it}/{n}", f"{gpu_used:.2f} MB", f"{lv:.8f}", f"{lr:.8f}"
+    print(f"\r{e}{' ' * (len('Epoch') + 12 - len(e))}{b}{' ' * (len('data_num') + 12 - len(b))}"
+          f"{g}{' ' * (len('GPU Mem') + 12 - len(g))}{ls}{' ' * (len('Loss') + 12 - len(ls))}"
+          f"{r}{' ' * (len('LR') + 12 - len(r))}{size}", end="", flush=True)
 
 
 def _binary_logits_from_two_class(output: torch.Tensor) -> torch.Tensor:
@@ -62,7 +117,8 @@ def binary_segmentation_loss(outputs, targets, loss_name: str, pos_weight=None, 
 def train_one_epoch_binary(model, optimizer, train_loader, device, loss_name: str, pos_weight, gpu_used, scaler, epoch,
                            train_epoch, ignore_index=None, max_batches=None):
     """train_and_eval.py:185-263"""
-    epoch_loss = 0.0
+    epoch_loss = torch.zeros((), dtype=torch.float64, device=device)
+    lag = _LaggedLoss()
     seen_batches = 0
     model_train = model.train().to(device)
     n_batches = len(train_loader)
@@ -83,20 +139,17 @@ def train_one_epoch_binary(model, optimizer, train_loader, device, loss_name: st
             scaler.scale(loss).backward()
             scaler.step(optimizer)
             scaler.update()
-        lv = loss.item()
-        epoch_loss += lv
+        epoch_loss += loss.detach().double()
         seen_batches += 1
-        if iteration == 0:
-            print(f"{LogColor.GREEN}Epoch{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}data_num{LogColor.RESET}{' ' * 12}"
-                  f"{LogColor.YELLOW}GPU Mem{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}Loss{LogColor.RESET}{' ' * 12}"
-                  f"{LogColor.YELLOW}LR{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}Image_size{LogColor.RESET}{' ' * 12}")
-        print(f"\r{epoch + 1}/{train_epoch}    {iteration + 1}/{n_batches}    {gpu_used:.2f} MB    {lv:.8f}    "
-              f"{get_lr(optimizer):.8f}    {imgs.shape[2]}", end="", flush=True)
+        _progress(epoch, train_epoch, iteration, n_batches, gpu_used, lag.push(loss), get_lr(optimizer), imgs.shape[2],
+                  iteration == 0)
         if max_batches is not None and seen_batches >= max_batches:
             break
+    _progress(epoch, train_epoch, seen_batches, n_batches, gpu_used, lag.flush(), get_lr(optimizer), imgs.shape[2],
+              False)
     print(f"{LogColor.GREEN}")
     time.sleep(0.2)
-    return epoch_loss / max(seen_batches, 1)
+    return float(epoch_loss.item()) / max(seen_batches, 1)
 
 
 def evaluate_binary(model, val_loader, device, loss_name: str, pos_weight, ignore_index=None, max_batches=None):
@@ -229,6 +282,7 @@ def train_one_epoch(model, optimizer, train_loader, device, dice_loss, focal_los
     import numpy as np
     cls_weights = np.ones([num_classes], np.float32)
     epoch_loss = torch.zeros((), dtype=torch.float64, device=device)
+    lag = _LaggedLoss()
     model_train = model.train().to(device)
     weights = torch.tensor(cls_weights).to(device)
     n_batches = len(train_loader)
@@ -248,12 +302,11 @@ def train_one_epoch(model, optimizer, train_loader, device, dice_loss, focal_los
             scaler.step(optimizer)
             scaler.update()
         epoch_loss += loss.detach().double()
-        if iteration == 0:
-            print(f"{LogColor.GREEN}Epoch{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}data_num{LogColor.RESET}{' ' * 12}"
-                  f"{LogColor.YELLOW}GPU Mem{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}Loss{LogColor.RESET}{' ' * 12}"
-                  f"{LogColor.YELLOW}LR{LogColor.RESET}{' ' * 12}{LogColor.YELLOW}Image_size{LogColor.RESET}{' ' * 12}")
-        print(f"\r{epoch + 1}/{train_epoch}    {iteration + 1}/{n_batches}    {gpu_used:.2f} MB    "
-              f"{get_lr(optimizer):.8f}    {imgs.shape[2]}", end="", flush=True)
+        _progress(epoch, train_epoch, iteration, n_batches, gpu_used, lag.push(loss), get_lr(optimizer), imgs.shape[2],
+                  iteration == 0)
+    if n_batches:
+        _progress(epoch, train_epoch, n_batches, n_batches, gpu_used, lag.flush(), get_lr(optimizer), imgs.shape[2],
+                  False)
     print(f"{LogColor.GREEN}")
     return float(epoch_loss.item()) / max(n_batches, 1)
 
