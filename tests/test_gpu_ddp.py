@@ -115,8 +115,9 @@ def _worker(rank, world, port, model_name, q, dtype="fp32", batch=2, size=64):
         rm = torch.cat([b.detach().float().reshape(-1) for k, b in m.named_buffers()]).cpu()
         rm0 = rm.clone()
         dist.broadcast(rm0, 0)
+        names = [(n, *m._slices[id(p)]) for n, p in m.named_parameters()]
         q.put((rank, local.cpu().numpy(), avg.cpu().numpy(), m._flat.detach().cpu().numpy(), pm.cpu().numpy(), nb,
-               bool(drift), bool(torch.equal(rm, rm0))))
+               bool(drift), bool(torch.equal(rm, rm0)), names))
         dist.destroy_process_group()
     except BaseException as e:  # report instead of hanging the parent
         import traceback
@@ -154,9 +155,13 @@ def test_dp2_one_gpu_hip_model(model_name, dtype, batch, size):
                 p.kill()
     for p in procs:
         assert p.exitcode == 0
-    (l0, a0, f0, r0, nb, drift, bsync0), (l1, a1, f1, r1, _, _, bsync1) = res[0], res[1]
+    (l0, a0, f0, r0, nb, drift, bsync0, names), (l1, a1, f1, r1, _, _, bsync1, _) = res[0], res[1]
     assert nb > 1, "expected several gradient buckets"
     want = 0.5 * (l0.astype(np.float64) + l1.astype(np.float64))
+    bad = [(n, off, int((np.abs(a0[off:off + k] - want[off:off + k]) > 1e-6 * np.abs(want[off:off + k]) + 1e-9).sum()), k)
+           for n, off, k in names]
+    bad = [b for b in bad if b[2]]
+    assert not bad, f"{len(bad)} parameters differ from the mean of the local gradients: {bad[:12]}"
     np.testing.assert_allclose(a0, want, rtol=1e-6, atol=1e-9)
     assert np.array_equal(a0, a1)
     assert np.array_equal(f0, f1), "parameters out of sync after the DP step"

@@ -9,3 +9,6 @@ timeout -k 10 400 python bench.py > gpurun_out/r03a_bench.json 2> gpurun_out/r03
 cut -c1-600 gpurun_out/r03a_bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r03a_prof -o run -- python bench.py --steps 3 --warmup 1 --cpu-baseline 0 --probe 0 > gpurun_out/r03a_prof.log 2>&1 || { echo prof failed; exit 1; }
 echo done
+timeout -k 10 300 python tools/layer_table.py --top 80 > gpurun_out/r03a_layers.txt 2>&1 || echo "layer table failed"
+python tools/trace_gaps.py gpurun_out/r03a_prof 2 > gpurun_out/r03a_gaps.txt 2>&1 || echo "gaps failed"
+python tools/trace_streams.py gpurun_out/r03a_prof 2 > gpurun_out/r03a_streams.txt 2>&1 || echo "streams failed"

@@ -377,8 +377,9 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
         side = ctx.side
         if side is not None:
             lib.stream_wait(side.cuda_stream, ctx.stream)
-            # dY and the inputs may be freed (compute-stream order) before the wgrad has run
-            for t in (dY, X1, X2):
+            # dY, the inputs and the input prologue's BN coefficients may be freed (compute-stream
+            # order) before the wgrad has run on the side stream, which lags the compute stream
+            for t in (dY, X1, X2) + ((lazy.sc, lazy.sh) if lazy is not None else ()):
                 if t is not None:
                     t.record_stream(side)
             ws = workspace(ws_bytes, dev, 1)
