@@ -48,14 +48,16 @@ def main():
         part = torch.empty(3, C, G, device=dev)
         coef = torch.empty(6, C, device=dev)
         S = M * C * 2
-        for var in ("plain", "amask", "amask+y2"):
-            mA = P(A) if var != "plain" else 0
+        mbits = torch.randint(0, 256, (M * (C // 8),), dtype=torch.uint8, device=dev)
+        for var in ("plain", "amask", "amask+y2", "mbits", "mbits+y2"):
+            mA = P(A) if var.startswith("amask") else P(mbits) if var.startswith("mbits") else 0
+            lda = 0 if var.startswith("mbits") else C
             msc, msh = (P(sc), P(sh)) if var == "plain" else (0, 0)
-            y2 = Y2 if var == "amask+y2" else None
-            nt = 2 + (var != "plain") + (y2 is not None)
+            y2 = Y2 if var.endswith("+y2") else None
+            nt = 2 + (var.startswith("amask")) + (y2 is not None) + (1 / 16 if var.startswith("mbits") else 0)
 
             def red():
-                lib.bn_bwd_reduce(DT_BF16, P(dA), C, mA, C, msc, msh, P(Y), C, P(mean), P(inv), P(y2), C,
+                lib.bn_bwd_reduce(DT_BF16, P(dA), C, mA, lda, msc, msh, P(Y), C, P(mean), P(inv), P(y2), C,
                                   P(mean), P(inv), M, C, P(part), G, st)
 
             def fin():
@@ -63,7 +65,7 @@ def main():
                                     P(inv), P(dg), P(db), P(coef), st)
 
             def app():
-                lib.bn_bwd_apply(DT_BF16, P(dA), C, mA, C, msc, msh, P(Y), C, P(mean), P(inv), P(out1), C, P(y2), C,
+                lib.bn_bwd_apply(DT_BF16, P(dA), C, mA, lda, msc, msh, P(Y), C, P(mean), P(inv), P(out1), C, P(y2), C,
                                  P(mean), P(inv), P(out2 if y2 is not None else None), C, P(coef), 0, 0, 0, M, C, st)
 
             t_r, t_f, t_a = timeit(red), timeit(fin), timeit(app)
@@ -78,6 +80,19 @@ def main():
 
         t = timeit(fapply)
         print(f"M={M:8d} C={C:5d} bn_apply(res) {t * 1e6:7.1f} us {3 * S / t / 1e9:6.0f} GB/s", flush=True)
+        Gs = -(-M // 128)
+        sp = torch.randn(Gs, 2, C, device=dev).abs()
+        rm, rv, nbt = torch.zeros(C, device=dev), torch.ones(C, device=dev), torch.zeros(1, dtype=torch.int64, device=dev)
+        o4 = [torch.empty(C, device=dev) for _ in range(4)]
+
+        def bfin():
+            lib.bn_finalize(P(sp), C, Gs, M, 128, P(g), P(sh), P(rm), P(rv), P(nbt), 0.1, 1e-5, *[P(o) for o in o4], st)
+
+        def rows():
+            lib.bn_bwd_finalize_rows(P(sp), C, Gs, M, P(g), P(inv), P(dg), P(db), P(coef), st)
+
+        print(f"M={M:8d} C={C:5d} bn_finalize (G={Gs}) {timeit(bfin) * 1e6:6.1f} us  bwd_finalize_rows "
+              f"{timeit(rows) * 1e6:6.1f} us", flush=True)
     print({k: round(v * 1e3, 3) for k, v in tot.items()}, "ms summed")
 
 

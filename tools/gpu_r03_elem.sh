@@ -1,0 +1,3 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python tools/elem_bench.py 2>&1 | grep -v amdgpu.ids

@@ -112,7 +112,8 @@ def _loader(ds, args, shuffle, rank, world, device, workers=None):
     dl = DataLoader(ds, batch_size=args.batch_size, shuffle=shuffle, sampler=sampler, num_workers=workers,
                     pin_memory=not hf, drop_last=False, collate_fn=make_collate(ds) if hf else collate,
                     worker_init_fn=_SeededWorkerInit(args.seed) if workers else None)
-    return DeviceLoader(dl, device) if hf else dl
+    # the fp32 one-hot seg_labels are read by the multiclass Dice term only
+    return DeviceLoader(dl, device, onehot=args.task == "multiclass") if hf else dl
 
 
 def _pos_weight_auto(train_ds, args, device):

@@ -39,7 +39,7 @@ def val(args):
                            cache_dir=args.cache_dir, return_cls_label=args.task == "multitask")
         print(f"Test samples: {len(ds)}")
         loader = DeviceLoader(DataLoader(ds, batch_size=args.batch_size, shuffle=False, num_workers=0,
-                                         collate_fn=make_collate(ds)), device)
+                                         collate_fn=make_collate(ds)), device, onehot=args.task == "multiclass")
     else:
         if args.task == "multiclass":
             raise ValueError("the synthetic set is binary; the multiclass task needs a real --data-path")
