@@ -4,7 +4,9 @@
     (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
 
 A step = zero_grad + forward + Lovasz-hinge loss + backward (+ RCCL gradient all-reduce when N>1) +
-fused Adam on one synthetic batch already resident in HBM.  Rank 0 prints ONE JSON line.
+fused Adam on one synthetic batch already resident in HBM.  Adam and the re-pack of the conv weights
+run per gradient bucket on the weight-gradient stream while backward continues (--overlap-adam 1,
+FusedAdam(overlap=True)); every parameter is updated inside each timed step.  Rank 0 prints ONE JSON line.
 `roofline` covers the dominant kernel (igemm_tn: conv fwd + dgrad), measured with HIP events around
 each of its launches in one probe step right after the timed region.  `cpu_baseline` times the CPU
 oracle (oracle/ref_cpu.py, fp32, the reference's op sequence) on the host on a bounded sample.
@@ -45,6 +47,9 @@ def parse():
     ap.add_argument("--graph", type=int, default=0, help="replay the whole step (fwd+loss+bwd+Adam) as a HIP graph")
     ap.add_argument("--stream", type=int, default=1, help="run the steps on a created (non-default) HIP stream")
     ap.add_argument("--priority", type=int, default=0, help="priority of that stream (lower = higher priority)")
+    ap.add_argument("--overlap-adam", type=int, default=1,
+                    help="Adam + weight re-pack per gradient bucket on the weight-gradient stream during backward")
+    ap.add_argument("--bucket-mb", type=float, default=8.0, help="gradient bucket size (MB)")
     return ap.parse_args()
 
 
@@ -181,9 +186,11 @@ def main():
     with contextlib.redirect_stdout(sys.stderr):  # weights_init's banner (reference behaviour) -> stderr
         model = create_model(args.model, weights="", **kw).to(dev).train()
     model.compute_dtype = "bf16"
-    buckets = GradBuckets(model) if world > 1 else None
+    buckets = GradBuckets(model, bucket_mb=args.bucket_mb) if world > 1 else None
     use_graph = bool(args.graph) and world == 1  # N>1: RCCL collectives stay eager
-    opt = FusedAdam(model, lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4, capturable=use_graph)
+    overlap = bool(args.overlap_adam) and not use_graph
+    opt = FusedAdam(model, lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4, capturable=use_graph, overlap=overlap,
+                    bucket_mb=args.bucket_mb)
     nbatches = 2
     multitask = args.model == "multitask_unet"
     data = []
@@ -313,7 +320,7 @@ def main():
             "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
             "step_tflops_per_gpu": round(step_tflops, 2),
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 3), "final_loss": round(final_loss, 5),
-            "hip_graph": use_graph, "params_in_sync": in_sync,
+            "hip_graph": use_graph, "overlap_adam": overlap, "params_in_sync": in_sync,
         }
         print(json.dumps(line))
     if world > 1:

@@ -33,7 +33,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, model_name, q, dtype="fp32", batch=2, size=64):
+def _worker(rank, world, port, model_name, q, dtype="fp32", batch=2, size=64, overlap=False):
     import contextlib
     import io
     import sys
@@ -98,12 +98,14 @@ def _worker(rank, world, port, model_name, q, dtype="fp32", batch=2, size=64):
         for k, b in m.named_buffers():  # undo the running-stat update of the local pass
             b.copy_(bufs[k])
         m._grad_hook, m._after_backward = hook, after
+        # overlap: Adam + re-pack per bucket on the weight-gradient stream right after its all-reduce
+        opt = FusedAdam(m, lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4, overlap=overlap)
+        p_before = m._flat.detach().clone()
         # the DP step: buckets all-reduced (AVG) from inside backward on the weight-gradient stream
         fwd_bwd()
         avg = m._flat_grad.detach().clone()
-        opt = FusedAdam(m, lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4)
-        p_before = m._flat.detach().clone()
         opt.step()
+        assert opt._step == 1
         torch.cuda.synchronize()
         # single-process Adam with the averaged gradient, for comparison
         pm, gm_ = p_before.clone(), {}
@@ -126,12 +128,14 @@ def _worker(rank, world, port, model_name, q, dtype="fp32", batch=2, size=64):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("model_name,dtype,batch,size", [
-    ("unet_resnet50", "fp32", 2, 64),
-    ("unet_resnet50", "bf16", 16, 512),    # C3's per-GPU step: the bench dtype, batch and size
-    ("multitask_unet", "bf16", 8, 512),    # C5's per-GPU step (seg BCE + CE, the cls head's buckets)
+@pytest.mark.parametrize("model_name,dtype,batch,size,overlap", [
+    ("unet_resnet50", "fp32", 2, 64, False),
+    ("unet_resnet50", "bf16", 16, 512, False),   # C3's per-GPU step: the bench dtype, batch and size
+    ("multitask_unet", "bf16", 8, 512, False),   # C5's per-GPU step (seg BCE + CE, the cls head's buckets)
+    ("unet_resnet50", "bf16", 4, 128, True),     # bench.py's step: Adam inside backward, per bucket
+    ("multitask_unet", "bf16", 8, 512, True),
 ])
-def test_dp2_one_gpu_hip_model(model_name, dtype, batch, size):
+def test_dp2_one_gpu_hip_model(model_name, dtype, batch, size, overlap):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import numpy as np
@@ -139,7 +143,7 @@ def test_dp2_one_gpu_hip_model(model_name, dtype, batch, size):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, model_name, q, dtype, batch, size)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, model_name, q, dtype, batch, size, overlap)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}

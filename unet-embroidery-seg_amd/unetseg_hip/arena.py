@@ -17,9 +17,20 @@ class FusedAdam(torch.optim.Optimizer):
     ``capturable=True`` (as torch.optim.Adam's flag): lr and the step count live in device memory so
     the step can be captured in a HIP graph and replayed; ``step()`` outside a capture refreshes the
     device lr from ``param_groups`` (one small H2D copy when it changed).
+
+    ``overlap=True``: the update runs per gradient bucket (ddp.GradBuckets; one is created with
+    ``allreduce=False`` when the model has none) on the weight-gradient stream DURING backward, right
+    after the bucket's last gradient (and its all-reduce under DDP), followed by the re-pack of that
+    bucket's conv weights into the GEMM images the next forward reads -- so neither the update nor
+    the pack sits on the compute stream's critical path.  ``step()`` then only commits the step
+    count.  The update uses ``param_groups[0]`` as read at that backward, so lr changes must come
+    before ``backward()``; incompatible with a grad scaler (no ``grad_scale``), and a backward is
+    always followed by ``step()`` (the update already happened).  bench.py uses it; train.py keeps
+    the reference's backward -> step order.
     """
 
-    def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, capturable=False):
+    def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, capturable=False,
+                 overlap=False, bucket_mb=8.0):
         if not hasattr(model, "_flat"):
             raise TypeError("FusedAdam needs a HipModel (flat parameter arena)")
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
@@ -32,6 +43,39 @@ class FusedAdam(torch.optim.Optimizer):
         self._hyper = None  # device [lr] (capturable)
         self._step_dev = None  # device int32 steps taken (capturable)
         self._lr_dev = None
+        self.overlap = overlap
+        self._applied = False  # an overlapped update ran in the last backward
+        if overlap:
+            if capturable:
+                raise ValueError("FusedAdam: overlap and capturable are exclusive")
+            from .ddp import GradBuckets
+            b = getattr(model, "_buckets", None)
+            if b is None:
+                b = GradBuckets(model, bucket_mb=bucket_mb, allreduce=False)
+            b.actions.append(self._bucket_update)
+            b.finish_actions.append(self._bucket_finish)
+
+    def _state(self, flat):
+        if self._m is None or self._m.device != flat.device:
+            self._m = torch.zeros_like(flat)
+            self._v = torch.zeros_like(flat)
+
+    def _bucket_update(self, i, s, e, stream):
+        """Adam over the arena slice [s, e) + re-pack of its convs, on `stream` (GradBuckets action)"""
+        m = self.model
+        flat, grad = m._flat, m._flat_grad
+        self._state(flat)
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        st = stream.cuda_stream if stream is not None else torch.cuda.current_stream(flat.device).cuda_stream
+        lib.adam(P(flat[s:e]), P(grad[s:e]), P(self._m[s:e]), P(self._v[s:e]), e - s, float(g["lr"]), float(b1),
+                 float(b2), float(g["eps"]), float(g["weight_decay"]), self._step + 1, None, st)
+        m._pack_range(s, e)
+        self._applied = True
+
+    def _bucket_finish(self):
+        if self._applied:
+            self.model._mark_prepacked()
 
     def zero_grad(self, set_to_none: bool = True):  # keep the grads as arena views
         self.model._attach_grads()
@@ -41,10 +85,15 @@ class FusedAdam(torch.optim.Optimizer):
     def step(self, closure=None, grad_scale=None):
         loss = closure() if closure is not None else None
         m = self.model
+        if self._applied:
+            if grad_scale is not None:
+                raise ValueError("FusedAdam(overlap=True) cannot take a grad scale (the update ran in backward)")
+            self._applied = False
+            self._step += 1
+            return loss
+        m._prepacked = None  # the weights change below: the next forward packs them
         flat, grad = m._flat, m._flat_grad
-        if self._m is None or self._m.device != flat.device:
-            self._m = torch.zeros_like(flat)
-            self._v = torch.zeros_like(flat)
+        self._state(flat)
         m._attach_grads()
         g = self.param_groups[0]
         self._step += 1

@@ -10,8 +10,19 @@ The reference is single-process (train.py:98); this is the build's DP path (SURV
   * BatchNorm uses per-GPU batch statistics and rank-local running stats (DDP without SyncBN);
   * with the op layer's weight-gradient stream (ops.OVERLAP) a bucket's collective is enqueued on
     that stream after it has waited for the compute stream, so it follows every writer.
+
+The same bucket tracking serves the optimizer overlap (``FusedAdam(overlap=True)``): per-bucket
+actions (``actions``: Adam over the bucket's arena slice and the re-pack of its conv weights) run on
+the weight-gradient stream right after the bucket's all-reduce (or, with ``allreduce=False`` on one
+GPU, right after its last gradient), so the update of the decoder's parameters overlaps the encoder's
+backward instead of running on the compute stream after it.  ``param_done`` is reported by the op
+layer only after the last compute-stream kernel that reads a parameter (or its packed image) has been
+enqueued, and the side stream waits for the compute stream before a bucket's work, so an update never
+overtakes a read of the old value.
 """
 from __future__ import annotations
+
+import contextlib
 
 import torch
 import torch.distributed as dist
@@ -19,10 +30,18 @@ import torch.distributed as dist
 from . import ops
 
 
+def _nullctx():
+    return contextlib.nullcontext()
+
+
 class GradBuckets:
-    def __init__(self, model, bucket_mb: float = 25.0, group=None):
+    def __init__(self, model, bucket_mb: float = 25.0, group=None, allreduce: bool = True):
         self.model = model
         self.group = group
+        self.allreduce = allreduce
+        prev = getattr(model, "_buckets", None)  # e.g. FusedAdam(overlap=True) made before DDP
+        self.actions = prev.actions if prev is not None else []  # fn(bucket, start, end, stream)
+        self.finish_actions = prev.finish_actions if prev is not None else []  # fn() after the last bucket
         flat = model._flat
         esz = flat.element_size()
         cap = max(1, int(bucket_mb * 1024 * 1024 / esz))
@@ -47,7 +66,9 @@ class GradBuckets:
         self._issued = None
         model._grad_hook = self._on_grad
         model._after_backward = self._finish
-        self.broadcast_state()
+        model._buckets = self
+        if allreduce:
+            self.broadcast_state()
 
     @torch.no_grad()
     def broadcast_state(self):
@@ -80,14 +101,19 @@ class GradBuckets:
         s, e, _ = self.buckets[i]
         view = self.model._flat_grad[s:e]
         side = ops.side_stream(view.device) if (ops.OVERLAP and view.is_cuda) else None
-        if side is None:
-            self._pending.append(dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
-        else:
+        if side is not None:
             # weight gradients are written on the side stream, BN/bias gradients on the compute
             # stream: the collective is ordered after both (side waits for compute, RCCL for side)
             side.wait_stream(torch.cuda.current_stream(view.device))
-            with torch.cuda.stream(side):
-                self._pending.append(dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            if self.allreduce:
+                w = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+                if self.actions:
+                    w.wait()  # RCCL: the current (side) stream waits; gloo: the host waits
+                else:
+                    self._pending.append(w)
+            for act in self.actions:
+                act(i, s, e, side)
         self._issued[i] = True
 
     def _on_grad(self, p):
@@ -108,6 +134,8 @@ class GradBuckets:
                 self._issue(i)
         for w in self._pending:
             w.wait()
+        for act in self.finish_actions:
+            act()
         self._left = None
         self._pending = []
 

@@ -143,9 +143,8 @@ class _ModelFn(torch.autograd.Function):
             holder["grad"] = g
         model._attach_grads()
         ctx.grad_hook = model._grad_hook
+        ctx.finish_hook = model._after_backward  # inside backward: before the streams join
         ctx.backward()
-        if model._after_backward is not None:
-            model._after_backward()
         fctx.hctx = None
         return (None, None, None) + (None,) * fctx.nparams
 
@@ -234,6 +233,8 @@ class HipModel(nn.Module):
                     m._buffers[k] = fn(b)
         for pc in self._packed:
             pc.wk = pc.wt = None
+        self._prepacked = None
+        self._range_tables = {}
         return self
 
     def _dtype(self):
@@ -246,12 +247,46 @@ class HipModel(nn.Module):
     def _pack_weights(self, ctx, need_t):
         if not self._packed:
             return
-        if getattr(self, "_pack_table", None) is None:
-            self._pack_table = ops.PackTable()
         # convs on the (padded) image need no data gradient -- unless an input op with parameters
         # sits in front of them (dualdense's BN-ReLU on the image: force_t)
-        self._pack_table.run(ctx, self._packed, [need_t and (pc.conv.in_channels >= 8 or getattr(pc, "force_t", False))
-                                                 for pc in self._packed])
+        flags = [need_t and (pc.conv.in_channels >= 8 or getattr(pc, "force_t", False)) for pc in self._packed]
+        key = (ctx.dt, str(ctx.device), tuple(flags))
+        pre = getattr(self, "_prepacked", None)
+        self._prepacked = None
+        if need_t:
+            self._pack_key = key  # the flags the per-bucket re-pack reuses (recording forwards only)
+        if pre == key:
+            return  # an overlapped optimizer update re-packed every conv right after writing it
+        if getattr(self, "_pack_table", None) is None:
+            self._pack_table = ops.PackTable()
+        self._pack_table.run(ctx, self._packed, flags)
+
+    def _pack_range(self, s, e):
+        """re-pack the convs whose weights lie in arena range [s, e) -- on the current stream, with
+        the dtype / transposed-image flags of the last forward (FusedAdam(overlap=True), per bucket)"""
+        key = getattr(self, "_pack_key", None)
+        if key is None or not self._packed:
+            return
+        tabs = self.__dict__.setdefault("_range_tables", {})
+        ent = tabs.get((s, e))
+        if ent is None:
+            sel = [i for i, pc in enumerate(self._packed) if s <= self._slices[id(pc.conv.weight)][0] < e]
+            ent = tabs[(s, e)] = (sel, ops.PackTable())
+        sel, table = ent
+        if not sel:
+            return
+        dt, dev, flags = key
+        ctx = ops.Ctx(dt, True, False, torch.device(dev))
+        table.run(ctx, [self._packed[i] for i in sel], [flags[i] for i in sel])
+
+    def _mark_prepacked(self):
+        """every bucket's convs were re-packed after the update: the next forward with the same
+        dtype / flags skips its pack"""
+        self._prepacked = getattr(self, "_pack_key", None)
+
+    def load_state_dict(self, *a, **k):
+        self._prepacked = None
+        return super().load_state_dict(*a, **k)
 
     def forward(self, x):
         if not x.is_cuda:

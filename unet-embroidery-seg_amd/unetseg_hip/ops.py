@@ -131,6 +131,7 @@ class Ctx:
         self.main = torch.cuda.current_stream(device)
         self.stream = self.main.cuda_stream
         self.grad_hook = None  # called with a param after its gradient is final (DDP bucketing)
+        self.finish_hook = None  # called once the tape is done, before the compute stream joins the side
         self.side = None  # weight-gradient stream, set while backward runs with OVERLAP
 
     def push(self, fn):
@@ -156,6 +157,9 @@ class Ctx:
                 fn = tape.pop()
                 fn()
                 del fn
+            if self.finish_hook is not None:
+                # the last buckets' collectives / optimizer updates, enqueued before the join below
+                self.finish_hook()
         finally:
             if self.side is not None:
                 # everything after backward (optimizer, frees of tape tensors) follows the wgrads
@@ -163,8 +167,10 @@ class Ctx:
                 self.side = None
 
     def param_done(self, *params):
-        """report parameters whose gradient is final (DDP bucketing; stand-in tensors that are not
-        model parameters, e.g. a re-laid-out weight, are ignored by the hook)"""
+        """report parameters whose gradient is final AND that no later compute-stream kernel of this
+        backward reads (nor its packed image): a bucket's all-reduce / optimizer update may run on the
+        side stream right after (stand-in tensors that are not model parameters, e.g. a re-laid-out
+        weight, are ignored by the hook)"""
         if self.grad_hook is not None:
             for p in params:
                 if p is not None:
@@ -403,8 +409,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
             with _probe("wgrad", flops, 1, ("wgrad",) + desc, stream=side):
                 lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(dY), ldp(dY), K, R, S,
                                  stride, pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, wst)
-        ctx.param_done(pc.conv.weight, b)
-        # data gradient
+        # data gradient (reads the packed weight pc.wt: the parameter is reported done after it)
         if Kp != K:
             if x1.need_grad:
                 wtp = torch.zeros(C1, Kp, dtype=ctx.tdtype, device=dev)
@@ -428,6 +433,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                                  H, W, 0, ctx.stream)
             give_grad(ctx, x1, g[..., :C1])
             give_grad(ctx, x2, g[..., C1:])
+        ctx.param_done(pc.conv.weight, b)
 
     ctx.push(bwd)
     return out, st
