@@ -48,6 +48,11 @@ CASES = {
     # ---- forward ----
     "fwd_halo3_relu": ("fwd_relu", (2, 64, 256, 64, 0, 64, 3, 1), ["fwd:halo3"]),           # up_conv @512^2 (rows)
     "fwd_halo3_stats": ("fwd_stats", (2, 128, 128, 64, 0, 64, 3, 1), ["fwd:halo3"]),        # layer1 conv2
+    # more spatial tiles than persistent blocks, unevenly dealt (320 tiles over 256 / 128 blocks):
+    # the three-stage halo pipeline's prefetch of absent tiles and its per-block tile counts
+    "fwd_halo3_relu_multi": ("fwd_relu", (5, 128, 128, 64, 0, 64, 3, 1), ["fwd:halo3"]),
+    "fwd_halo3_stats_multi": ("fwd_stats", (5, 128, 128, 64, 0, 64, 3, 1), ["fwd:halo3"]),
+    "fwd_halo3_k128_multi": ("fwd_all", (3, 128, 128, 64, 0, 128, 3, 1), ["fwd:halo3"]),
     "fwd_ring256x128_t9": ("fwd_all", (16, 32, 32, 1024, 2048, 512, 3, 1), ["fwd:ring256x128_t9"]),  # up_concat4.conv1
     "fwd_ring256x128_t9_s2": ("fwd_stats", (16, 128, 128, 128, 0, 128, 3, 2), ["fwd:ring256x128_t9"]),  # layer2 conv2
     "fwd_ring256x128_t1": ("fwd_stats", (16, 64, 64, 512, 0, 128, 1, 1), ["fwd:ring256x128_t1"]),
@@ -69,6 +74,7 @@ CASES = {
     "fwd_generic_cin8": ("fwd_stats", (2, 64, 64, 8, 0, 64, 3, 1), ["fwd:generic"]),
     # ---- data gradient (plain / accumulated) ----
     "dgrad_halo3": ("dgrad", (1, 128, 128, 64, 0, 64, 3, 1), ["dgrad:halo3"]),
+    "dgrad_halo3_multi": ("dgrad", (5, 128, 128, 64, 0, 64, 3, 1), ["dgrad:halo3"]),
     "dgrad_ring256x128_t9": ("dgrad", (16, 64, 64, 128, 0, 128, 3, 1), ["dgrad:ring256x128_t9"]),
     "dgrad_ring256x128_t9_cat": ("dgrad", (16, 32, 32, 1024, 2048, 512, 3, 1), ["dgrad:ring256x128_t9"]),
     "dgrad_ring256x128_t1": ("dgrad", (16, 64, 64, 128, 0, 512, 1, 1), ["dgrad:ring256x128_t1"]),
@@ -91,6 +97,8 @@ CASES = {
     "post1_ring256x128_t9": ("post1", (16, 32, 32, 512, 0, 512, 3, 1), ["dgrad_post1:ring256x128_t9"]),
     "post1_ring128x128_5st_t9": ("post1", (8, 64, 64, 128, 0, 128, 3, 1), ["dgrad_post1:ring128x128_5st_t9"]),
     "post2_halo3": ("post2", (1, 128, 128, 64, 0, 64, 3, 1), ["dgrad_post2:halo3"]),
+    "post1_halo3_multi": ("post1", (5, 128, 128, 64, 0, 64, 3, 1), ["dgrad_post1:halo3"]),
+    "post2_halo3_multi": ("post2", (5, 128, 128, 64, 0, 64, 3, 1), ["dgrad_post2:halo3"]),
     "post2_tn128x128_1st": ("post2", (1, 64, 64, 512, 0, 128, 1, 1), ["dgrad_post2:tn128x128_1st"]),
     # batch 8: layer2 conv3 (128 -> 512 at 64^2), its data gradient with bn2-ReLU's backward fused
     "post2_tn128x128": ("post2", (8, 64, 64, 128, 0, 512, 1, 1), ["dgrad_post2:tn128x128"]),

@@ -51,6 +51,9 @@ struct FastTNArgs {
   const float* head_b;
   float* head_y;
   int head_k;
+  // issue-order options of the LDS-DMA ring (set by the launcher; UNETSEG_TN_SCHED): bit 0 = the
+  // waves of the second SIMD pair issue their K step's DMAs after the first K half's MFMAs
+  int sched;
 };
 
 struct FastWgradArgs {

@@ -334,6 +334,10 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
 #pragma unroll
     for (int s0 = 0; s0 < NS - 1; ++s0) issue(s0 / TAPS, s0 % TAPS, s0);
     int stage = 0;
+    // DMA issue costs the issuing wave tens of cycles per instruction; right after the barrier every
+    // wave would issue at once and leave the MFMA pipes idle.  With sched bit 0 the waves sharing a
+    // SIMD (w and w + 4 of 8) split: one issues before its first K half, the other after it.
+    const bool late = (a.sched & 1) && NWM * NWN == 8 && ((wid >> 2) & 1);
     for (int c = 0; c < nch; ++c) {
 #pragma unroll
       for (int t = 0; t < TAPS; ++t) {
@@ -341,9 +345,10 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
         bf16x8 pf[FP], wf[FC];
         frags(stage, 0, pf, wf);  // first fragments in flight while this step's loads issue
         const int st2 = stage == 0 ? NS - 1 : stage - 1;  // (stage + NS - 1) % NS
-        issue(c + (t + NS - 1) / TAPS, (t + NS - 1) % TAPS, st2);
+        if (!late) issue(c + (t + NS - 1) / TAPS, (t + NS - 1) % TAPS, st2);
         mfmas(pf, wf);
         frags(stage, 1, pf, wf);
+        if (late) issue(c + (t + NS - 1) / TAPS, (t + NS - 1) % TAPS, st2);
         mfmas(pf, wf);
         stage = stage == NS - 1 ? 0 : stage + 1;
       }
@@ -961,6 +966,8 @@ int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   // 2D spatial tiles measured slower than row-major tiles with the chunk-outer K order: opt-in
   static const bool t2d = getenv("UNETSEG_T2D") != nullptr;
   b.t2d = (t2d && a.nr * a.ns > 1 && a.wc % 32 == 0 && a.wc > 32 && a.hc % TR == 0) ? TR : 0;
+  static const int sched = getenv("UNETSEG_TN_SCHED") ? atoi(getenv("UNETSEG_TN_SCHED")) : 0;
+  b.sched = sched;
   hipLaunchKernelGGL((tn_fast_kernel<BM, BN, NWM, NWN, ST, POST, TAPS, PRE>), grid, dim3(NT), lds, st, b);
   return 0;
 }
@@ -980,6 +987,7 @@ int launch_tn_multi_cfg(const FastTNArgs* fs, int n, hipStream_t st) {
   for (int k = 0; k < n; ++k) {
     m.c[k] = fs[k];
     m.c[k].t2d = 0;
+    m.c[k].sched = 0;
     m.gx[k] = ceil_div(fs[k].M, BM);
     m.gy[k] = ceil_div(fs[k].Ng, BN);
     m.start[k] = total;

@@ -551,6 +551,422 @@ __global__ __launch_bounds__(64 * NW) void halo3_wgrad_kernel(HaloWgradArgs a, i
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// halo3r: the same convolutions with the weights resident in VGPRs instead of LDS.
+//
+// halo3_kernel keeps 72 KiB of weights in LDS, which leaves room for only two halo stages: one
+// tile's DMA (43 KiB per CU) is in flight while the current tile computes, and the counters show the
+// waves parked on that wait for a third of their cycles (SQ_WAIT_ANY 36 %, HBM at ~3.4 TB/s, MFMA
+// busy 45 % at 512^2).  Here each wave holds the weights of 32 output channels x 9 taps x 64 input
+// channels in registers (144 VGPRs, loaded once per block), which frees the LDS for THREE halo
+// stages: tile t+2 streams in while tile t computes (87 KiB in flight per CU), and the per-MFMA LDS
+// traffic drops to the pixel fragments only.
+//   waves: wid & 1 = output-channel half (32 channels, FC = 2 groups of 16); wid >> 1 = pixel set
+//   (FP = 32 / NW groups of 16 pixels of the 8 x 32 tile).
+//   Every wave issues exactly HI halo DMAs per tile (lanes past the halo load out of range into a
+//   padded stage) and, for the post-ops, exactly FC*FP aux loads, so all waits are compile-time
+//   vmcnt values: the epilogue waits for this tile's aux loads (issued before tile t+2's DMA), the
+//   end of a tile for tile t+1's halo; tile t+2's DMA stays in flight across the barrier.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint2 bload64_asm(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  uint2 v;
+  asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
+  return v;
+}
+
+template <int NW>
+constexpr int halo3r_stage_chunks() {
+  return ((10 * (HW_TW + 2) * 8 + 64 * NW - 1) / (64 * NW)) * 64 * NW;
+}
+
+template <int NW>
+size_t halo3r_lds_bytes() {
+  // [3 stages][padded halo] + red [NW/2][64] + bias [64] + post coefficients [4][64] + head [256][2]
+  return (size_t)3 * halo3r_stage_chunks<NW>() * 16 + (size_t)(NW / 2) * 64 * 4 + 64 * 4 + 256 * 4 + 256 * 2 * 4;
+}
+
+template <int NW, int POST, int EPI>
+__global__ __launch_bounds__(64 * NW) void halo3r_kernel(FastTNArgs a, int tiles_w, int tiles_h, int n_sp, int G_per,
+                                                         unsigned y_bytes, unsigned aux_bytes) {
+  constexpr int TH = 8;
+  constexpr bool kDyn = (EPI & kEpiDyn) != 0;
+  const bool has_bias = kDyn ? a.bias != nullptr : (EPI & kEpiBias) != 0;
+  const bool do_relu = kDyn ? a.relu != 0 : (EPI & kEpiRelu) != 0;
+  const bool do_stats = kDyn ? a.stats != nullptr : (EPI & kEpiStats) != 0;
+  const bool do_acc = kDyn ? a.accumulate != 0 : (EPI & kEpiAcc) != 0;
+  constexpr int HK = (EPI & kEpiHead2) ? 2 : (EPI & kEpiHead1) ? 1 : 0;
+  static_assert(HK == 0 || (!kDyn && POST == 0), "the fused head rides on a fixed bias + ReLU epilogue");
+  constexpr int NPG = NW / 2;                // pixel sets
+  constexpr int FP = 16 / NPG;               // 16-pixel groups per wave
+  constexpr int FC = 2;                      // 16-channel output groups per wave (32 channels)
+  constexpr int HP = (TH + 2) * (HW_TW + 2); // halo pixels
+  constexpr int HCH = HP * 8;                // 16-B chunks of a halo
+  constexpr int HI = (HCH + 64 * NW - 1) / (64 * NW);  // halo DMA instructions per wave
+  constexpr int SCH = HI * 64 * NW;          // chunks per (padded) stage
+  static_assert(SCH == halo3r_stage_chunks<NW>(), "stage size");
+  constexpr int NA = POST ? FP * FC : 0;     // aux loads per wave per tile
+  constexpr int NS = FP * FC + FP * HK;      // stores per wave per tile
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];
+  uint4* hl = lds;                                          // [3][SCH]
+  float* red = reinterpret_cast<float*>(hl + 3 * SCH);      // [NPG][64]
+  float* sbias = red + NPG * 64;                            // [64]
+  float* pco = sbias + 64;                                  // [4][64]: sc, sh, mean, inv
+  float* hred = pco + 256;                                  // [256 pixels][2]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wch = wid & 1, pg = wid >> 1;
+  const int tn = blockIdx.x / G_per, slot = blockIdx.x % G_per;
+  const int n0 = tn * 64;
+  const int my_tiles = slot < n_sp ? (n_sp - slot + G_per - 1) / G_per : 0;
+  const __amdgpu_buffer_rsrc_t rx = srd(a.x1, a.x1_bytes);
+  const __amdgpu_buffer_rsrc_t rw = srd(a.wt, a.w_bytes);
+  const __amdgpu_buffer_rsrc_t ry = srd(a.y, y_bytes);
+  const __amdgpu_buffer_rsrc_t ra = srd(POST ? a.aux : a.y, POST ? aux_bytes : 0u);
+  const unsigned hw_img = (unsigned)(a.OH * a.OW);
+  const __amdgpu_buffer_rsrc_t rh = srd(HK ? (const void*)a.head_y : a.y,
+                                        HK ? (unsigned)(a.M / (a.OH * a.OW)) * HK * hw_img * 4u : 0u);
+  const int j16 = lane & 15, kg = lane >> 4;
+
+  if (kDyn && a.bias && tid < 64) sbias[tid] = a.bias[n0 + tid];
+  if (POST == 2 && tid < 64) {
+    pco[tid] = a.psc[n0 + tid];
+    pco[64 + tid] = a.psh[n0 + tid];
+    pco[128 + tid] = a.pmean[n0 + tid];
+    pco[192 + tid] = a.pinv[n0 + tid];
+  }
+
+  // ---- resident weights: wr[jt][kk][c] = output channel n0 + 32 wch + 16 c + j16, halo tap jt,
+  // input channels 8 (4 kk + kg) .. +7 (the MFMA A fragment) ----
+  bf16x8 wr[9][2][FC];
+#pragma unroll
+  for (int jt = 0; jt < 9; ++jt) {
+    const int jr = jt / 3, js = jt - jr * 3;
+    const int wtap = (a.r0 + a.rs * jr) * a.S + (a.s0 + a.ss * js);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int c = 0; c < FC; ++c) {
+        const int k = wch * 32 + c * 16 + j16;
+        uint4 v = bload(rw, (unsigned)(n0 + k) * (unsigned)a.ldwb + (unsigned)(wtap * 128 + (kk * 4 + kg) * 16));
+        wr[jt][kk][c] = *reinterpret_cast<bf16x8*>(&v);
+      }
+  }
+  float hwr[HK > 0 ? HK : 1][FC][4], hbr[HK > 0 ? HK : 1];
+#pragma unroll
+  for (int k = 0; k < HK; ++k) {
+    hbr[k] = a.head_b[k];
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) hwr[k][c][e] = a.head_w[k * 64 + wch * 32 + c * 16 + kg * 4 + e];
+  }
+  float breg[FC][4];
+#pragma unroll
+  for (int c = 0; c < FC; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) breg[c][e] = (!kDyn && has_bias) ? a.bias[n0 + wch * 32 + c * 16 + kg * 4 + e] : 0.f;
+  // the preloads above are compiler-tracked: retire them here (a pre-existing wait the compiler
+  // accounts for), so no conservative vmcnt(0) lands inside the tile loop
+  __builtin_amdgcn_s_waitcnt(0);
+
+  // ---- halo DMA of tile t into stage t % 3 (see halo3_kernel); the lane geometry is recomputed per
+  // issue (a few VALU) rather than held in 2 x HI VGPRs; slots past the halo load out of range into
+  // the stage padding, so every wave issues exactly HI DMAs ----
+  auto issue_halo = [&](int t) {
+    const int stage = t % 3;
+    const unsigned base = __builtin_amdgcn_readfirstlane(lds_addr(hl + stage * SCH));
+    if (t >= my_tiles) {  // no such tile: the same count of DMAs, all out of range (zero fill)
+#pragma unroll
+      for (int i = 0; i < HI; ++i) dma16(rx, base + (unsigned)((i * NW + wid) * 1024), kOOB);
+      return;
+    }
+    const int sp = slot + t * G_per;
+    const int tw = sp % tiles_w, rest = sp / tiles_w;
+    const int th = rest % tiles_h, nb = rest / tiles_h;
+    const int h0 = th * TH, w0 = tw * HW_TW;
+    const unsigned hb = __builtin_amdgcn_readfirstlane((unsigned)((nb * a.H + h0 - 1) * a.W + w0 - 1) * (unsigned)a.ldc1b);
+    const unsigned kill = __builtin_amdgcn_readfirstlane(16u | (h0 == 0 ? 1u : 0u) | (h0 + TH >= a.H ? 2u : 0u) |
+                                                         (w0 == 0 ? 4u : 0u) | (w0 + HW_TW >= a.W ? 8u : 0u));
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const int idx = (i * NW + wid) * 64 + lane;
+      const int hp = idx >> 3, hr = hp / (HW_TW + 2), hc = hp - hr * (HW_TW + 2);
+      const unsigned flag = idx >= HCH ? 16u : (hr == 0 ? 1u : 0u) | (hr == TH + 1 ? 2u : 0u) | (hc == 0 ? 4u : 0u) |
+                                                   (hc == HW_TW + 1 ? 8u : 0u);
+      const unsigned off = (unsigned)(hr * a.W + hc) * (unsigned)a.ldc1b + swzh(hp, lane & 7) * 16u;
+      dma16(rx, base + (unsigned)((i * NW + wid) * 1024), (flag & kill) ? kOOB : hb + off);
+    }
+  };
+
+  // this lane's pixels: group g = pg * FP + p of the tile's 16 groups (2 per row)
+  float pq0[FC][4], pq1[FC][4];
+#pragma unroll
+  for (int c = 0; c < FC; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pq0[c][e] = pq1[c][e] = 0.f;
+  issue_halo(0);
+  issue_halo(1);
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(HI) : "memory");
+
+  // halo pixel of tap (0, 0) for each of this lane's pixel groups
+  unsigned u0[FP];
+#pragma unroll
+  for (int p = 0; p < FP; ++p) {
+    const int g = pg * FP + p;
+    u0[p] = (unsigned)(((g >> 1) + 1) * (HW_TW + 2) + (g & 1) * 16 + j16 + 1);
+  }
+  f32x4 acc[FC][FP];
+  for (int t = 0; t < my_tiles; ++t) {
+    // the tap shifts pass through an opaque copy per tile: the 9 x FP fragment addresses are then
+    // recomputed per tile (4 VALU each, beside the MFMAs) instead of being hoisted into 36 VGPRs
+    int dh0 = a.dh0, dhs = a.dhs, dw0 = a.dw0, dws = a.dws;
+    asm volatile("" : "+s"(dh0), "+s"(dhs), "+s"(dw0), "+s"(dws));
+    const int sp = slot + t * G_per;
+    const int tw = sp % tiles_w, rest = sp / tiles_w;
+    const int th = rest % tiles_h, nb = rest / tiles_h;
+    // post-op aux values of this tile: issued halfway through the tap loop (their registers live only
+    // from there) and before tile t+2's DMA, so the epilogue's wait for them leaves that DMA in flight
+    uint2 zr[FC][FP];
+    auto issue_aux = [&]() {
+#pragma unroll
+      for (int p = 0; p < FP; ++p) {
+        const int g = pg * FP + p;
+        const long opix = ((long)nb * a.OH + th * TH + (g >> 1)) * a.OW + tw * HW_TW + (g & 1) * 16 + j16;
+#pragma unroll
+        for (int c = 0; c < FC; ++c)
+          zr[c][p] = bload64_asm(ra, (unsigned)(opix * a.ld_aux + n0 + wch * 32 + c * 16 + kg * 4) * 2u);
+      }
+      issue_halo(t + 2);
+    };
+    if (!POST) issue_halo(t + 2);
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int p = 0; p < FP; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* hs = reinterpret_cast<const char*>(hl + (t % 3) * SCH);
+    // 18 steps (tap jt, K half kk), software-pipelined by hand: the pixel fragments of step s+1 are
+    // read before the MFMAs of step s, and sched_group_barrier pins that order (left to itself the
+    // scheduler issues each read right before its MFMAs and the waves sit on lgkmcnt)
+    // byte address of halo pixel u, chunk kg (kk 0): u * 128 + ((kg ^ u) & 7) * 16 (swzh); chunk
+    // 4 + kg (kk 1) differs in address bit 6 only
+    auto tap_addr = [&](int jt, unsigned (&ad)[FP]) {
+      const int jr = jt / 3, js = jt - jr * 3;
+      const int delta = (dh0 + dhs * jr) * (HW_TW + 2) + dw0 + dws * js;  // uniform
+#pragma unroll
+      for (int p = 0; p < FP; ++p) {
+        const unsigned u = u0[p] + (unsigned)delta;
+        ad[p] = (u << 7) | (((u ^ (unsigned)kg) & 7u) << 4);
+      }
+    };
+    auto frag_load = [&](const unsigned (&ad)[FP], int kk, bf16x8 (&pf)[FP]) {
+#pragma unroll
+      for (int p = 0; p < FP; ++p) {
+        uint4 v = *reinterpret_cast<const uint4*>(hs + (ad[p] ^ (kk ? 64u : 0u)));
+        pf[p] = *reinterpret_cast<bf16x8*>(&v);
+      }
+    };
+    unsigned ad[FP];
+    bf16x8 pfb[2][FP];
+    tap_addr(0, ad);
+    frag_load(ad, 0, pfb[0]);
+    __builtin_amdgcn_sched_group_barrier(0x100, FP, 0);  // step 0's reads form the first group
+#pragma unroll
+    for (int st = 0; st < 18; ++st) {
+      const int jt = st >> 1, kk = st & 1;
+      if (st + 1 < 18) {
+        if (kk == 1) tap_addr(jt + 1, ad);
+        frag_load(ad, (st + 1) & 1, pfb[(st + 1) & 1]);
+      }
+#pragma unroll
+      for (int c = 0; c < FC; ++c)
+#pragma unroll
+        for (int p = 0; p < FP; ++p)
+          acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[jt][kk][c], pfb[st & 1][p], acc[c][p], 0, 0, 0);
+      if (st + 1 < 18) __builtin_amdgcn_sched_group_barrier(0x100, FP, 0);  // DS reads of step st+1
+      __builtin_amdgcn_sched_group_barrier(0x008, FC * FP, 0);              // MFMAs of step st
+      if (POST && st == 8) issue_aux();
+    }
+
+    // ================= epilogue =================
+    if (POST) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HI) : "memory");  // this tile's aux (tile t+2's halo may fly)
+#pragma unroll
+      for (int c = 0; c < FC; ++c)
+#pragma unroll
+        for (int p = 0; p < FP; ++p) asm volatile("" : "+v"(zr[c][p]));
+    }
+    float csum[FC][4];
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) csum[c][e] = 0.f;
+    uint2 outv[FC][FP];
+    unsigned outo[FP];
+#pragma unroll
+    for (int p = 0; p < FP; ++p) {
+      const int g = pg * FP + p;
+      const long opix = ((long)nb * a.OH + th * TH + (g >> 1)) * a.OW + tw * HW_TW + (g & 1) * 16 + j16;
+      outo[p] = (unsigned)(opix * a.ldy + n0) * 2u;
+#pragma unroll
+      for (int c = 0; c < FC; ++c) {
+        const int cb = wch * 32 + c * 16 + kg * 4;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[c][p][e] + (!has_bias ? 0.f : kDyn ? sbias[cb + e] : breg[c][e]);
+          if (do_relu) v[e] = fmaxf(v[e], 0.f);
+        }
+        if (do_acc) {
+          const bf16* ob = reinterpret_cast<const bf16*>((const char*)a.y + outo[p] + cb * 2);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)ob[e];
+        }
+        bf16 o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = (bf16)v[e];
+          v[e] = (float)o[e];
+        }
+        if (POST) {
+          const bf16* z = reinterpret_cast<const bf16*>(&zr[c][p]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float zf = (float)z[e];
+            bool on = zf > 0.f;
+            float xh = 0.f;
+            if (POST == 2) {
+              const int ch = cb + e;
+              on = fmaf(zf, pco[ch], pco[64 + ch]) > 0.f;
+              xh = (zf - pco[128 + ch]) * pco[192 + ch];
+            }
+            v[e] = on ? v[e] : 0.f;
+            o[e] = (bf16)v[e];
+            pq0[c][e] += v[e];
+            if (POST == 2) pq1[c][e] += v[e] * xh;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          csum[c][e] += v[e];
+          acc[c][p][e] = v[e];
+        }
+        outv[c][p] = *reinterpret_cast<uint2*>(o);
+      }
+    }
+    if (HK) {
+      // head logits: this wave's 32 channels per pixel (4 channel groups kg summed by shuffles); the
+      // odd-channel-half waves hand their partial sums to the even ones through LDS
+      float hsum[HK > 0 ? HK : 1][FP];
+#pragma unroll
+      for (int p = 0; p < FP; ++p)
+#pragma unroll
+        for (int k = 0; k < HK; ++k) {
+          float h = 0.f;
+#pragma unroll
+          for (int c = 0; c < FC; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) h = fmaf(acc[c][p][e], hwr[k][c][e], h);
+          h += __shfl_xor(h, 16);
+          h += __shfl_xor(h, 32);
+          hsum[k][p] = h;
+          if (wch == 1 && kg == 0) hred[((pg * FP + p) * 16 + j16) * 2 + k] = h;
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+      for (int p = 0; p < FP; ++p) {
+        const int g = pg * FP + p;
+        const unsigned pix = (unsigned)((th * TH + (g >> 1)) * a.OW + tw * HW_TW + (g & 1) * 16 + j16);
+#pragma unroll
+        for (int k = 0; k < HK; ++k) {
+          const float h = hsum[k][p] + hred[(g * 16 + j16) * 2 + k] + hbr[k];
+          bstore32(rh, (wch == 0 && kg == 0) ? ((unsigned)(nb * HK + k) * hw_img + pix) * 4u : kOOB, h);
+        }
+      }
+    }
+    if (do_stats) {
+      // per-tile BN partials over the 256 pixels: column sums, then M2 about the tile mean
+#pragma unroll
+      for (int c = 0; c < FC; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float s = row16_sum(csum[c][e]);
+          if (j16 == 0) red[pg * 64 + wch * 32 + c * 16 + kg * 4 + e] = s;
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      float qv[FC][4];
+#pragma unroll
+      for (int c = 0; c < FC; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int col = wch * 32 + c * 16 + kg * 4 + e;
+          float tot = 0.f;
+#pragma unroll
+          for (int w = 0; w < NPG; ++w) tot += red[w * 64 + col];
+          const float mean = tot * (1.0f / (TH * HW_TW));
+          float q = 0.f;
+#pragma unroll
+          for (int p = 0; p < FP; ++p) {
+            const float d = acc[c][p][e] - mean;
+            q += d * d;
+          }
+          qv[c][e] = row16_sum(q);
+        }
+      float stot = 0.f;
+      if (tid < 64)
+#pragma unroll
+        for (int w = 0; w < NPG; ++w) stot += red[w * 64 + tid];
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+      for (int c = 0; c < FC; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (j16 == 0) red[pg * 64 + wch * 32 + c * 16 + kg * 4 + e] = qv[c][e];
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (tid < 64) {
+        float q = 0.f;
+#pragma unroll
+        for (int w = 0; w < NPG; ++w) q += red[w * 64 + tid];
+        a.stats[(long)sp * 2 * a.Ng + n0 + tid] = stot;
+        a.stats[(long)sp * 2 * a.Ng + a.Ng + n0 + tid] = q;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < FP; ++p)
+#pragma unroll
+      for (int c = 0; c < FC; ++c) bstore64(ry, outo[p] + (wch * 32 + c * 16 + kg * 4) * 2, outv[c][p]);
+    // tile t+1's halo landed: after it this wave issued tile t-1's stores, tile t's aux loads, tile
+    // t+2's DMA and tile t's stores (compiler-visible stats stores only add to the wait); the
+    // barrier also frees stage t % 3 for tile t+3's DMA, `red` and `hred`
+    constexpr int kEnd = NS + NA + HI + NS;  // vmcnt holds 6 bits: a smaller count only waits longer
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(kEnd < 63 ? kEnd : 63) : "memory");
+  }
+  // the zero-fill DMAs of the last two (absent) tiles may still be landing in the stages
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  if (POST) {
+    float* pr = reinterpret_cast<float*>(hl);  // [NW][2][64]
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float t0 = row16_sum(pq0[c][e]), t1 = POST == 2 ? row16_sum(pq1[c][e]) : 0.f;
+        if (j16 == 0) {
+          const int col = wch * 32 + c * 16 + kg * 4 + e;
+          pr[(pg * 2 + 0) * 64 + col] = t0;
+          pr[(pg * 2 + 1) * 64 + col] = t1;
+        }
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (tid < 128) {
+      const int k = tid >> 6, ch = tid & 63;
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NPG; ++w) t += pr[(w * 2 + k) * 64 + ch];
+      a.ppart[(long)blockIdx.x * 2 * a.Ng + k * a.Ng + n0 + ch] = t;
+    }
+  }
+}
+
 template <int TH, int NW>
 size_t halo_lds_bytes(int head_k = 0) {
   (void)head_k;
@@ -607,7 +1023,60 @@ int halo3_blocks(const FastTNArgs& a) {
   return ntn * G_per;
 }
 
+template <int NW, int POST, int EPI>
+static int launch_halo3r_cfg(const FastTNArgs& a, hipStream_t st) {
+  constexpr int TH = 8;
+  const int tiles_w = a.wc / HW_TW, tiles_h = a.hc / TH;
+  const int n_img = a.M / (a.hc * a.wc);
+  const int n_sp = n_img * tiles_h * tiles_w;
+  const int ntn = a.Ng / 64;
+  int G_per = 256 / ntn;
+  if (G_per < 1) G_per = 1;
+  if (G_per > n_sp) G_per = n_sp;
+  const size_t lds = halo3r_lds_bytes<NW>();
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3r_kernel<NW, POST, EPI>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const unsigned y_bytes = (unsigned)((long)a.M * a.ldy * 2);
+  const long aux_bytes = POST ? (long)a.M * a.ld_aux * 2 : 0;
+  if (aux_bytes >= (1L << 31)) return -1;
+  hipLaunchKernelGGL((halo3r_kernel<NW, POST, EPI>), dim3(ntn * G_per), dim3(64 * NW), lds, st, a, tiles_w, tiles_h,
+                     n_sp, G_per, y_bytes, (unsigned)aux_bytes);
+  return 0;
+}
+
+template <int NW>
+static int launch_halo3r(const FastTNArgs& a, int epi, bool dyn, hipStream_t st) {
+  if (a.head_y) {
+    if (a.post || epi != (kEpiBias | kEpiRelu) || (a.head_k != 1 && a.head_k != 2)) return -1;
+    return a.head_k == 2 ? launch_halo3r_cfg<NW, 0, kEpiBias | kEpiRelu | kEpiHead2>(a, st)
+                         : launch_halo3r_cfg<NW, 0, kEpiBias | kEpiRelu | kEpiHead1>(a, st);
+  }
+  if (a.post == 1) return epi == 0 && !dyn ? launch_halo3r_cfg<NW, 1, 0>(a, st) : launch_halo3r_cfg<NW, 1, kEpiDyn>(a, st);
+  if (a.post == 2) return epi == 0 && !dyn ? launch_halo3r_cfg<NW, 2, 0>(a, st) : launch_halo3r_cfg<NW, 2, kEpiDyn>(a, st);
+  if (!dyn) switch (epi) {
+      case kEpiBias | kEpiRelu: return launch_halo3r_cfg<NW, 0, kEpiBias | kEpiRelu>(a, st);
+      case kEpiStats: return launch_halo3r_cfg<NW, 0, kEpiStats>(a, st);
+      case 0: return launch_halo3r_cfg<NW, 0, 0>(a, st);
+      case kEpiAcc: return launch_halo3r_cfg<NW, 0, kEpiAcc>(a, st);
+      default: break;
+    }
+  return launch_halo3r_cfg<NW, 0, kEpiDyn>(a, st);
+}
+
 int launch_halo3(const FastTNArgs& a, hipStream_t st) {
+  // UNETSEG_HALO_R=1: the register-resident-weight kernel (UNETSEG_HALO_R_NW=4: one wave per SIMD)
+  static const bool v1 = getenv("UNETSEG_HALO_R") == nullptr;
+  static const int rnw = getenv("UNETSEG_HALO_R_NW") ? atoi(getenv("UNETSEG_HALO_R_NW")) : 8;
+  if (!v1) {
+    static const bool dyn_r = getenv("UNETSEG_HALO_EPI_DYN") != nullptr;
+    const int epi_r = (a.bias ? kEpiBias : 0) | (a.relu ? kEpiRelu : 0) | (a.stats ? kEpiStats : 0) |
+                      (a.accumulate ? kEpiAcc : 0);
+    return rnw == 4 ? launch_halo3r<4>(a, epi_r, dyn_r, st) : launch_halo3r<8>(a, epi_r, dyn_r, st);
+  }
   static const int nw = getenv("UNETSEG_HALO_W4") ? 4 : 8;
   // fused dgrad post-ops are separate instantiations: their registers must not cost the plain path
   static const bool dyn = getenv("UNETSEG_HALO_EPI_DYN") != nullptr;
