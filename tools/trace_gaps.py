@@ -3,7 +3,7 @@ non-library kernels (copies / fills) of a training step.
 
     python tools/trace_gaps.py <dir with run_kernel_trace.csv> [steps]
 
-Per step (split at the Adam kernel): the compute stream's summed kernel time, its idle time between
+Per step (split at the stem's input pack): the compute stream's summed kernel time, its idle time between
 consecutive kernels (histogram, and the largest gaps with the kernels on either side), and for every
 copyBuffer / FillFunctor / elementwise launch the kernel before and after it on its stream.
 """
@@ -21,10 +21,11 @@ def main():
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
     ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"], r["Kernel_Name"]) for r in rows)
-    adam = [i for i, k in enumerate(ks) if "adam_kernel" in k[3]]
-    lo, hi = adam[-steps - 1] + 1, adam[-1] + 1
+    # a step starts at the stem input pack (Adam runs once per gradient bucket with --overlap-adam)
+    mark = [i for i, k in enumerate(ks) if "pack_input_stem" in k[3]]
+    lo, hi = mark[-steps], len(ks)
     sel = ks[lo:hi]
-    main_stream = ks[adam[-1]][2]
+    main_stream = ks[mark[-1]][2]
     by = defaultdict(list)
     for k in sel:
         by[k[2]].append(k)

@@ -2,7 +2,7 @@
 
     python tools/trace_streams.py <dir with run_kernel_trace.csv> [steps]
 
-Takes the last `steps` training steps (split at the Adam kernel), and prints per stream: summed
+Takes the last `steps` training steps (split at the stem's input pack), and prints per stream: summed
 kernel time, union-of-intervals wall, and the top kernels by time on each stream; plus the idle
 gaps of the compute stream (time where no kernel of that stream runs).
 """
@@ -18,11 +18,13 @@ def main():
     rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"], r["Kernel_Name"]) for r in rows]
     ks.sort()
-    adam = [i for i, k in enumerate(ks) if "adam_kernel" in k[3]]
-    if len(adam) < steps + 1:
-        print("not enough steps", len(adam))
+    # a step starts at the stem input pack (Adam runs once per gradient bucket with --overlap-adam);
+    # the last step is closed by the final kernel of the trace
+    mark = [i for i, k in enumerate(ks) if "pack_input_stem" in k[3]]
+    if len(mark) < steps:
+        print("not enough steps", len(mark))
         return
-    lo, hi = adam[-steps - 1] + 1, adam[-1] + 1
+    lo, hi = mark[-steps], len(ks)
     sel = ks[lo:hi]
     t0, t1 = sel[0][0], max(k[1] for k in sel)
     wall = (t1 - t0) / 1e6 / steps
