@@ -112,7 +112,8 @@ def run_resnet(ctx, r, x):
     feat1 = ops.bn(ctx, y, st, r.bn1, relu=True)
     h = ops.maxpool(ctx, feat1, r.maxpool.kernel_size, r.maxpool.stride, r.maxpool.ceil_mode)
     feats = [feat1]
-    for layer in (r.layer1, r.layer2, r.layer3, r.layer4):
+    for name, layer in (("layer1", r.layer1), ("layer2", r.layer2), ("layer3", r.layer3), ("layer4", r.layer4)):
+        ops.flush_point(ctx, name)
         for i in range(len(layer)):
             h = run_bottleneck(ctx, layer[i], h)
         feats.append(h)

@@ -37,6 +37,7 @@ def run_resnet_decoder(ctx, m, feats, head=None):
     """unet_resnet.py:92-100 (shared by MultiTaskUNet).  head: the model's 1x1 head conv, fused into
     the last conv's epilogue where the shape allows (ops.pw_head then reuses those logits)"""
     f1, f2, f3, f4, f5 = feats
+    ops.flush_point(ctx, "decoder")
     u = run_unet_up(ctx, m.up_concat4, f4, f5)
     u = run_unet_up(ctx, m.up_concat3, f3, u)
     u = run_unet_up(ctx, m.up_concat2, f2, u)

@@ -133,6 +133,7 @@ class Ctx:
         self.grad_hook = None  # called with a param after its gradient is final (DDP bucketing)
         self.finish_hook = None  # called once the tape is done, before the compute stream joins the side
         self.side = None  # weight-gradient stream, set while backward runs with OVERLAP
+        self.deferred = []  # weight-gradient launches held back until a flush point (defer_wgrad)
 
     def push(self, fn):
         if self.tape is not None:
@@ -157,6 +158,7 @@ class Ctx:
                 fn = tape.pop()
                 fn()
                 del fn
+            self.flush_deferred()
             if self.finish_hook is not None:
                 # the last buckets' collectives / optimizer updates, enqueued before the join below
                 self.finish_hook()
@@ -165,6 +167,10 @@ class Ctx:
                 # everything after backward (optimizer, frees of tape tensors) follows the wgrads
                 lib.stream_wait(self.stream, self.side.cuda_stream)
                 self.side = None
+
+    def flush_deferred(self):
+        while self.deferred:
+            self.deferred.pop(0)()
 
     def param_done(self, *params):
         """report parameters whose gradient is final AND that no later compute-stream kernel of this
@@ -175,6 +181,26 @@ class Ctx:
             for p in params:
                 if p is not None:
                     self.grad_hook(p)
+
+
+#: weight gradients of convs whose output has >= this many pixels per image (the decoder's 256^2 / 512^2
+#: 3x3 convs) are held back in backward until the flush point between the decoder and the encoder
+#: (flush_point): they then run on the side stream beside the encoder's small, latency-bound layers
+#: instead of beside the data gradients of their own layers (0 = off; UNETSEG_WG_DEFER_HW)
+WG_DEFER_HW = int(os.environ.get("UNETSEG_WG_DEFER_HW", "0"))
+#: where the flush marker sits in forward order: "decoder" (before the decoder), "layer4" / "layer3" / "layer2"
+#: (before that encoder layer: in backward the held-back gradients start once that layer's backward is done)
+WG_FLUSH = os.environ.get("UNETSEG_WG_FLUSH", "decoder")
+
+
+def defer_wgrad(ctx, N, Pq, Qq, R, S, x2):
+    return bool(WG_DEFER_HW) and ctx.side is not None and Pq * Qq >= WG_DEFER_HW and R * S > 1
+
+
+def flush_point(ctx, where):
+    """forward marker: in backward, the deferred weight gradients are launched when the tape reaches it"""
+    if WG_DEFER_HW and where == WG_FLUSH:
+        ctx.push(ctx.flush_deferred)
 
 
 def gbuf(ctx, node):
@@ -376,39 +402,45 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
             dYp = torch.zeros(N, Pq, Qq, Kp, dtype=ctx.tdtype, device=dev)
             lib.add(ctx.dt, P(dY), ldp(dY), P(dYp), Kp, M, K, ctx.stream)
             dY = dYp
-        # weight gradient: on the side stream when overlapping (it only needs dY and the inputs,
-        # and nothing in the data-gradient chain reads its output)
         cin = C1 + C2
-        ws_bytes = lib.conv2d_wgrad_workspace(ctx.dt, N, Pq, Qq, Kp, cin, R, S)
-        side = ctx.side
-        if side is not None:
-            lib.stream_wait(side.cuda_stream, ctx.stream)
-            # dY, the inputs and the input prologue's BN coefficients may be freed (compute-stream
-            # order) before the wgrad has run on the side stream, which lags the compute stream
-            for t in (dY, X1, X2) + ((lazy.sc, lazy.sh) if lazy is not None else ()):
-                if t is not None:
-                    t.record_stream(side)
-            ws = workspace(ws_bytes, dev, 1)
-            wst = side.cuda_stream
-        else:
-            ws = workspace(ws_bytes, dev)
-            wst = ctx.stream
-        if Kp != K:
-            dwp = torch.empty(Kp, pc.C, dtype=torch.float32, device=dev)
+
+        def launch_wgrad():
+            # weight gradient: on the side stream when overlapping (it only needs dY and the inputs,
+            # and nothing in the data-gradient chain reads its output)
+            ws_bytes = lib.conv2d_wgrad_workspace(ctx.dt, N, Pq, Qq, Kp, cin, R, S)
+            side = ctx.side
             if side is not None:
-                dwp.record_stream(side)
-            with _probe("wgrad", flops, 1, ("wgrad_padk",) + desc, stream=side):
-                lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), 0, 0, 0, N, H, W, P(dY), Kp, Kp, 1, 1, 1, 0, P(ws),
-                                 ws.numel(), P(dwp), pc.C, 0, wst)
-                lib.add(DT_F32, P(dwp), pc.C, P(pc.conv.weight.grad), pc.C, K, pc.C, wst)
-        elif lazy is not None:
-            with _probe("wgrad", flops, 1, ("wgrad_bnrelu_in",) + desc, stream=side):
-                lib.conv2d_wgrad_bnrelu_in(ctx.dt, P(X1), C1, ldp(X1), N, H, W, P(dY), ldp(dY), K, P(lazy.sc),
-                                           P(lazy.sh), P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, wst)
-        else:
-            with _probe("wgrad", flops, 1, ("wgrad",) + desc, stream=side):
-                lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(dY), ldp(dY), K, R, S,
-                                 stride, pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, wst)
+                lib.stream_wait(side.cuda_stream, ctx.stream)
+                # dY, the inputs and the input prologue's BN coefficients may be freed (compute-stream
+                # order) before the wgrad has run on the side stream, which lags the compute stream
+                for t in (dY, X1, X2) + ((lazy.sc, lazy.sh) if lazy is not None else ()):
+                    if t is not None:
+                        t.record_stream(side)
+                ws = workspace(ws_bytes, dev, 1)
+                wst = side.cuda_stream
+            else:
+                ws = workspace(ws_bytes, dev)
+                wst = ctx.stream
+            if Kp != K:
+                dwp = torch.empty(Kp, pc.C, dtype=torch.float32, device=dev)
+                if side is not None:
+                    dwp.record_stream(side)
+                with _probe("wgrad", flops, 1, ("wgrad_padk",) + desc, stream=side):
+                    lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), 0, 0, 0, N, H, W, P(dY), Kp, Kp, 1, 1, 1, 0, P(ws),
+                                     ws.numel(), P(dwp), pc.C, 0, wst)
+                    lib.add(DT_F32, P(dwp), pc.C, P(pc.conv.weight.grad), pc.C, K, pc.C, wst)
+            elif lazy is not None:
+                with _probe("wgrad", flops, 1, ("wgrad_bnrelu_in",) + desc, stream=side):
+                    lib.conv2d_wgrad_bnrelu_in(ctx.dt, P(X1), C1, ldp(X1), N, H, W, P(dY), ldp(dY), K, P(lazy.sc),
+                                               P(lazy.sh), P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, wst)
+            else:
+                with _probe("wgrad", flops, 1, ("wgrad",) + desc, stream=side):
+                    lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(dY), ldp(dY), K, R, S,
+                                     stride, pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, wst)
+
+        deferred = defer_wgrad(ctx, N, Pq, Qq, R, S, x2)
+        if not deferred:
+            launch_wgrad()
         # data gradient (reads the packed weight pc.wt: the parameter is reported done after it)
         if Kp != K:
             if x1.need_grad:
@@ -433,7 +465,13 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                                  H, W, 0, ctx.stream)
             give_grad(ctx, x1, g[..., :C1])
             give_grad(ctx, x2, g[..., C1:])
-        ctx.param_done(pc.conv.weight, b)
+        if deferred:
+            def late():
+                launch_wgrad()
+                ctx.param_done(pc.conv.weight, b)
+            ctx.deferred.append(late)
+        else:
+            ctx.param_done(pc.conv.weight, b)
 
     ctx.push(bwd)
     return out, st
