@@ -211,9 +211,23 @@ def _key_list(direction, shape):
 
 
 def covered_keys():
+    import os
     keys = set()
-    for direction, shape, _ in CASES.values():
+    for direction, shape, _ in HALO_CASES.values():
         keys.update(_key_list(direction, shape))
+    for direction, shape, expect in CASES.values():
+        if not _gather_ring(expect):
+            keys.update(_key_list(direction, shape))
+            continue
+        old = os.environ.get("UNETSEG_TN_NO_HALO_RING")
+        os.environ["UNETSEG_TN_NO_HALO_RING"] = "1"
+        try:
+            keys.update(_key_list(direction, shape))
+        finally:
+            if old is None:
+                del os.environ["UNETSEG_TN_NO_HALO_RING"]
+            else:
+                os.environ["UNETSEG_TN_NO_HALO_RING"] = old
     return keys
 
 
@@ -256,10 +270,40 @@ def _P(t):
     return 0 if t is None else t.data_ptr()
 
 
+# the halo-A ring (configuration 21: 3x3 stride-1 convs on 8 x 32 spatial tiles, A operand from a
+# per-chunk halo in LDS) takes the 256x128 gather ring's place where it applies (the default); the
+# gather-ring cases of those shapes run with UNETSEG_TN_NO_HALO_RING=1 (read per call)
+HALO_CASES = {
+    "hring_fwd_cat": ("fwd_all", (16, 32, 32, 1024, 2048, 512, 3, 1), ["fwd:ring256x128_halo"]),  # up_concat4.conv1
+    "hring_fwd_cat_c1_128": ("fwd_all", (16, 64, 64, 128, 64, 256, 3, 1), ["fwd:ring256x128_halo"]),
+    "hring_fwd_stats": ("fwd_stats", (16, 64, 64, 256, 0, 256, 3, 1), ["fwd:ring256x128_halo"]),
+    "hring_fwd_ng192": ("fwd_all", (16, 64, 64, 128, 0, 192, 3, 1), ["fwd:ring256x128_halo"]),
+    "hring_dgrad": ("dgrad", (16, 64, 64, 256, 0, 256, 3, 1), ["dgrad:ring256x128_halo"]),
+    "hring_dgrad_cat": ("dgrad", (16, 128, 128, 256, 256, 128, 3, 1), ["dgrad:ring256x128_halo"]),  # up_concat2.conv1
+    "hring_post1": ("post1", (16, 32, 32, 512, 0, 512, 3, 1), ["dgrad_post1:ring256x128_halo"]),
+    "hring_post2": ("post2", (16, 64, 64, 128, 0, 128, 3, 1), ["dgrad_post2:ring256x128_halo"]),
+}
+
+
+def _gather_ring(expect):
+    """a case written for the 256x128 gather ring on a shape the halo-A ring now takes"""
+    return bool(expect) and any(k is not None and k.endswith("ring256x128_t9") for k in expect)
+
+
+@pytest.mark.parametrize("cid", list(HALO_CASES))
+def test_halo_ring_case(cid):
+    _run_case(cid, *HALO_CASES[cid])
+
+
 @pytest.mark.parametrize("cid", list(CASES))
-def test_config_case(cid):
+def test_config_case(cid, monkeypatch):
+    if _gather_ring(CASES[cid][2]):
+        monkeypatch.setenv("UNETSEG_TN_NO_HALO_RING", "1")
+    _run_case(cid, *CASES[cid])
+
+
+def _run_case(cid, direction, shape, expect):
     from unetseg_hip.lib import DT_BF16, lib
-    direction, shape, expect = CASES[cid]
     keys = _key_list(direction, shape)
     if expect is not None:
         got = [k for k in keys if k is not None]

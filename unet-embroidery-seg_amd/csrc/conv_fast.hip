@@ -13,6 +13,7 @@
 //  * wgrad: pixels are consumed 32 per K step along image rows (Q % 32 == 0), so (n, p, q0) of a
 //    K step is scalar; fragments come from LDS with ds_read_b64_tr_b16.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "conv_fast.h"
@@ -37,9 +38,17 @@ constexpr int tn_waves_per_simd() {
 
 // byte offset of the input-prologue coefficients in the TN kernel's dynamic LDS: after the operand
 // stages or the epilogue's transpose tiles + stats scratch, whichever is larger
-template <int BM, int BN, int NWM, int NWN, int ST>
+// halo-A ring (HA): 16-B chunks of one (padded) halo stage -- every wave issues the same number of
+// halo DMA instructions, so the stage is rounded up to whole instructions of the block
+template <int BM, int NWM, int NWN>
+constexpr int kHaloChunks() {
+  constexpr int NT = 64 * NWM * NWN;
+  return ((BM / 32 + 2) * 34 * 8 + NT - 1) / NT * NT;
+}
+template <int BM, int BN, int NWM, int NWN, int ST, bool HA = false>
 constexpr size_t kPreOff() {
-  constexpr size_t stages = (size_t)(ST == 1 || ST == 5 ? 1 : ST >= 13 ? ST - 10 : 2) * (BM + BN) * 8 * 16;
+  constexpr size_t stages = HA ? ((size_t)2 * kHaloChunks<BM, NWM, NWN>() + (size_t)(ST - 10) * BN * 8) * 16
+                               : (size_t)(ST == 1 || ST == 5 ? 1 : ST >= 13 ? ST - 10 : 2) * (BM + BN) * 8 * 16;
   constexpr size_t epi = (size_t)NWM * NWN * 64 * ((BN / NWN) * 2 + 16) + 2 * NWM * BN * 4;
   return ((stages > epi ? stages : epi) + 15) / 16 * 16;
 }
@@ -52,7 +61,8 @@ constexpr size_t kPreOff() {
 // PRE: the input prologue of FastTNArgs (x1 = BN input z, staged as relu(z*in_sc + in_sh) between the
 // global load and the LDS store); the per-channel coefficients sit in LDS after the tile stages.
 // The tile body: did = this block's linear id among gx * gy tiles (gy column tiles per row tile).
-template <int BM, int BN, int NWM, int NWN, int ST, bool POST, int TAPS, bool PRE>
+// HA (halo A operand, TAPS == 9 on the LDS-DMA ring): see the K loop below.
+template <int BM, int BN, int NWM, int NWN, int ST, bool POST, int TAPS, bool PRE, bool HA = false>
 __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did, const int gx, const int gy) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int WTM = BM / NWM, WTN = BN / NWN;
@@ -284,7 +294,142 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
     }
   };
 
-  if constexpr (kDMA && TAPS > 0) {
+  if constexpr (HA) {
+    // ---- halo-A ring: 3x3 stride-1 "same" convolutions whose BM-row tile is a TRH x 32 spatial
+    // block (a.t2d == TRH).  Per 64-channel chunk the (TRH+2) x 34 halo of the tile is LDS-DMA'd
+    // ONCE (double buffered, the next chunk's halo in flight during this chunk's nine taps) and the
+    // nine taps read their A fragments from it at a uniform pixel shift; only the weights stream
+    // through the NS-stage ring, one tap per K step.  Per chunk that is ~43 KiB of A DMA instead of
+    // 9 x 32 KiB of re-gathered tap rows: 2.3x fewer DMA instructions per MFMA than the gather ring.
+    static_assert(TAPS == 9 && kDMA && !PRE && B_PER == 2, "halo-A ring: 3x3 taps, weights in row pairs");
+    constexpr int NS = ST - 10;
+    constexpr int TRH = BM / 32;
+    constexpr int HPIX = (TRH + 2) * 34;
+    constexpr int HST = kHaloChunks<BM, NWM, NWN>();  // 16-B chunks per halo stage (padded)
+    constexpr int HI = HST / NT;                       // halo DMA instructions per wave (every wave)
+    constexpr int WST = BN * 8;                        // 16-B chunks per weight stage
+    constexpr int WP = B_PER;                          // weight DMA instructions per wave per K step
+    static_assert(HI % 2 == 0, "halo rows are issued in pairs");
+    static_assert(WP * (NS - 2) + HI <= 63, "vmcnt range");
+    // this block's spatial tile (row_pix with t2d == TRH: tiles of TRH image rows x 32 columns,
+    // stacked over the images; hc % TRH == 0, so a tile never straddles two images)
+    const int tpr = a.wc >> 5;
+    const int tt = m0 / BM;
+    const int rest = tt / tpr, twi = tt - rest * tpr;
+    const int hg = rest * TRH;  // first row of the tile in the stacked (N * hc) row space
+    const int nb = hg / a.hc, h0 = hg - nb * a.hc, w0 = twi * 32;
+    const unsigned pb1 = a.x1_bytes / (unsigned)a.ldc1b;
+    const unsigned pb2 = a.x2 ? a.x2_bytes / (unsigned)a.ldc2b : 0u;
+    const unsigned pbad = (pb1 > pb2 ? pb1 : pb2) + 1u;
+    // this lane's halo DMA slots: source pixel (or pbad: outside the image / past the halo) and the
+    // swizzled source chunk; LDS slot (hp, lane & 7) holds chunk (lane & 7) ^ (hp & 7)
+    unsigned hvp[HI], hsw[HI];
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const int idx = (i * (NWM * NWN) + wid) * 64 + lane;
+      const int hp = idx >> 3;
+      const int hr = hp / 34, hcol = hp - hr * 34;
+      const int h = h0 - 1 + hr, w = w0 - 1 + hcol;
+      const bool ok = hp < HPIX && h >= 0 && h < a.H && w >= 0 && w < a.W;
+      hvp[i] = ok ? (unsigned)((nb * a.H + h) * a.W + w) : pbad;
+      hsw[i] = (unsigned)(((lane & 7) ^ (hp & 7)) * 16);
+    }
+    unsigned tw[9];  // weight byte offset of each tap
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int jr = t / 3, js = t - jr * 3;
+      tw[t] = (unsigned)(((a.r0 + a.rs * jr) * a.S + (a.s0 + a.ss * js)) * a.cin) * 2u;
+    }
+    // A fragment p of this lane: tile pixel (row wm * WTM / 32 + p / 2, column (p & 1) * 16 + lane % 16)
+    // -> halo pixel at the centre tap; a tap adds the uniform shift dh * 34 + dw
+    static_assert(WTM == 64 && FP == 4, "64-row wave tiles: two image rows of 32 pixels");
+    int hq[FP];
+#pragma unroll
+    for (int p = 0; p < FP; ++p) hq[p] = (wm * 2 + (p >> 1) + 1) * 34 + (p & 1) * 16 + (lane & 15) + 1;
+    const int chA = lane >> 4;  // 16-B chunk of the first K half (the second is chA ^ 4)
+    unsigned foffW[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int r = lane & 15;
+      foffW[kk] = (unsigned)((wn * WTN + r) * 128 + ((kk * 4 + (lane >> 4)) ^ ((r >> 1) & 7)) * 16);
+    }
+    const unsigned hbase = lds_addr(lds);
+    const unsigned wbase = hbase + 2u * HST * 16u;
+    const int nch = a.cin >> 6;
+    auto issue_halo = [&](int c, int hs) {
+      const bool live = c < nch;
+      const int c64 = c * 64;
+      const bool first = c64 < a.c1;
+      const __amdgpu_buffer_rsrc_t rx = srd_u(first ? a.x1 : a.x2, !live ? 0u : first ? a.x1_bytes : a.x2_bytes);
+      const unsigned ldcb = first ? (unsigned)a.ldc1b : (unsigned)a.ldc2b;
+      const unsigned soff = __builtin_amdgcn_readfirstlane(live ? (unsigned)(first ? c64 : c64 - a.c1) * 2u : 0u);
+      const unsigned sb = __builtin_amdgcn_readfirstlane(hbase + (unsigned)(hs * HST * 16) + (unsigned)(wid * 1024));
+#pragma unroll
+      for (int i = 0; i < HI; i += 2)
+        dma16x2<NT * 16>(rx, sb + (unsigned)(i * NT * 16), __umul24(hvp[i], ldcb) + hsw[i],
+                         __umul24(hvp[i + 1], ldcb) + hsw[i + 1], soff);
+    };
+    auto issue_w = [&](int c, int t, int stage) {
+      const bool live = c < nch;
+      const __amdgpu_buffer_rsrc_t rwx = srd_u(a.wt, live ? a.w_bytes : 0u);
+      const unsigned wsoff = __builtin_amdgcn_readfirstlane(live ? tw[t] + (unsigned)(c * 64) * 2u : 0u);
+      const unsigned sb = __builtin_amdgcn_readfirstlane(wbase + (unsigned)(stage * WST * 16) + (unsigned)(wid * 8 * 128));
+      dma16x2<RSTEP * 128>(rwx, sb, boff[0], boff[1], wsoff);
+    };
+    // wait for this step's weight stage (and, at a chunk's first tap, its halo): the younger DMAs
+    // still in flight are the NS-2 later weight steps plus the next chunk's halo when it was issued
+    // after this step's weights (taps 1 .. NS-1 of a chunk)
+    auto wait_step = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      constexpr int n = WP * (NS - 2) + ((t >= 1 && t <= NS - 1) ? HI : 0);
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(n) : "memory");
+    };
+    issue_halo(0, 0);
+#pragma unroll
+    for (int s0 = 0; s0 < NS - 1; ++s0) issue_w(s0 / 9, s0 % 9, s0);
+    int stage = 0;
+    for (int c = 0; c < nch; ++c) {
+      const char* hs = reinterpret_cast<const char*>(lds) + (c & 1) * HST * 16;
+      auto step = [&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        wait_step(tc);
+        const int jr = t / 3, js = t - jr * 3;
+        const int shift = (a.dh0 + a.dhs * jr) * 34 + (a.dw0 + a.dws * js);
+        unsigned ab[FP];
+#pragma unroll
+        for (int p = 0; p < FP; ++p) {
+          const int hp = hq[p] + shift;
+          ab[p] = (unsigned)(hp * 128 + ((chA ^ (hp & 7)) * 16));
+        }
+        const char* ws = reinterpret_cast<const char*>(lds) + 2 * HST * 16 + stage * WST * 16;
+        bf16x8 pf[FP], wf[FC];
+#pragma unroll
+        for (int p = 0; p < FP; ++p) pf[p] = *reinterpret_cast<const bf16x8*>(hs + ab[p]);
+#pragma unroll
+        for (int cc = 0; cc < FC; ++cc) wf[cc] = *reinterpret_cast<const bf16x8*>(ws + foffW[0] + cc * 2048);
+        const int st2 = stage == 0 ? NS - 1 : stage - 1;  // (stage + NS - 1) % NS
+        issue_w(c + (t + NS - 1) / 9, (t + NS - 1) % 9, st2);
+        if constexpr (t == 0) issue_halo(c + 1, (c + 1) & 1);
+        mfmas(pf, wf);
+#pragma unroll
+        for (int p = 0; p < FP; ++p) pf[p] = *reinterpret_cast<const bf16x8*>(hs + (ab[p] ^ 64u));
+#pragma unroll
+        for (int cc = 0; cc < FC; ++cc) wf[cc] = *reinterpret_cast<const bf16x8*>(ws + foffW[1] + cc * 2048);
+        mfmas(pf, wf);
+        stage = stage == NS - 1 ? 0 : stage + 1;
+      };
+      step(std::integral_constant<int, 0>{});
+      step(std::integral_constant<int, 1>{});
+      step(std::integral_constant<int, 2>{});
+      step(std::integral_constant<int, 3>{});
+      step(std::integral_constant<int, 4>{});
+      step(std::integral_constant<int, 5>{});
+      step(std::integral_constant<int, 6>{});
+      step(std::integral_constant<int, 7>{});
+      step(std::integral_constant<int, 8>{});
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  } else if constexpr (kDMA && TAPS > 0) {
     constexpr int NS = ST - 10, PER = A_PER + B_PER;
     static_assert(NS >= 3 && PER * (NS - 2) <= 63, "vmcnt range");
     static_assert(A_PER % 2 == 0 && (B_PER % 2 == 0 || B_PER == 1), "rows are issued in pairs");
@@ -639,9 +784,9 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
   }
 }
 
-template <int BM, int BN, int NWM, int NWN, int ST, bool POST, int TAPS = 0, bool PRE = false>
+template <int BM, int BN, int NWM, int NWN, int ST, bool POST, int TAPS = 0, bool PRE = false, bool HA = false>
 __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN, ST>())) void tn_fast_kernel(FastTNArgs a) {
-  tn_fast_body<BM, BN, NWM, NWN, ST, POST, TAPS, PRE>(a, blockIdx.x + gridDim.x * blockIdx.y, gridDim.x, gridDim.y);
+  tn_fast_body<BM, BN, NWM, NWN, ST, POST, TAPS, PRE, HA>(a, blockIdx.x + gridDim.x * blockIdx.y, gridDim.x, gridDim.y);
 }
 
 // Several independent GEMMs of one configuration in one launch: the output-parity classes of a
@@ -946,29 +1091,30 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     }
 }
 
-template <int BM, int BN, int NWM, int NWN, int ST, bool POST = false, int TAPS = 0, bool PRE = false>
+template <int BM, int BN, int NWM, int NWN, int ST, bool POST = false, int TAPS = 0, bool PRE = false, bool HA = false>
 int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   constexpr int NT = 64 * NWM * NWN;
   // operand stages, or the epilogue's per-wave transpose tiles + stats scratch if larger; then the
   // input-prologue coefficients (PRE)
   constexpr size_t kMaxPre = 2 * 2048 * 4;
-  const size_t lds = kPreOff<BM, BN, NWM, NWN, ST>() + (PRE ? (size_t)2 * a.c1 * 4 : 0);
+  constexpr size_t off = kPreOff<BM, BN, NWM, NWN, ST, HA>();
+  const size_t lds = off + (PRE ? (size_t)2 * a.c1 * 4 : 0);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_fast_kernel<BM, BN, NWM, NWN, ST, POST, TAPS, PRE>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(kPreOff<BM, BN, NWM, NWN, ST>() + (PRE ? kMaxPre : 0)));
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_fast_kernel<BM, BN, NWM, NWN, ST, POST, TAPS, PRE, HA>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(off + (PRE ? kMaxPre : 0)));
     attr = true;
   }
   dim3 grid(ceil_div(a.M, BM), ceil_div(a.Ng, BN), 1);
   FastTNArgs b = a;
   constexpr int TR = BM / 32;
-  // 2D spatial tiles measured slower than row-major tiles with the chunk-outer K order: opt-in
+  // 2D spatial tiles measured slower than row-major tiles with the chunk-outer K order: opt-in for
+  // the gather ring; the halo-A ring is built on them
   static const bool t2d = getenv("UNETSEG_T2D") != nullptr;
-  b.t2d = (t2d && a.nr * a.ns > 1 && a.wc % 32 == 0 && a.wc > 32 && a.hc % TR == 0) ? TR : 0;
+  b.t2d = (HA || (t2d && a.nr * a.ns > 1 && a.wc % 32 == 0 && a.wc > 32 && a.hc % TR == 0)) ? TR : 0;
   static const int sched = getenv("UNETSEG_TN_SCHED") ? atoi(getenv("UNETSEG_TN_SCHED")) : 0;
   b.sched = sched;
-  hipLaunchKernelGGL((tn_fast_kernel<BM, BN, NWM, NWN, ST, POST, TAPS, PRE>), grid, dim3(NT), lds, st, b);
+  hipLaunchKernelGGL((tn_fast_kernel<BM, BN, NWM, NWN, ST, POST, TAPS, PRE, HA>), grid, dim3(NT), lds, st, b);
   return 0;
 }
 
@@ -1028,9 +1174,30 @@ static int launch_tn_dma(const FastTNArgs& a, hipStream_t st) {
 // 7-10: the same tiles on the LDS-DMA ring.  Measured (tools/gpu_cfg_sweep.sh): the 256x128 ring
 // (3 stages) beats the register-staged 256x128 by 3-8 % on every large layer; the 64x128 ring (4
 // stages) is 15 % faster on deep-K small-M layers (3x3 at 16x16, 72 K steps) but slower on short K.
+// The halo-A ring (configuration 21) serves a 3x3 stride-1 "same" conv whose output grid tiles into
+// 8 x 32 spatial blocks, in place of the 256x128 gather ring.
+static bool halo_a_ok(const FastTNArgs& a) {
+  // default since the round-3 A/B (+1.8 % end to end); UNETSEG_TN_NO_HALO_RING=1 keeps the gather
+  // ring -- read per call so a test can run both rings in one process
+  if (getenv("UNETSEG_TN_NO_HALO_RING") != nullptr || a.in_sc || a.nr != 3 || a.ns != 3 || a.istride != 1) return false;
+  if (a.dhs * a.dhs != 1 || a.dws * a.dws != 1) return false;
+  const int dh_lo = a.dhs > 0 ? a.dh0 : a.dh0 - 2, dw_lo = a.dws > 0 ? a.dw0 : a.dw0 - 2;
+  if (dh_lo != -1 || dw_lo != -1) return false;  // one halo pixel on every side
+  if (a.H != a.hc || a.W != a.wc || a.hc % 8 || a.wc % 32) return false;
+  return tn_taps(a) == 9;
+}
+
+static int tn_config_base(const FastTNArgs& a);
+
 static int tn_config(const FastTNArgs& a) {
-  if (const char* e = getenv("UNETSEG_TN_CFG")) {  // experiments: force a configuration (1..14)
+  const int c = tn_config_base(a);
+  return (c == 7 && halo_a_ok(a)) ? 21 : c;
+}
+
+static int tn_config_base(const FastTNArgs& a) {
+  if (const char* e = getenv("UNETSEG_TN_CFG")) {  // experiments: force a configuration (1..14, 19-21)
     const int c = atoi(e);
+    if (c == 21) return 7;  // the halo-A ring where it applies (tn_config), else the gather ring
     if (((c >= 1 && c <= 14) || c == 19 || c == 20) && !(a.in_sc && c >= 7 && c <= 14)) return c;
   }
   static const bool no_dma_env = getenv("UNETSEG_TN_NO_DMA") != nullptr;
@@ -1062,7 +1229,7 @@ static int tn_config(const FastTNArgs& a) {
 // row tile (BM) of each TN configuration
 static int tn_cfg_bm(int cfg) {
   switch (cfg) {
-    case 1: case 2: case 7: case 11: case 14: return 256;
+    case 1: case 2: case 7: case 11: case 14: case 21: return 256;
     case 5: case 9: return 64;
     default: return 128;
   }
@@ -1124,6 +1291,14 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 14: return launch_tn_dma<256, 64, 4, 2, 13>(a, st);
     case 19: return a.post ? launch_tn_cfg<128, 128, 2, 2, 5, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 5>(a, st);
     case 20: return a.post ? launch_tn_cfg<128, 64, 2, 2, 5, true>(a, st) : launch_tn_cfg<128, 64, 2, 2, 5>(a, st);
+    case 21: {
+      // weight ring depth: 3 stages (144 KiB of LDS with the two halo stages); 4 fill all 160 KiB
+      static const bool ns4 = getenv("UNETSEG_TN_HALO_NS4") != nullptr;
+      if (ns4) return a.post ? launch_tn_cfg<256, 128, 4, 2, 14, true, 9, false, true>(a, st)
+                             : launch_tn_cfg<256, 128, 4, 2, 14, false, 9, false, true>(a, st);
+      return a.post ? launch_tn_cfg<256, 128, 4, 2, 13, true, 9, false, true>(a, st)
+                    : launch_tn_cfg<256, 128, 4, 2, 13, false, 9, false, true>(a, st);
+    }
     default: return a.post ? launch_tn_cfg<128, 128, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 3>(a, st);
   }
 }

@@ -4,6 +4,7 @@ from __future__ import annotations
 import torch
 
 from .lib import lib
+from . import ops
 from .ops import P
 
 
@@ -78,13 +79,29 @@ class FusedAdam(torch.optim.Optimizer):
             self.model._mark_prepacked()
 
     def zero_grad(self, set_to_none: bool = True):  # keep the grads as arena views
-        self.model._attach_grads()
-        self.model._flat_grad.zero_()
+        m = self.model
+        m._attach_grads()
+        g = m._flat_grad
+        if ops.OVERLAP and g.is_cuda and not torch.cuda.is_current_stream_capturing():
+            # nothing writes the arena before backward: clear it on the weight-gradient stream, idle
+            # during the forward, instead of in front of the forward on the compute stream; the
+            # backward (and any step / grad read before it) waits for this event
+            cur = torch.cuda.current_stream(g.device)
+            side = ops.side_stream(g.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                g.zero_()
+            ev = torch.cuda.Event()
+            ev.record(side)
+            m._grad_zero_event = ev
+        else:
+            g.zero_()
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale=None):
         loss = closure() if closure is not None else None
         m = self.model
+        m._wait_grad_zero()
         if self._applied:
             if grad_scale is not None:
                 raise ValueError("FusedAdam(overlap=True) cannot take a grad scale (the update ran in backward)")

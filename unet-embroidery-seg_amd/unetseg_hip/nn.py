@@ -141,6 +141,7 @@ class _ModelFn(torch.autograd.Function):
         model = fctx.model
         for holder, g in zip(ctx.out_holders, grads):
             holder["grad"] = g
+        model._wait_grad_zero()
         model._attach_grads()
         ctx.grad_hook = model._grad_hook
         ctx.finish_hook = model._after_backward  # inside backward: before the streams join
@@ -187,6 +188,13 @@ class HipModel(nn.Module):
                 cpad = 8 if m.in_channels < 8 else None
                 m._pc = ops.PackedConv(m, cpad)
                 self._packed.append(m._pc)
+
+    def _wait_grad_zero(self):
+        """the compute stream waits for a gradient-arena clear enqueued on the side stream (FusedAdam.zero_grad)"""
+        ev = getattr(self, "_grad_zero_event", None)
+        if ev is not None:
+            torch.cuda.current_stream(self._flat_grad.device).wait_event(ev)
+            self._grad_zero_event = None
 
     def _repoint(self):
         for p in self._param_list:
