@@ -282,12 +282,17 @@ HALO_CASES = {
     "hring_dgrad_cat": ("dgrad", (16, 128, 128, 256, 256, 128, 3, 1), ["dgrad:ring256x128_halo"]),  # up_concat2.conv1
     "hring_post1": ("post1", (16, 32, 32, 512, 0, 512, 3, 1), ["dgrad_post1:ring256x128_halo"]),
     "hring_post2": ("post2", (16, 64, 64, 128, 0, 128, 3, 1), ["dgrad_post2:ring256x128_halo"]),
+    # <= 64 output channels: 256x64 tiles (up_concat1.conv1 192 -> 64 at 256^2, here at 64^2)
+    "hring64_fwd_cat": ("fwd_all", (2, 64, 64, 64, 128, 64, 3, 1), ["fwd:ring256x64_halo"]),
+    "hring64_fwd_stats_k40": ("fwd_stats", (2, 64, 96, 192, 0, 40, 3, 1), ["fwd:ring256x64_halo"]),
+    "hring64_dgrad": ("dgrad", (2, 64, 64, 64, 0, 128, 3, 1), ["dgrad:ring256x64_halo"]),
+    "hring64_post1": ("post1", (2, 32, 64, 64, 0, 128, 3, 1), ["dgrad_post1:ring256x64_halo"]),
 }
 
 
 def _gather_ring(expect):
     """a case written for the 256x128 gather ring on a shape the halo-A ring now takes"""
-    return bool(expect) and any(k is not None and k.endswith("ring256x128_t9") for k in expect)
+    return bool(expect) and any(k is not None and k.endswith(("ring256x128_t9", "ring128x64_t9")) for k in expect)
 
 
 @pytest.mark.parametrize("cid", list(HALO_CASES))
