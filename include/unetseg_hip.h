@@ -124,6 +124,17 @@ int unetseg_conv2d_dgrad_post(int dtype, const void* dy, int ldy, int n, int p, 
                               int cin, int r, int s, int stride, int pad, void* dx, int ldx, int h, int w, int post,
                               const void* aux, int ld_aux, const float* psc, const float* psh, const float* pmean,
                               const float* pinv, float* part, int rows, void* stream);
+/* 1x1 stride-1 data gradient accumulated onto the residual gradient already in dx (ldx == cin), with the
+   residual BN-add-ReLU backward's first pass in its epilogue (model/resnet_backbone.py:88,110-113: the
+   next block's conv1 is the last consumer of the block output): dx = mask * bf16(dgrad + dx), mask =
+   the packed ReLU bits written by unetseg_bn_apply_mask, part[rows][2 or 3][cin] = (sum d,
+   sum d * (y1 - mean1) * inv1 [, sum d * (y2 - mean2) * inv2]) per row tile (y2 = the downsample
+   branch's BN input, NULL: none).  Replaces unetseg_bn_bwd_reduce over dx.  part == NULL: returns rows,
+   or 0 when the shape has no fused kernel (bf16 only). */
+int unetseg_conv2d_dgrad_post_res(int dtype, const void* dy, int ldy, int n, int p, int q, const void* wt, int cout,
+                                  int cin, void* dx, int ldx, const void* y1, int ld1, const float* mean1,
+                                  const float* inv1, const unsigned char* mbits, const void* y2, int ld2,
+                                  const float* mean2, const float* inv2, float* part, int rows, void* stream);
 size_t unetseg_conv2d_wgrad_workspace(int dtype, int n, int p, int q, int cout, int cin, int r, int s);
 /* dw fp32 [cout][dw_c][r][s] (PyTorch layout) (+)= sum_pix dy x; ws of the size queried above */
 int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h,
@@ -202,6 +213,11 @@ int unetseg_colsum_finalize(const float* part, int C, int G, float* out, int acc
    unetseg_conv2d_dgrad_post (model/resnet_backbone.py BatchNorm2d backward, unet_resnet.py ReLU) */
 int unetseg_bn_bwd_finalize_rows(const float* part, int C, int G, long M, const float* g1, const float* inv1,
                                  float* dg1, float* db1, float* coef, void* stream);
+/* the same for the residual post-op's part[G][1+nbranch][C] (unetseg_conv2d_dgrad_post_res): coefficients
+   of both branches as unetseg_bn_bwd_finalize */
+int unetseg_bn_bwd_finalize_rows_res(const float* part, int C, int G, long M, int nbranch, const float* g1,
+                                     const float* inv1, float* dg1, float* db1, const float* g2, const float* inv2,
+                                     float* dg2, float* db2, float* coef, void* stream);
 int unetseg_colsum_rows(const float* part, int C, int G, int k, float* out, int accumulate, void* stream);
 
 /* ---- pooling / resampling (nn.MaxPool2d: model/resnet_backbone.py:131, model/unet_plain.py:25,

@@ -210,9 +210,17 @@ def _key_list(direction, shape):
     return introspect.call_configs((d, N, H, W, C1, C2, K, R, R, s, R // 2, C1, C2))
 
 
+# residual post-op data gradients (dgrad_post3): the configurations tests/test_gpu_post_res.py drives
+# (N, H, W, K, C) of its SHAPES with a fixed configuration
+POST3_SHAPES = [(16, 128, 128, 64, 256), (4, 64, 64, 128, 512), (16, 32, 32, 256, 1024), (16, 16, 16, 512, 2048)]
+
+
 def covered_keys():
     import os
+    from unetseg_hip import introspect
     keys = set()
+    for N, H, W, K, C in POST3_SHAPES:
+        keys.update(introspect.call_configs(("dgrad_post3", N, H, W, C, 0, K, 1, 1, 1, 0, C, 0)))
     for direction, shape, _ in HALO_CASES.values():
         keys.update(_key_list(direction, shape))
     for direction, shape, expect in CASES.values():

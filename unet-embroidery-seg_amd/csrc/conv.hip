@@ -1156,6 +1156,42 @@ UNETSEG_API int unetseg_conv2d_dgrad_post(int dtype, const void* dy, int ldy, in
   return 0;
 }
 
+// Data gradient of a 1x1 stride-1 conv accumulated onto the residual gradient already in dx, with the
+// residual-BN backward's first pass in the epilogue (post 3, conv_fast.h): dx = mask * bf16(dgrad + dx),
+// mask = the block output's packed ReLU bits (unetseg_bn_apply_mask), part[tile][2 or 3][cin] = sum d,
+// sum d * xhat1 [, sum d * xhat2] with xhat_b = (y_b - mean_b) * inv_b.  Replaces the separate
+// unetseg_bn_bwd_reduce pass over dx of model/resnet_backbone.py:110-113 (bn3 + residual add + ReLU)
+// when this conv (the next block's conv1, :88) is the last consumer to deliver its gradient.
+// part == NULL: returns the partial rows a call writes, or 0 when the shape has no fused kernel.
+UNETSEG_API int unetseg_conv2d_dgrad_post_res(int dtype, const void* dy, int ldy, int n, int p, int q, const void* wt,
+                                              int cout, int cin, void* dx, int ldx, const void* y1, int ld1,
+                                              const float* mean1, const float* inv1, const unsigned char* mbits,
+                                              const void* y2, int ld2, const float* mean2, const float* inv2,
+                                              float* part, int rows, void* stream) {
+  if (dtype != DT_BF16 || n <= 0 || p <= 0 || q <= 0 || cout % 8 || ldy % 8 || cin % 8 || ldx != cin) return 0;
+  IgemmArgs a;
+  if (!dgrad_classes(dy ? dy : kSomePtr, ldy, n, p, q, wt ? wt : kSomePtr, cout, cin, 1, 1, 1, 0,
+                     dx ? dx : const_cast<void*>(kSomePtr), ldx, p, q, 0, 0, a) || a.M <= 0)
+    return 0;
+  FastTNArgs f;
+  if (!fast_tn_args(a, f)) return 0;
+  f.post = 3;
+  f.accumulate = 0;  // the residual gradient is added in registers before the mask
+  if (!tn_fast_post_res_ok(f)) return 0;
+  const int total = tn_fast_post_rows(f);
+  if (!part) return total;
+  US_CHECK_ARG(dy && wt && dx && y1 && mean1 && inv1 && mbits, "conv2d_dgrad_post_res: null pointer");
+  US_CHECK_ARG(!y2 || (mean2 && inv2 && ld2 >= cin), "conv2d_dgrad_post_res: second branch needs y2, mean2, inv2");
+  US_CHECK_ARG(ld1 >= cin, "conv2d_dgrad_post_res: ld1 < cin");
+  US_CHECK_ARG(rows == total, "conv2d_dgrad_post_res: rows %d != %d", rows, total);
+  f.aux = y1; f.ld_aux = ld1; f.pmean = mean1; f.pinv = inv1; f.mbits = mbits;
+  f.aux2 = y2; f.ld_aux2 = ld2; f.pmean2 = mean2; f.pinv2 = inv2;
+  f.ppart = part;
+  US_CHECK_ARG(launch_tn_fast(f, (hipStream_t)stream) == 0, "conv2d_dgrad_post_res: no fused kernel");
+  US_LAUNCH_CHECK("conv2d_dgrad_post_res");
+  return 0;
+}
+
 // Configuration of each output-parity class of unetseg_conv2d_dgrad / _dgrad_post:
 // cfg_out[ph * stride + pw] (kCfg* codes; -1 = class not launched), taps_out likewise (may be NULL).
 // Returns the number of classes launched.

@@ -40,6 +40,17 @@ struct FastTNArgs {
   const float* pmean;
   const float* pinv;
   float* ppart;
+  // post 3 (residual-BN backward, the data gradient accumulated in registers): aux = the BN input z,
+  // pmean / pinv its batch statistics, mbits the packed ReLU mask of the block output (the
+  // unetseg_bn_apply_mask layout [M][Ng/8]), aux2 / ld_aux2 / pmean2 / pinv2 the downsample branch's BN
+  // input and statistics (aux2 NULL: none).  y holds the residual gradient already delivered; what is
+  // stored is d = mask * bf16(bf16(dgrad) + y), and ppart[tile][2 or 3][Ng] = sum d, sum d * xhat1
+  // [, sum d * xhat2].
+  const unsigned char* mbits;
+  const void* aux2;
+  int ld_aux2;
+  const float* pmean2;
+  const float* pinv2;
   int t2d;  // rows of a 2D spatial tile (BM = t2d x 32 pixels), 0 = row-major GEMM rows (set by the launcher)
   // input prologue: x1 is the producer's BN input z, the conv reads relu(z * in_sc[c] + in_sh[c])
   // (its BN-ReLU output, never materialised); register-staged configurations only, x2 == NULL
@@ -104,6 +115,7 @@ int tn_multi_tile_m(const FastTNArgs* fs, int n);
 int launch_tn_multi(const FastTNArgs* fs, int n, hipStream_t st);
 int tn_fast_tile_m(const FastTNArgs& a);
 int tn_fast_post_rows(const FastTNArgs& a);  // partial rows (ppart) a launch_tn_fast call writes
+bool tn_fast_post_res_ok(const FastTNArgs& a);  // the configuration has a post-3 (residual) instantiation
 int halo3_blocks(const FastTNArgs& a);
 bool halo3_ok(const FastTNArgs& a);
 int launch_halo3(const FastTNArgs& a, hipStream_t st);

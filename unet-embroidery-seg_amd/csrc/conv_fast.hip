@@ -49,7 +49,7 @@ template <int BM, int BN, int NWM, int NWN, int ST, bool HA = false>
 constexpr size_t kPreOff() {
   constexpr size_t stages = HA ? ((size_t)2 * kHaloChunks<BM, NWM, NWN>() + (size_t)(ST - 10) * BN * 8) * 16
                                : (size_t)(ST == 1 || ST == 5 ? 1 : ST >= 13 ? ST - 10 : 2) * (BM + BN) * 8 * 16;
-  constexpr size_t epi = (size_t)NWM * NWN * 64 * ((BN / NWN) * 2 + 16) + 2 * NWM * BN * 4;
+  constexpr size_t epi = (size_t)NWM * NWN * 64 * ((BN / NWN) * 2 + 16) + 3 * NWM * BN * 4;
   return ((stages > epi ? stages : epi) + 15) / 16 * 16;
 }
 
@@ -62,7 +62,7 @@ constexpr size_t kPreOff() {
 // global load and the LDS store); the per-channel coefficients sit in LDS after the tile stages.
 // The tile body: did = this block's linear id among gx * gy tiles (gy column tiles per row tile).
 // HA (halo A operand, TAPS == 9 on the LDS-DMA ring): see the K loop below.
-template <int BM, int BN, int NWM, int NWN, int ST, bool POST, int TAPS, bool PRE, bool HA = false>
+template <int BM, int BN, int NWM, int NWN, int ST, int POST, int TAPS, bool PRE, bool HA = false>
 __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did, const int gx, const int gy) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int WTM = BM / NWM, WTN = BN / NWN;
@@ -597,7 +597,7 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
   const int cnt = min(WTM, a.M - row0);
   constexpr int LROW = WTN * 2 + 16;  // bytes per LDS row (padded: conflict-free 8-B writes)
   char* tl = reinterpret_cast<char*>(lds) + wid * (WTM * LROW);
-  // per-wave (sum, M2) of the stats, after every wave's transpose tile: [2][NWM][BN]
+  // per-wave (sum, M2) of the stats / post-op partials, after every wave's transpose tile: [2 or 3][NWM][BN]
   float* red = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + NWM * NWN * WTM * LROW);
 
   float csum[FC][4];
@@ -621,7 +621,7 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
   };
   // post-op aux values, loaded first so their latency overlaps the rounding pass
   uint2 zr[FC][FP];
-  if (POST) {
+  if (POST == 1) {
 #pragma unroll
     for (int c = 0; c < FC; ++c) {
       const int nb = n0 + wn * WTN + c * 16 + kg * 4;
@@ -647,7 +647,7 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
       }
     }
   }
-  if (POST) {
+  if (POST == 1) {
     // mask the rounded gradient with the producer's ReLU (recomputed from aux) and reduce its
     // backward partials over the wave's rows: q0 = sum d, q1 = sum d * xhat (BN)
 #pragma unroll
@@ -727,13 +727,48 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
   constexpr int RPI = 64 / CPR;         // rows per store instruction
   const int ck = lane % CPR, rsub = lane / CPR;
   const int nc = n0 + wn * WTN + ck * 8;
+  // post 3 (residual-BN backward) on the transposed tile, 8 channels x this lane's rows: d = mask *
+  // bf16(dgrad + the residual gradient already in y); q0 = sum d, q1 = sum d * xhat1 [, q2 = .. xhat2]
+  constexpr int NQ3 = POST == 3 ? 8 : 1;
+  float q3[3][NQ3], mu3[2][NQ3], iv3[2][NQ3];
+  const bool two = POST == 3 && a.aux2 != nullptr;
+  if constexpr (POST == 3) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool ok = nc + e < a.Ng;
+      q3[0][e] = q3[1][e] = q3[2][e] = 0.f;
+      mu3[0][e] = ok ? a.pmean[nc + e] : 0.f;
+      iv3[0][e] = ok ? a.pinv[nc + e] : 0.f;
+      mu3[1][e] = (ok && two) ? a.pmean2[nc + e] : 0.f;
+      iv3[1][e] = (ok && two) ? a.pinv2[nc + e] : 0.f;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < WTM / RPI; ++i) {
     const int r = i * RPI + rsub;
     if (r >= cnt || nc >= a.Ng) continue;
-    bf16* ptr = (bf16*)a.y + out_pix(row0 + r) * a.ldy + nc;
+    const long opx = out_pix(row0 + r);
+    bf16* ptr = (bf16*)a.y + opx * a.ldy + nc;
     uint4 v = *reinterpret_cast<const uint4*>(tl + r * LROW + ck * 16);
-    if (a.accumulate) {  // dx += dgrad (two bf16 tensors summed in fp32, like autograd's accumulation)
+    if constexpr (POST == 3) {
+      const uint4 old = *reinterpret_cast<const uint4*>(ptr);
+      const uint4 z = *reinterpret_cast<const uint4*>((const bf16*)a.aux + opx * a.ld_aux + nc);
+      const uint4 z2 = two ? *reinterpret_cast<const uint4*>((const bf16*)a.aux2 + opx * a.ld_aux2 + nc) : uint4{0u, 0u, 0u, 0u};
+      const unsigned mk = a.mbits[opx * (a.Ng >> 3) + (nc >> 3)];
+      const bf16* ob = reinterpret_cast<const bf16*>(&old);
+      const bf16* zb = reinterpret_cast<const bf16*>(&z);
+      const bf16* z2b = reinterpret_cast<const bf16*>(&z2);
+      bf16* nv = reinterpret_cast<bf16*>(&v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bf16 sm = (bf16)((float)nv[e] + (float)ob[e]);  // == the accumulating store
+        const float d = ((mk >> e) & 1u) ? (float)sm : 0.f;
+        nv[e] = (bf16)d;
+        q3[0][e] += d;
+        q3[1][e] = fmaf(d, ((float)zb[e] - mu3[0][e]) * iv3[0][e], q3[1][e]);
+        if (two) q3[2][e] = fmaf(d, ((float)z2b[e] - mu3[1][e]) * iv3[1][e], q3[2][e]);
+      }
+    } else if (a.accumulate) {  // dx += dgrad (two bf16 tensors summed in fp32, like autograd's accumulation)
       const uint4 old = *reinterpret_cast<const uint4*>(ptr);
       const bf16* ob = reinterpret_cast<const bf16*>(&old);
       bf16* nv = reinterpret_cast<bf16*>(&v);
@@ -742,20 +777,42 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
     }
     *reinterpret_cast<uint4*>(ptr) = v;
   }
+  if constexpr (POST == 3) {
+    // sum over the lanes of this chunk column (same ck), then one lane per chunk writes the wave's
+    // partials of its 8 channels to red[q][NWM][BN]
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        for (int o = CPR; o < 64; o <<= 1) q3[q][e] += __shfl_xor(q3[q][e], o, 64);
+    if (rsub == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int col = wn * WTN + ck * 8 + e;
+        red[wm * BN + col] = q3[0][e];
+        red[(NWM + wm) * BN + col] = q3[1][e];
+        red[(2 * NWM + wm) * BN + col] = q3[2][e];
+      }
+    }
+  }
   if (POST) {
-    // plain sums of the NWM row-waves' partials -> ppart[tile_m][2][Ng]
+    // plain sums of the NWM row-waves' partials -> ppart[tile_m][nq][Ng] (nq = 3 with a second
+    // residual branch, else 2)
+    const int nq = (POST == 3 && a.aux2) ? 3 : 2;
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     for (int col = tid; col < BN; col += NT) {
       const int n = n0 + col;
       if (n >= a.Ng) continue;
-      float t0 = 0.f, t1 = 0.f;
+      float t0 = 0.f, t1 = 0.f, t2 = 0.f;
 #pragma unroll
       for (int w = 0; w < NWM; ++w) {
         t0 += red[w * BN + col];
         t1 += red[(NWM + w) * BN + col];
+        if (POST == 3) t2 += red[(2 * NWM + w) * BN + col];
       }
-      a.ppart[(long)tile_m * 2 * a.Ng + n] = t0;
-      a.ppart[(long)tile_m * 2 * a.Ng + a.Ng + n] = t1;
+      a.ppart[(long)tile_m * nq * a.Ng + n] = t0;
+      a.ppart[(long)tile_m * nq * a.Ng + a.Ng + n] = t1;
+      if (nq == 3) a.ppart[(long)tile_m * nq * a.Ng + 2 * a.Ng + n] = t2;
     }
   }
   if (a.stats) {
@@ -788,7 +845,7 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
   }
 }
 
-template <int BM, int BN, int NWM, int NWN, int ST, bool POST, int TAPS = 0, bool PRE = false, bool HA = false>
+template <int BM, int BN, int NWM, int NWN, int ST, int POST, int TAPS = 0, bool PRE = false, bool HA = false>
 __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN, ST>())) void tn_fast_kernel(FastTNArgs a) {
   tn_fast_body<BM, BN, NWM, NWN, ST, POST, TAPS, PRE, HA>(a, blockIdx.x + gridDim.x * blockIdx.y, gridDim.x, gridDim.y);
 }
@@ -804,7 +861,7 @@ struct TNMulti {
   int n;
 };
 
-template <int BM, int BN, int NWM, int NWN, int ST, bool POST>
+template <int BM, int BN, int NWM, int NWN, int ST, int POST>
 __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN>())) void tn_multi_kernel(TNMulti m) {
   const int b = blockIdx.x;
   int k = 0;
@@ -1095,7 +1152,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     }
 }
 
-template <int BM, int BN, int NWM, int NWN, int ST, bool POST = false, int TAPS = 0, bool PRE = false, bool HA = false>
+template <int BM, int BN, int NWM, int NWN, int ST, int POST = 0, int TAPS = 0, bool PRE = false, bool HA = false>
 int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   constexpr int NT = 64 * NWM * NWN;
   // operand stages, or the epilogue's per-wave transpose tiles + stats scratch if larger; then the
@@ -1122,7 +1179,7 @@ int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   return 0;
 }
 
-template <int BM, int BN, int NWM, int NWN, int ST, bool POST>
+template <int BM, int BN, int NWM, int NWN, int ST, int POST>
 int launch_tn_multi_cfg(const FastTNArgs* fs, int n, hipStream_t st) {
   constexpr int NT = 64 * NWM * NWN;
   static bool attr = false;
@@ -1263,8 +1320,27 @@ int tn_fast_config(const FastTNArgs& a, int* taps_out) {
   return cfg;
 }
 
+// Configurations with a post-3 (residual-BN backward) instantiation: the tiles the bottleneck conv1
+// data gradients take (1x1, 1-8 K steps).
+bool tn_fast_post_res_ok(const FastTNArgs& a) {
+  const int cfg = tn_config(a);
+  return cfg == 4 || cfg == 19 || cfg == 20 || ((cfg == 7 || cfg == 10) && tn_taps(a) == 1);
+}
+
+static int launch_tn_post_res(const FastTNArgs& a, hipStream_t st) {
+  switch (tn_config(a)) {
+    case 4: return launch_tn_cfg<128, 128, 2, 2, 1, 3>(a, st);
+    case 19: return launch_tn_cfg<128, 128, 2, 2, 5, 3>(a, st);
+    case 20: return launch_tn_cfg<128, 64, 2, 2, 5, 3>(a, st);
+    case 7: return tn_taps(a) == 1 ? launch_tn_cfg<256, 128, 4, 2, 13, 3, 1>(a, st) : -1;
+    case 10: return tn_taps(a) == 1 ? launch_tn_cfg<128, 128, 2, 2, 15, 3, 1>(a, st) : -1;
+    default: return -1;
+  }
+}
+
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
   if (a.M <= 0 || a.Ng <= 0) return 0;
+  if (a.post == 3) return a.in_sc ? -1 : launch_tn_post_res(a, st);
   if (a.in_sc) {  // input prologue (fwd only: no post-op), register-staged configurations
     switch (tn_config(a)) {
       case 1: return launch_tn_cfg<256, 64, 4, 1, 2, false, 0, true>(a, st);

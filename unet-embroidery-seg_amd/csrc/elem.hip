@@ -458,6 +458,37 @@ __global__ void bn_bwd_finalize_rows_kernel(const float* part, int C, int G, lon
   }
 }
 
+// The two-branch form for the residual post-op (unetseg_conv2d_dgrad_post_res): part[g][1+nbranch][C] =
+// (sum dz, sum dz*xhat1 [, sum dz*xhat2]) per row tile; coefficients as bn_bwd_finalize_kernel.
+__global__ void bn_bwd_finalize_rows_res_kernel(const float* part, int C, int G, long M, int nbranch, const float* g1,
+                                                const float* inv1, float* dg1, float* db1, const float* g2,
+                                                const float* inv2, float* dg2, float* db2, float* coef) {
+  __shared__ double sc[16];
+  const int c = blockIdx.x;
+  const int nq = 1 + nbranch;
+  double t[3] = {0, 0, 0};
+  for (int k = 0; k < nq; ++k) {
+    double acc = 0.0;
+    for (int g = threadIdx.x; g < G; g += blockDim.x) acc += part[((long)g * nq + k) * C + c];
+    t[k] = block_sum(acc, sc);
+  }
+  if (threadIdx.x == 0) {
+    const double sdz = t[0];
+    dg1[c] += (float)t[1];
+    db1[c] += (float)sdz;
+    coef[0 * C + c] = g1[c] * inv1[c];
+    coef[1 * C + c] = (float)(sdz / (double)M);
+    coef[2 * C + c] = (float)(t[1] / (double)M);
+    if (nbranch == 2) {
+      dg2[c] += (float)t[2];
+      db2[c] += (float)sdz;
+      coef[3 * C + c] = g2[c] * inv2[c];
+      coef[4 * C + c] = (float)(sdz / (double)M);
+      coef[5 * C + c] = (float)(t[2] / (double)M);
+    }
+  }
+}
+
 // out[c] (+)= sum_g part[g][k][c] for part [G][2][C] (bias gradient from the fused ReLU post-op)
 __global__ void colsum_rows_kernel(const float* part, int C, int G, int k, float* out, int accumulate) {
   __shared__ double sc[16];
@@ -1356,7 +1387,9 @@ UNETSEG_API int unetseg_reduce_tiles(int dtype, long M, int C, int* tv_out, int*
   const int groups = cv / tv;
   // ~2048 blocks over (pixel tiles x channel groups); at least 2 unrolled groups of rows per
   // thread so the partials stay a few % of the data
-  long target = 2048 / groups;
+  // UNETSEG_RED_TARGET (tests): another block count, i.e. another summation order of the same partials
+  const char* te = getenv("UNETSEG_RED_TARGET");
+  long target = (te ? atol(te) : 2048) / groups;
   if (target < 64) target = 64;
   long per = (M + rows * target - 1) / (rows * target);
   per = (per + RU - 1) / RU * RU;
@@ -1477,6 +1510,18 @@ UNETSEG_API int unetseg_bn_bwd_finalize_rows(const float* part, int C, int G, lo
   hipLaunchKernelGGL(bn_bwd_finalize_rows_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, C, G, M, g1, inv1,
                      dg1, db1, coef);
   US_LAUNCH_CHECK("bn_bwd_finalize_rows");
+  return 0;
+}
+
+UNETSEG_API int unetseg_bn_bwd_finalize_rows_res(const float* part, int C, int G, long M, int nbranch, const float* g1,
+                                                 const float* inv1, float* dg1, float* db1, const float* g2,
+                                                 const float* inv2, float* dg2, float* db2, float* coef, void* stream) {
+  US_CHECK_ARG(part && g1 && inv1 && dg1 && db1 && coef && M > 0 && C > 0 && G > 0 && (nbranch == 1 || nbranch == 2),
+               "bn_bwd_finalize_rows_res: bad args");
+  US_CHECK_ARG(nbranch == 1 || (g2 && inv2 && dg2 && db2), "bn_bwd_finalize_rows_res: branch 2 needs its pointers");
+  hipLaunchKernelGGL(bn_bwd_finalize_rows_res_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, C, G, M, nbranch,
+                     g1, inv1, dg1, db1, g2, inv2, dg2, db2, coef);
+  US_LAUNCH_CHECK("bn_bwd_finalize_rows_res");
   return 0;
 }
 

@@ -86,6 +86,8 @@ SIGNATURES = {
     "unetseg_conv2d_dgrad_post": (I, [I, P, I, I, I, I, P, I, I, I, I, I, I, P, I, I, I, I, P, I, P, P, P, P, P, I,
                                       P]),
     "unetseg_bn_bwd_finalize_rows": (I, [P, I, I, L, P, P, P, P, P, P]),
+    "unetseg_conv2d_dgrad_post_res": (I, [I, P, I, I, I, I, P, I, I, P, I, P, I, P, P, P, P, I, P, P, P, I, P]),
+    "unetseg_bn_bwd_finalize_rows_res": (I, [P, I, I, L, I, P, P, P, P, P, P, P, P, P, P]),
     "unetseg_colsum_rows": (I, [P, I, I, I, P, I, P]),
     "unetseg_pack_input_stem": (I, [P, I, I, I, I, P, P]),
     "unetseg_stem_pack_weight": (I, [P, I, I, P, P]),
@@ -122,7 +124,7 @@ SIGNATURES = {
 
 #: functions returning a value rather than a status (no RuntimeError on non-zero)
 VALUE_FUNCS = {"reduce_tiles", "pw_small_tiles", "conv_tile_m", "abi_version", "conv2d_fwd_tile_m",
-               "conv2d_dgrad_post", "stem_fwd_tile_m", "attn_bwd1_tiles", "pw_small_tile", "conv2d_fwd_config",
+               "conv2d_dgrad_post", "conv2d_dgrad_post_res", "stem_fwd_tile_m", "attn_bwd1_tiles", "pw_small_tile", "conv2d_fwd_config",
                "conv2d_dgrad_config", "conv2d_wgrad_config", "stem_config", "pw_head_tiles", "channel_stats_tiles",
                "augment_tables_len", "pack_tiles",
                "conv2d_fwd_bnrelu_in_config", "conv2d_fwd_head_ok", "upsample2x_bwd_tiles"}

@@ -134,6 +134,8 @@ class Ctx:
         self.finish_hook = None  # called once the tape is done, before the compute stream joins the side
         self.side = None  # weight-gradient stream, set while backward runs with OVERLAP
         self.deferred = []  # weight-gradient launches held back until a flush point (defer_wgrad)
+        self.flushed = False  # the flush marker has run in this backward
+        self.has_marker = False  # the forward recorded a flush marker (models without one defer nothing)
 
     def push(self, fn):
         if self.tape is not None:
@@ -183,24 +185,40 @@ class Ctx:
                     self.grad_hook(p)
 
 
-#: weight gradients of convs whose output has >= this many pixels per image (the decoder's 256^2 / 512^2
-#: 3x3 convs) are held back in backward until the flush point between the decoder and the encoder
-#: (flush_point): they then run on the side stream beside the encoder's small, latency-bound layers
-#: instead of beside the data gradients of their own layers (0 = off; UNETSEG_WG_DEFER_HW)
-WG_DEFER_HW = int(os.environ.get("UNETSEG_WG_DEFER_HW", "0"))
+#: weight gradients of 3x3 convs whose output has >= this many pixels per image are held back in
+#: backward until a flush marker (flush_point): they then run on the side stream beside the encoder's
+#: memory-bound layers instead of beside the data gradients of their own layers.  Default: the
+#: decoder's virtual-concat convs (MFMA-bound, each used to share the CUs with its own equally heavy data
+#: gradient), released when the backward reaches layer4 -- step A/B +0.45 % (three interleaved repeats);
+#: holding back every decoder 3x3 wgrad, or releasing at layer3, measured neutral to -3 %
+#: (0 = off; UNETSEG_WG_DEFER_HW, UNETSEG_WG_DEFER_CAT, UNETSEG_WG_FLUSH)
+WG_DEFER_HW = int(os.environ.get("UNETSEG_WG_DEFER_HW", "1024"))
 #: where the flush marker sits in forward order: "decoder" (before the decoder), "layer4" / "layer3" / "layer2"
 #: (before that encoder layer: in backward the held-back gradients start once that layer's backward is done)
-WG_FLUSH = os.environ.get("UNETSEG_WG_FLUSH", "decoder")
+WG_FLUSH = os.environ.get("UNETSEG_WG_FLUSH", "layer4")
+
+
+#: only the virtual-concat convs (the decoder's unetUp conv1) are held back (UNETSEG_WG_DEFER_CAT=0: every 3x3)
+WG_DEFER_CAT = os.environ.get("UNETSEG_WG_DEFER_CAT", "1") == "1"
 
 
 def defer_wgrad(ctx, N, Pq, Qq, R, S, x2):
-    return bool(WG_DEFER_HW) and ctx.side is not None and Pq * Qq >= WG_DEFER_HW and R * S > 1
+    """hold this conv's weight gradient until the flush marker (never after it has run: the
+    encoder's own gradients are not pushed to the end of the backward)"""
+    return (bool(WG_DEFER_HW) and ctx.side is not None and ctx.has_marker and not ctx.flushed
+            and Pq * Qq >= WG_DEFER_HW and R * S > 1
+            and (x2 is not None or not WG_DEFER_CAT))
 
 
 def flush_point(ctx, where):
     """forward marker: in backward, the deferred weight gradients are launched when the tape reaches it"""
-    if WG_DEFER_HW and where == WG_FLUSH:
-        ctx.push(ctx.flush_deferred)
+    if WG_DEFER_HW and where == WG_FLUSH and ctx.tape is not None:
+        ctx.has_marker = True
+
+        def marker():
+            ctx.flushed = True
+            ctx.flush_deferred()
+        ctx.push(marker)
 
 
 def gbuf(ctx, node):
@@ -512,11 +530,46 @@ def conv_bn(ctx, x, pc, bnm, x2=None, lazy=False):
     return Node(y)
 
 
+#: the residual BN-add-ReLU backward's first pass in the next block's conv1 data gradient
+#: (unetseg_conv2d_dgrad_post_res; UNETSEG_NO_POST_RES=1: separate bn_bwd_reduce pass)
+FUSE_RES = os.environ.get("UNETSEG_NO_POST_RES", "0") != "1"
+
+
+def _dgrad_fused_res(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
+    """x1 is a bottleneck output relu(BN3(y3) + residual) (model/resnet_backbone.py:110-113) consumed by
+    this 1x1 conv (the next block's conv1) and by that block's residual add, whose gradient is already
+    in x1.grad: accumulate the dgrad onto it, mask with the stored ReLU bits and write BN3's backward
+    partials in the epilogue (and the downsample BN's, block 0) -- the producer's bn_bwd_reduce pass
+    over the gradient is not run."""
+    if not (FUSE_RES and x1.fuse is not None and x1.fuse[0] == 3 and x1.grad is not None and x1.uses == 2 and
+            ctx.dt == DT_BF16 and (pc.R, pc.S) == (1, 1) and pc.conv.stride in (1, (1, 1)) and
+            x1.grad.is_contiguous() and ldp(x1.grad) == C1 and H == Pq and W == Qq):
+        return False
+    _, y3, s1, mbits, y2, s2 = x1.fuse
+    K = pc.K
+    rows = lib.conv2d_dgrad_post_res(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, 0, C1, P(y3), ldp(y3), 0, 0,
+                                     0, 0, 0, 0, 0, 0, 0, ctx.stream)
+    if rows <= 0:
+        return False
+    nq = 3 if y2 is not None else 2
+    part = ctx.f32(rows, nq, C1)
+    g = x1.grad
+    with _probe("igemm_tn", flops, 1, ("dgrad_post3",) + desc):
+        lib.conv2d_dgrad_post_res(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, P(g), C1, P(y3), ldp(y3),
+                                  P(s1.mean), P(s1.inv), P(mbits), P(y2), ldp(y2), P(s2.mean if s2 else None),
+                                  P(s2.inv if s2 else None), P(part), rows, ctx.stream)
+    x1.fused = (part, rows, nq)
+    return True
+
+
 def _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
     """dgrad into x1.grad with the backward mask + first reduction of the ReLU / BN-ReLU that
     produced x1 fused into the epilogue.  Only when this conv is x1's sole consumer (so its dgrad
     is x1's whole gradient) and the shape has a fused kernel; returns False otherwise."""
-    if not (FUSE and x1.fuse is not None and x1.grad is None and x1.uses == 1 and ctx.dt == DT_BF16):
+    if _dgrad_fused_res(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
+        return True
+    if not (FUSE and x1.fuse is not None and x1.fuse[0] != 3 and x1.grad is None and x1.uses == 1 and
+            ctx.dt == DT_BF16):
         return False
     kind, aux, st = x1.fuse
     K, R, S = pc.K, pc.R, pc.S
@@ -667,6 +720,9 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None, lazy=False):
         lib.bn_apply_mask(ctx.dt, P(Y), ldp(Y), P(s1.sc), P(s1.sh), P(R), ldp(R), P(s2.sc if s2 else None),
                           P(s2.sh if s2 else None), mode, P(a), C, M, C, P(mbits), ctx.stream)
         out = Node(a)
+        # a consumer conv that delivers this output's gradient last may run BN3's backward pass 1
+        # (and the downsample BN's) in its data-gradient epilogue (_dgrad_fused_res)
+        out.fuse = (3, Y, s1, mbits, res_bn[0].data if res_bn is not None else None, s2)
     else:
         a = ctx.empty(N, H, W, C)
         lib.bn_apply(ctx.dt, P(Y), ldp(Y), P(s1.sc), P(s1.sh), P(R), ldp(R), P(s2.sc if s2 else None),
@@ -682,6 +738,36 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None, lazy=False):
             return
         if not ctx.training:
             raise NotImplementedError("backward through eval-mode BatchNorm is not on the hot path")
+        if out.fused is not None and len(out.fused) == 3:
+            # residual BN-add-ReLU: the next block's conv1 dgrad stored dz = mask * dA in dA's buffer and
+            # the (sum dz, sum dz*xhat1 [, sum dz*xhat2]) row partials (_dgrad_fused_res)
+            part, rows, nq = out.fused
+            coef = ctx.f32(6, C)
+            b2 = res_bn[2] if res_bn is not None else None
+            y2 = res_bn[0] if res_bn is not None else None
+            lib.bn_bwd_finalize_rows_res(P(part), C, rows, M, nq - 1, P(bnm.weight), P(s1.inv), P(bnm.weight.grad),
+                                         P(bnm.bias.grad), P(b2.weight if b2 else None), P(s2.inv if s2 else None),
+                                         P(b2.weight.grad if b2 else None), P(b2.bias.grad if b2 else None), P(coef),
+                                         ctx.stream)
+            ctx.param_done(bnm.weight, bnm.bias)
+            if b2 is not None:
+                ctx.param_done(b2.weight, b2.bias)
+            dy1, acc1 = gbuf(ctx, y)
+            assert acc1 == 0
+            dy2 = Y2 = None
+            if y2 is not None:
+                Y2 = y2.data
+                dy2, acc2 = gbuf(ctx, y2)
+                assert acc2 == 0
+            if res is not None and res.need_grad:
+                # the residual gradient IS dz: the block input's gradient starts as this buffer (the
+                # block's conv1 dgrad accumulates onto it later; nothing reads dz after this apply)
+                assert res.grad is None
+                res.grad = dA
+            lib.bn_bwd_apply(ctx.dt, P(dA), ldp(dA), 0, C, 0, 0, P(Y), ldp(Y), P(s1.mean), P(s1.inv), P(dy1), ldp(dy1),
+                             P(Y2), ldp(Y2), P(s2.mean if s2 else None), P(s2.inv if s2 else None), P(dy2), ldp(dy2),
+                             P(coef), 0, 0, 0, M, C, ctx.stream)
+            return
         if out.fused is not None:
             # the consumer's dgrad stored dz = dA * mask and the (sum dz, sum dz*xhat) row partials
             part, rows = out.fused
