@@ -295,12 +295,18 @@ HALO_CASES = {
     "hring64_fwd_stats_k40": ("fwd_stats", (2, 64, 96, 192, 0, 40, 3, 1), ["fwd:ring256x64_halo"]),
     "hring64_dgrad": ("dgrad", (2, 64, 64, 64, 0, 128, 3, 1), ["dgrad:ring256x64_halo"]),
     "hring64_post1": ("post1", (2, 32, 64, 64, 0, 128, 3, 1), ["dgrad_post1:ring256x64_halo"]),
+    # one or two 128x128 tiles per CU: 4 x 32 tiles (layer3 conv2 256 -> 256 at 32^2)
+    "hring128_fwd_stats": ("fwd_stats", (16, 32, 32, 256, 0, 256, 3, 1), ["fwd:ring128x128_halo"]),
+    "hring128_post2": ("post2", (16, 32, 32, 256, 0, 256, 3, 1), ["dgrad_post2:ring128x128_halo"]),
+    "hring128_dgrad_ng192": ("dgrad", (8, 32, 64, 384, 0, 192, 3, 1), ["dgrad:ring128x128_halo"]),
+    "hring128_post1": ("post1", (8, 32, 32, 512, 0, 512, 3, 1), ["dgrad_post1:ring128x128_halo"]),  # B=8 up_concat4.conv2
 }
 
 
 def _gather_ring(expect):
     """a case written for the 256x128 gather ring on a shape the halo-A ring now takes"""
-    return bool(expect) and any(k is not None and k.endswith(("ring256x128_t9", "ring128x64_t9")) for k in expect)
+    return bool(expect) and any(k is not None and k.endswith(("ring256x128_t9", "ring128x64_t9", "ring128x128_5st_t9"))
+                                for k in expect)
 
 
 @pytest.mark.parametrize("cid", list(HALO_CASES))

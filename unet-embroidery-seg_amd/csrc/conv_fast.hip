@@ -42,8 +42,8 @@ constexpr int tn_waves_per_simd() {
 // halo DMA instructions, so the stage is rounded up to whole instructions of the block
 template <int BM, int NWM, int NWN>
 constexpr int kHaloChunks() {
-  constexpr int NT = 64 * NWM * NWN;
-  return ((BM / 32 + 2) * 34 * 8 + NT - 1) / NT * NT;
+  constexpr int NT = 64 * NWM * NWN;  // rounded to instruction pairs (issued two at a time)
+  return ((BM / 32 + 2) * 34 * 8 + 2 * NT - 1) / (2 * NT) * (2 * NT);
 }
 template <int BM, int BN, int NWM, int NWN, int ST, bool HA = false>
 constexpr size_t kPreOff() {
@@ -301,7 +301,7 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
     // nine taps read their A fragments from it at a uniform pixel shift; only the weights stream
     // through the NS-stage ring, one tap per K step.  Per chunk that is ~43 KiB of A DMA instead of
     // 9 x 32 KiB of re-gathered tap rows: 2.3x fewer DMA instructions per MFMA than the gather ring.
-    static_assert(TAPS == 9 && kDMA && !PRE && (B_PER == 2 || B_PER == 1), "halo-A ring: 3x3 taps");
+    static_assert(TAPS == 9 && kDMA && !PRE && (B_PER % 2 == 0 || B_PER == 1), "halo-A ring: 3x3 taps");
     constexpr int NS = ST - 10;
     constexpr int TRH = BM / 32;
     constexpr int HPIX = (TRH + 2) * 34;
@@ -377,7 +377,9 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
       if constexpr (B_PER == 1) {
         dma16s(rwx, sb, boff[0], wsoff);
       } else {
-        dma16x2<RSTEP * 128>(rwx, sb, boff[0], boff[1], wsoff);
+#pragma unroll
+        for (int i = 0; i < B_PER; i += 2)
+          dma16x2<RSTEP * 128>(rwx, sb + (unsigned)(RSTEP * i * 128), boff[i], boff[i + 1], wsoff);
       }
     };
     // wait for this step's weight stage (and, at a chunk's first tap, its halo): the younger DMAs
@@ -1235,8 +1237,9 @@ static int launch_tn_dma(const FastTNArgs& a, hipStream_t st) {
 // 7-10: the same tiles on the LDS-DMA ring.  Measured (tools/gpu_cfg_sweep.sh): the 256x128 ring
 // (3 stages) beats the register-staged 256x128 by 3-8 % on every large layer; the 64x128 ring (4
 // stages) is 15 % faster on deep-K small-M layers (3x3 at 16x16, 72 K steps) but slower on short K.
-// The halo-A ring (configuration 21, or 22 for <= 64 output channels) serves a 3x3 stride-1 "same"
-// conv whose output grid tiles into 8 x 32 spatial blocks, in place of the gather rings 7 / 13.
+// The halo-A ring (configuration 21, 22 for <= 64 output channels, 23 on 128x128 tiles) serves a 3x3
+// stride-1 "same" conv whose output grid tiles into 8 x 32 spatial blocks, in place of the gather
+// rings 7 / 13 / 10.
 static bool halo_a_ok(const FastTNArgs& a) {
   // default since the round-3 A/B (+1.8 % end to end); UNETSEG_TN_NO_HALO_RING=1 keeps the gather
   // ring -- read per call so a test can run both rings in one process
@@ -1252,7 +1255,7 @@ static int tn_config_base(const FastTNArgs& a);
 
 static int tn_config(const FastTNArgs& a) {
   const int c = tn_config_base(a);
-  if ((c == 7 || (c == 13 && !getenv("UNETSEG_TN_CFG_NO22"))) && halo_a_ok(a)) return c == 7 ? 21 : 22;
+  if ((c == 7 || c == 13 || (c == 10 && !getenv("UNETSEG_TN_CFG_NO23"))) && halo_a_ok(a)) return c == 7 ? 21 : c == 13 ? 22 : 23;
   return c;
 }
 
@@ -1292,6 +1295,7 @@ static int tn_config_base(const FastTNArgs& a) {
 static int tn_cfg_bm(int cfg) {
   switch (cfg) {
     case 1: case 2: case 7: case 11: case 14: case 21: case 22: return 256;
+    case 23: return 128;
     case 5: case 9: return 64;
     default: return 128;
   }
@@ -1383,6 +1387,10 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     // 64 output channels or fewer: 256x64 (eight waves of 64x32), one weight row per wave and step
     case 22: return a.post ? launch_tn_cfg<256, 64, 4, 2, 13, true, 9, false, true>(a, st)
                            : launch_tn_cfg<256, 64, 4, 2, 13, false, 9, false, true>(a, st);
+    // in place of the 5-stage 128x128 gather ring (one or two tiles per CU): 4 x 32 spatial tiles,
+    // four waves, the weights on a 5-stage ring
+    case 23: return a.post ? launch_tn_cfg<128, 128, 2, 2, 15, true, 9, false, true>(a, st)
+                           : launch_tn_cfg<128, 128, 2, 2, 15, false, 9, false, true>(a, st);
     default: return a.post ? launch_tn_cfg<128, 128, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 3>(a, st);
   }
 }
