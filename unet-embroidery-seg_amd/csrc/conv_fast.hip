@@ -45,7 +45,7 @@ constexpr int kHaloChunks() {
   constexpr int NT = 64 * NWM * NWN;  // rounded to instruction pairs (issued two at a time)
   return ((BM / 32 + 2) * 34 * 8 + 2 * NT - 1) / (2 * NT) * (2 * NT);
 }
-template <int BM, int BN, int NWM, int NWN, int ST, bool HA = false>
+template <int BM, int BN, int NWM, int NWN, int ST, int HA = 0>
 constexpr size_t kPreOff() {
   constexpr size_t stages = HA ? ((size_t)2 * kHaloChunks<BM, NWM, NWN>() + (size_t)(ST - 10) * BN * 8) * 16
                                : (size_t)(ST == 1 || ST == 5 ? 1 : ST >= 13 ? ST - 10 : 2) * (BM + BN) * 8 * 16;
@@ -61,8 +61,9 @@ constexpr size_t kPreOff() {
 // PRE: the input prologue of FastTNArgs (x1 = BN input z, staged as relu(z*in_sc + in_sh) between the
 // global load and the LDS store); the per-channel coefficients sit in LDS after the tile stages.
 // The tile body: did = this block's linear id among gx * gy tiles (gy column tiles per row tile).
-// HA (halo A operand, TAPS == 9 on the LDS-DMA ring): see the K loop below.
-template <int BM, int BN, int NWM, int NWN, int ST, int POST, int TAPS, bool PRE, bool HA = false>
+// HA (halo A operand, TAPS == 9 on the LDS-DMA ring; the value = pieces the next chunk's halo DMA is
+// issued in, at taps 0, 9/HA, ..): see the K loop below.
+template <int BM, int BN, int NWM, int NWN, int ST, int POST, int TAPS, bool PRE, int HA = 0>
 __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did, const int gx, const int gy) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int WTM = BM / NWM, WTN = BN / NWN;
@@ -311,6 +312,9 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
     constexpr int WP = B_PER;                          // weight DMA instructions per wave per K step
     static_assert(HI % 2 == 0, "halo rows are issued in pairs");
     static_assert(WP * (NS - 2) + HI <= 63, "vmcnt range");
+    // the next chunk's halo goes out in HA pieces (HI / HA DMA instructions each) at taps 0, 9 / HA, ..
+    constexpr int HPC = HI / HA, TPER = 9 / HA;
+    static_assert(HI % (2 * HA) == 0 && 9 % HA == 0, "halo pieces of whole instruction pairs");
     // this block's spatial tile (row_pix with t2d == TRH: tiles of TRH image rows x 32 columns,
     // stacked over the images; hc % TRH == 0, so a tile never straddles two images)
     const int tpr = a.wc >> 5;
@@ -356,7 +360,7 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
     const unsigned hbase = lds_addr(lds);
     const unsigned wbase = hbase + 2u * HST * 16u;
     const int nch = a.cin >> 6;
-    auto issue_halo = [&](int c, int hs) {
+    auto issue_halo = [&](int c, int hs, int i0, int i1) {
       const bool live = c < nch;
       const int c64 = c * 64;
       const bool first = c64 < a.c1;
@@ -365,7 +369,7 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
       const unsigned soff = __builtin_amdgcn_readfirstlane(live ? (unsigned)(first ? c64 : c64 - a.c1) * 2u : 0u);
       const unsigned sb = __builtin_amdgcn_readfirstlane(hbase + (unsigned)(hs * HST * 16) + (unsigned)(wid * 1024));
 #pragma unroll
-      for (int i = 0; i < HI; i += 2)
+      for (int i = i0; i < i1; i += 2)
         dma16x2<NT * 16>(rx, sb + (unsigned)(i * NT * 16), __umul24(hvp[i], ldcb) + hsw[i],
                          __umul24(hvp[i + 1], ldcb) + hsw[i + 1], soff);
     };
@@ -387,10 +391,16 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
     // after this step's weights (taps 1 .. NS-1 of a chunk)
     auto wait_step = [&](auto tc) {
       constexpr int t = decltype(tc)::value;
-      constexpr int n = WP * (NS - 2) + ((t >= 1 && t <= NS - 1) ? HI : 0);
+      // halo pieces issued in the NS-1 iterations since this step's weights went out (those
+      // iterations' taps t-1 .. t-NS+1, mod 9)
+      constexpr int n = WP * (NS - 2) + HPC * (((((t - 1) % 9 + 9) % 9) % TPER == 0 ? 1 : 0) +
+                                               (NS >= 3 && ((((t - 2) % 9 + 9) % 9) % TPER == 0) ? 1 : 0) +
+                                               (NS >= 4 && ((((t - 3) % 9 + 9) % 9) % TPER == 0) ? 1 : 0) +
+                                               (NS >= 5 && ((((t - 4) % 9 + 9) % 9) % TPER == 0) ? 1 : 0));
+      static_assert(NS <= 5, "wait count");
       asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(n) : "memory");
     };
-    issue_halo(0, 0);
+    issue_halo(0, 0, 0, HI);
 #pragma unroll
     for (int s0 = 0; s0 < NS - 1; ++s0) issue_w(s0 / 9, s0 % 9, s0);
     int stage = 0;
@@ -415,7 +425,7 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
         for (int cc = 0; cc < FC; ++cc) wf[cc] = *reinterpret_cast<const bf16x8*>(ws + foffW[0] + cc * 2048);
         const int st2 = stage == 0 ? NS - 1 : stage - 1;  // (stage + NS - 1) % NS
         issue_w(c + (t + NS - 1) / 9, (t + NS - 1) % 9, st2);
-        if constexpr (t == 0) issue_halo(c + 1, (c + 1) & 1);
+        if constexpr (t % TPER == 0) issue_halo(c + 1, (c + 1) & 1, (t / TPER) * HPC, (t / TPER + 1) * HPC);
         mfmas(pf, wf);
 #pragma unroll
         for (int p = 0; p < FP; ++p) pf[p] = *reinterpret_cast<const bf16x8*>(hs + (ab[p] ^ 64u));
@@ -847,7 +857,7 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
   }
 }
 
-template <int BM, int BN, int NWM, int NWN, int ST, int POST, int TAPS = 0, bool PRE = false, bool HA = false>
+template <int BM, int BN, int NWM, int NWN, int ST, int POST, int TAPS = 0, bool PRE = false, int HA = 0>
 __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN, ST>())) void tn_fast_kernel(FastTNArgs a) {
   tn_fast_body<BM, BN, NWM, NWN, ST, POST, TAPS, PRE, HA>(a, blockIdx.x + gridDim.x * blockIdx.y, gridDim.x, gridDim.y);
 }
@@ -1154,7 +1164,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void wgrad_fast_kernel(FastWgradArg
     }
 }
 
-template <int BM, int BN, int NWM, int NWN, int ST, int POST = 0, int TAPS = 0, bool PRE = false, bool HA = false>
+template <int BM, int BN, int NWM, int NWN, int ST, int POST = 0, int TAPS = 0, bool PRE = false, int HA = 0>
 int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   constexpr int NT = 64 * NWM * NWN;
   // operand stages, or the epilogue's per-wave transpose tiles + stats scratch if larger; then the
@@ -1379,18 +1389,22 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 21: {
       // weight ring depth: 3 stages (144 KiB of LDS with the two halo stages); 4 fill all 160 KiB
       static const bool ns4 = getenv("UNETSEG_TN_HALO_NS4") != nullptr;
-      if (ns4) return a.post ? launch_tn_cfg<256, 128, 4, 2, 14, true, 9, false, true>(a, st)
-                             : launch_tn_cfg<256, 128, 4, 2, 14, false, 9, false, true>(a, st);
-      return a.post ? launch_tn_cfg<256, 128, 4, 2, 13, true, 9, false, true>(a, st)
-                    : launch_tn_cfg<256, 128, 4, 2, 13, false, 9, false, true>(a, st);
+      // UNETSEG_TN_HALO_SPLIT=3: the next chunk's halo DMA in three pieces (taps 0, 3, 6)
+      static const bool split = getenv("UNETSEG_TN_HALO_SPLIT") && atoi(getenv("UNETSEG_TN_HALO_SPLIT")) == 3;
+      if (ns4) return a.post ? launch_tn_cfg<256, 128, 4, 2, 14, true, 9, false, 1>(a, st)
+                             : launch_tn_cfg<256, 128, 4, 2, 14, false, 9, false, 1>(a, st);
+      if (split) return a.post ? launch_tn_cfg<256, 128, 4, 2, 13, true, 9, false, 3>(a, st)
+                               : launch_tn_cfg<256, 128, 4, 2, 13, false, 9, false, 3>(a, st);
+      return a.post ? launch_tn_cfg<256, 128, 4, 2, 13, true, 9, false, 1>(a, st)
+                    : launch_tn_cfg<256, 128, 4, 2, 13, false, 9, false, 1>(a, st);
     }
     // 64 output channels or fewer: 256x64 (eight waves of 64x32), one weight row per wave and step
-    case 22: return a.post ? launch_tn_cfg<256, 64, 4, 2, 13, true, 9, false, true>(a, st)
-                           : launch_tn_cfg<256, 64, 4, 2, 13, false, 9, false, true>(a, st);
+    case 22: return a.post ? launch_tn_cfg<256, 64, 4, 2, 13, true, 9, false, 1>(a, st)
+                           : launch_tn_cfg<256, 64, 4, 2, 13, false, 9, false, 1>(a, st);
     // in place of the 5-stage 128x128 gather ring (one or two tiles per CU): 4 x 32 spatial tiles,
     // four waves, the weights on a 5-stage ring
-    case 23: return a.post ? launch_tn_cfg<128, 128, 2, 2, 15, true, 9, false, true>(a, st)
-                           : launch_tn_cfg<128, 128, 2, 2, 15, false, 9, false, true>(a, st);
+    case 23: return a.post ? launch_tn_cfg<128, 128, 2, 2, 15, true, 9, false, 1>(a, st)
+                           : launch_tn_cfg<128, 128, 2, 2, 15, false, 9, false, 1>(a, st);
     default: return a.post ? launch_tn_cfg<128, 128, 2, 2, 3, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 3>(a, st);
   }
 }
