@@ -21,11 +21,12 @@ def main():
     from unetseg_hip.losses import binary_segmentation_loss
     from utils.synthetic import make_batch
 
-    if os.environ.get("HA_STREAM", "0") == "1":  # bench.py's default: a created (non-legacy) stream
+    if os.environ.get("HA_STREAM", "1") == "1":  # bench.py's default: a created (non-legacy) stream
         torch.cuda.set_stream(torch.cuda.Stream())
     m = create_model("unet_resnet50", weights="", num_classes=2).cuda().train()
     m.compute_dtype = "bf16"
-    opt = FusedAdam(m, lr=1e-4, weight_decay=1e-4)
+    # bench.py's optimizer: Adam + re-pack per gradient bucket during backward (HA_OVERLAP=0: after it)
+    opt = FusedAdam(m, lr=1e-4, weight_decay=1e-4, overlap=os.environ.get("HA_OVERLAP", "1") == "1")
     x, y = make_batch(16, 512, seed=5)
     x, y = x.cuda(), y.cuda()
 
@@ -51,8 +52,10 @@ def main():
         e.record()
         evs.append(e)
         done = [int(ev.query()) for ev in evs[-4:]]
+        st = torch.cuda.memory_stats()
         print(f"step {k}: host {1e3 * (t - t_prev):6.2f} ms (fwd {1e3 * (tf - t_prev):5.2f}, bwd {1e3 * (tb - tf):5.2f}) "
-              f"last-4 step events done: {done}", flush=True)
+              f"last-4 step events done: {done}  segments {st.get('segment.all.current', -1)} "
+              f"alloc_retries {st.get('num_alloc_retries', -1)} hipMalloc {st.get('num_device_alloc', -1)}", flush=True)
         t_prev = t
     torch.cuda.synchronize()
 

@@ -1389,8 +1389,9 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 21: {
       // weight ring depth: 3 stages (144 KiB of LDS with the two halo stages); 4 fill all 160 KiB
       static const bool ns4 = getenv("UNETSEG_TN_HALO_NS4") != nullptr;
-      // UNETSEG_TN_HALO_SPLIT=3: the next chunk's halo DMA in three pieces (taps 0, 3, 6)
-      static const bool split = getenv("UNETSEG_TN_HALO_SPLIT") && atoi(getenv("UNETSEG_TN_HALO_SPLIT")) == 3;
+      // the next chunk's halo DMA in three pieces at taps 0, 3, 6 (A/B +0.3 %; UNETSEG_TN_HALO_SPLIT=1:
+      // all of it at tap 0)
+      static const bool split = !(getenv("UNETSEG_TN_HALO_SPLIT") && atoi(getenv("UNETSEG_TN_HALO_SPLIT")) == 1);
       if (ns4) return a.post ? launch_tn_cfg<256, 128, 4, 2, 14, true, 9, false, 1>(a, st)
                              : launch_tn_cfg<256, 128, 4, 2, 14, false, 9, false, 1>(a, st);
       if (split) return a.post ? launch_tn_cfg<256, 128, 4, 2, 13, true, 9, false, 3>(a, st)
