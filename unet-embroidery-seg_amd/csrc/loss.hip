@@ -89,23 +89,48 @@ __global__ void radix_scan_kernel(uint32_t* hist, int T) {
   }
 }
 
-// stable scatter: the tile is consumed in 16 rounds of 256 keys (original order = round-major)
-__global__ void radix_scatter_kernel(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
-                                     long P, int T, int shift, const uint32_t* hist) {
-  __shared__ uint32_t base[256];
+// stable scatter.  The tile is ranked in 16 rounds of 256 keys (original order = round-major) into LDS
+// in digit order, then written out from LDS: consecutive slots of one digit go to consecutive global
+// positions, so the writes leave as runs (~16 keys per digit and tile) instead of one scattered 4-B
+// store per key.
+__global__ __launch_bounds__(256) void radix_scatter_kernel(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
+                                                            uint32_t* vout, long P, int T, int shift,
+                                                            const uint32_t* hist) {
+  __shared__ uint32_t gbase[256];  // global position of this tile's first key of each digit
+  __shared__ uint32_t lstart[256];  // tile-local first slot of each digit
+  __shared__ uint32_t run[256];     // keys of each digit placed so far
   __shared__ uint32_t wcnt[4][256];
+  __shared__ uint32_t sk[kTile], sv[kTile];
   const int t = blockIdx.x, b = blockIdx.y;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  base[threadIdx.x] = hist[((long)b * 256 + threadIdx.x) * T + t];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t* hb = hist + (long)b * 256 * T;
   const long seg = (long)b * P;
   const long tbase = (long)t * kTile;
   const long n = min((long)kTile, P - tbase);
+  // this tile's count of digit `tid`: the next entry of the digit-major exclusive scan minus this one
+  const long hi = (long)tid * T + t;
+  const uint32_t g0 = hb[hi];
+  const uint32_t cnt = (hi + 1 < 256L * T ? hb[hi + 1] : (uint32_t)P) - g0;
+  gbase[tid] = g0;
+  // exclusive scan of the 256 counts (wave prefix sums, then the four wave totals)
+  uint32_t x = cnt;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wcnt[0][wid] = x;
+  __syncthreads();
+  uint32_t off = 0;
+  for (int w = 0; w < wid; ++w) off += wcnt[0][w];
+  lstart[tid] = off + x - cnt;
+  run[tid] = 0;
+  __syncthreads();
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
   for (int round = 0; round < kTile / 256; ++round) {
-    const long i = round * 256L + threadIdx.x;
+    const long i = round * 256L + tid;
     const bool ok = i < n;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) wcnt[w][threadIdx.x] = 0;
+    for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
     __syncthreads();
     uint32_t key = 0, val = 0, d = 0;
     if (ok) {
@@ -123,13 +148,21 @@ __global__ void radix_scatter_kernel(const uint32_t* kin, const uint32_t* vin, u
     if (ok && lrank == 0) wcnt[wid][d] = (uint32_t)__popcll(m);
     __syncthreads();
     if (ok) {
-      uint32_t pos = base[d] + lrank;
+      uint32_t pos = lstart[d] + run[d] + lrank;
       for (int w = 0; w < wid; ++w) pos += wcnt[w][d];
-      kout[seg + pos] = key;
-      vout[seg + pos] = val;
+      sk[pos] = key;
+      sv[pos] = val;
     }
     __syncthreads();
-    base[threadIdx.x] += wcnt[0][threadIdx.x] + wcnt[1][threadIdx.x] + wcnt[2][threadIdx.x] + wcnt[3][threadIdx.x];
+    run[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
+  }
+  __syncthreads();
+  for (int j = tid; j < n; j += 256) {
+    const uint32_t key = sk[j];
+    const uint32_t d = (key >> shift) & 255u;
+    const uint32_t pos = gbase[d] + (uint32_t)j - lstart[d];
+    kout[seg + pos] = key;
+    vout[seg + pos] = sv[j];
   }
 }
 
