@@ -1477,10 +1477,20 @@ UNETSEG_API int unetseg_stem_pack_weight(const float* w, int K, int C, void* wk,
 }
 
 // row tile of the stem's BN partial statistics (stats is [ceil(M/tile)][2][K])
+// the stem's TN arguments; UNETSEG_STEM_CFG = a register-staged or generic-ring TN configuration
+// (1, 2, 3, 5, 6, 8, 11, 12, 13, 14) for experiments, else tn_config's rule
+static bool stem_fast_args(const IgemmArgs& a, FastTNArgs& f) {
+  if (!fast_tn_args(a, f)) return false;
+  static const int forced = getenv("UNETSEG_STEM_CFG") ? atoi(getenv("UNETSEG_STEM_CFG")) : 0;
+  if (forced == 1 || forced == 2 || forced == 3 || forced == 5 || forced == 6 || forced == 8 || (forced >= 11 && forced <= 14))
+    f.force_cfg = forced;
+  return true;
+}
+
 UNETSEG_API int unetseg_stem_fwd_tile_m(int n, int h, int w, int K) {
   IgemmArgs a = stem_args(nullptr, n, h, w, nullptr, K);
   FastTNArgs f;
-  if (!fast_tn_args(a, f)) return -1;
+  if (!stem_fast_args(a, f)) return -1;
   return tn_fast_tile_m(f);
 }
 
@@ -1494,7 +1504,7 @@ UNETSEG_API int unetseg_stem_config(int n, int h, int w, int K, int* splits_out)
     FastWgradArgs g = stem_wgrad_args(kSomePtr, n, h, w, kSomePtr, K, K);
     *splits_out = wgrad_fast_splits(K, g.Ng, g.Kpix);
   }
-  if (!fast_tn_args(a, f)) return -1;
+  if (!stem_fast_args(a, f)) return -1;
   return tn_fast_config(f, nullptr);
 }
 
@@ -1504,7 +1514,7 @@ UNETSEG_API int unetseg_stem_fwd(const void* xp, int n, int h, int w, const void
   IgemmArgs a = stem_args(xp, n, h, w, wk, K);
   a.y = y; a.ldy = ldy; a.accumulate = 0; a.bias = nullptr; a.relu = 0; a.stats = stats;
   FastTNArgs f;
-  US_CHECK_ARG(fast_tn_args(a, f), "stem_fwd: shape not supported by the fast kernels");
+  US_CHECK_ARG(stem_fast_args(a, f), "stem_fwd: shape not supported by the fast kernels");
   launch_tn_fast(f, (hipStream_t)stream);
   US_LAUNCH_CHECK("stem_fwd");
   return 0;

@@ -65,6 +65,9 @@ struct FastTNArgs {
   // issue-order options of the LDS-DMA ring (set by the launcher; UNETSEG_TN_SCHED): bit 0 = the
   // waves of the second SIMD pair issue their K step's DMAs after the first K half's MFMAs
   int sched;
+  // a TN configuration chosen by the caller instead of tn_config's rule (0: the rule) -- the stem's
+  // experiments (UNETSEG_STEM_CFG)
+  int force_cfg;
 };
 
 struct FastWgradArgs {

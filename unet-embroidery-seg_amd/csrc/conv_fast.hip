@@ -1264,6 +1264,7 @@ static bool halo_a_ok(const FastTNArgs& a) {
 static int tn_config_base(const FastTNArgs& a);
 
 static int tn_config(const FastTNArgs& a) {
+  if (a.force_cfg) return a.force_cfg;
   const int c = tn_config_base(a);
   if ((c == 7 || c == 13 || (c == 10 && !getenv("UNETSEG_TN_CFG_NO23"))) && halo_a_ok(a)) return c == 7 ? 21 : c == 13 ? 22 : 23;
   return c;

@@ -63,29 +63,51 @@ __global__ void radix_hist_kernel(const uint32_t* keys, long P, int T, int shift
   hist[((long)b * 256 + threadIdx.x) * T + t] = h[threadIdx.x];
 }
 
-// exclusive scan of hist[b][256*T] (digit-major) in place; one 1024-thread block per segment
-__global__ void radix_scan_kernel(uint32_t* hist, int T) {
-  __shared__ uint32_t part[1024];
-  const int b = blockIdx.x;
+// exclusive scan of hist[b][256*T] (digit-major) in place; one 1024-thread block per segment.  Each
+// thread owns a contiguous run of the segment, loaded once into registers; the runs' totals are
+// scanned with wave shuffles and one LDS exchange of the 16 wave totals.
+constexpr int kScanPer = 32;  // entries per thread held in registers (up to 128 tiles = 524288 pixels per image)
+__global__ __launch_bounds__(1024) void radix_scan_kernel(uint32_t* hist, int T) {
+  __shared__ uint32_t wsum[16];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   uint32_t* h = hist + (long)b * 256 * T;
   const long n = 256L * T;
   const long per = (n + 1023) / 1024;
-  const long lo = threadIdx.x * per, hi = min(n, lo + per);
+  const long lo = tid * per, hi = min(n, lo + per);
+  const bool regs = per <= kScanPer;  // else (more than 524288 pixels per image) two passes over memory
+  uint32_t v[kScanPer];
   uint32_t s = 0;
-  for (long i = lo; i < hi; ++i) s += h[i];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
+  if (regs) {
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+      v[i] = (i < per && lo + i < hi) ? h[lo + i] : 0u;
+      s += v[i];
+    }
+  } else {
+    for (long i = lo; i < hi; ++i) s += h[i];
   }
-  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-  for (long i = lo; i < hi; ++i) {
-    const uint32_t c = h[i];
-    h[i] = run;
-    run += c;
+  // inclusive scan of the per-thread totals within the wave, then across the 16 waves
+  uint32_t x = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  uint32_t run = x - s;
+  for (int w = 0; w < wid; ++w) run += wsum[w];
+  if (regs) {
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+      if (i < per && lo + i < hi) h[lo + i] = run;
+      run += v[i];
+    }
+  } else {
+    for (long i = lo; i < hi; ++i) {
+      const uint32_t c = h[i];
+      h[i] = run;
+      run += c;
+    }
   }
 }
 
