@@ -82,6 +82,13 @@ int unetseg_conv2d_fwd_head_ok(int dtype, int ldc1, int n, int h, int w, int ldy
 int unetseg_conv2d_fwd_head(int dtype, const void* x1, int ldc1, int n, int h, int w, const void* wk,
                             const float* bias, void* y, int ldy, int head_k, const float* head_w, const float* head_b,
                             float* logits, void* stream);
+/* The decoder's 512^2 up_conv conv1 (3x3, 64 -> 64, stride 1, pad 1, bias + ReLU; model/unet_resnet.py:
+ * 90-97): y as unetseg_conv2d_fwd, plus the ReLU mask of the stored y packed to bits, mbits[pixel][8]
+ * (bit e of byte b = y[pixel][8b + e] > 0), which its consumer's data gradient reads (post 4 of
+ * unetseg_conv2d_dgrad_post) instead of the 64-channel activation.  bf16, halo path only; mbits ==
+ * NULL: returns 1 when the shape qualifies, else 0 (host only, nothing launched). */
+int unetseg_conv2d_fwd_mask(int dtype, const void* x1, int ldc1, int n, int h, int w, const void* wk,
+                            const float* bias, void* y, int ldy, unsigned char* mbits, void* stream);
 /* its weight gradient with the same input prologue (workspace: unetseg_conv2d_wgrad_workspace) */
 int unetseg_conv2d_wgrad_bnrelu_in(int dtype, const void* x1, int c1, int ldc1, int n, int h, int w, const void* dy,
                                    int ldy, int cout, const float* in_sc, const float* in_sh, float* ws,
@@ -118,15 +125,17 @@ int unetseg_conv2d_dgrad(int dtype, const void* dy, int ldy, int n, int p, int q
    (post 2: aux = BN input z; psc/psh = BN affine, pmean/pinv = batch stats) mask and writes the
    first backward reduction of that op: part[rows][2][cin] = (sum d, sum d*xhat) per row tile
    (fuses model/resnet_backbone.py:95-110 ReLU+BN backward pass 1 / unet_resnet.py:37-40 ReLU+bias
-   into the consumer conv's dgrad).  part == NULL: returns rows, or -1 when the shape has no fused
-   path (bf16 fast kernels only). */
+   into the consumer conv's dgrad).  post 4: post 1 with the mask read from the producer's packed
+   ReLU bits (aux = mbits of unetseg_conv2d_fwd_mask, ld_aux ignored; 64-channel halo path only).
+   part == NULL: returns rows, or -1 when the shape has no fused path (bf16 fast kernels only). */
 int unetseg_conv2d_dgrad_post(int dtype, const void* dy, int ldy, int n, int p, int q, const void* wt, int cout,
                               int cin, int r, int s, int stride, int pad, void* dx, int ldx, int h, int w, int post,
                               const void* aux, int ld_aux, const float* psc, const float* psh, const float* pmean,
                               const float* pinv, float* part, int rows, void* stream);
-/* 1x1 stride-1 data gradient accumulated onto the residual gradient already in dx (ldx == cin), with the
-   residual BN-add-ReLU backward's first pass in its epilogue (model/resnet_backbone.py:88,110-113: the
-   next block's conv1 is the last consumer of the block output): dx = mask * bf16(dgrad + dx), mask =
+/* 1x1 stride-1 data gradient accumulated onto the other consumers' gradient already in dx (pixel stride
+   ldx >= cin, a multiple of 8: dx may be a channel slice of a skip-concat gradient), with the residual
+   BN-add-ReLU backward's first pass in its epilogue (model/resnet_backbone.py:88,110-113: the next
+   block's conv1 is the last consumer of the block output): dx = mask * bf16(dgrad + dx), mask =
    the packed ReLU bits written by unetseg_bn_apply_mask, part[rows][2 or 3][cin] = (sum d,
    sum d * (y1 - mean1) * inv1 [, sum d * (y2 - mean2) * inv2]) per row tile (y2 = the downsample
    branch's BN input, NULL: none).  Replaces unetseg_bn_bwd_reduce over dx.  part == NULL: returns rows,

@@ -212,7 +212,11 @@ def _key_list(direction, shape):
 
 # residual post-op data gradients (dgrad_post3): the configurations tests/test_gpu_post_res.py drives
 # (N, H, W, K, C) of its SHAPES with a fixed configuration
-POST3_SHAPES = [(16, 128, 128, 64, 256), (4, 64, 64, 128, 512), (16, 32, 32, 256, 1024), (16, 16, 16, 512, 2048)]
+POST3_SHAPES = [(16, 128, 128, 64, 256), (4, 64, 64, 128, 512), (16, 32, 32, 256, 1024), (16, 16, 16, 512, 2048),
+                (16, 128, 128, 128, 256), (16, 64, 64, 256, 512), (16, 32, 32, 512, 1024)]
+
+
+RELU_BITS_SHAPES = [(16, 512, 512), (2, 64, 96)]
 
 
 def covered_keys():
@@ -221,6 +225,9 @@ def covered_keys():
     keys = set()
     for N, H, W, K, C in POST3_SHAPES:
         keys.update(introspect.call_configs(("dgrad_post3", N, H, W, C, 0, K, 1, 1, 1, 0, C, 0)))
+    # ReLU-bit data gradients (dgrad_post4): tests/test_gpu_relu_bits.py's shapes
+    for N, H, W in RELU_BITS_SHAPES:
+        keys.update(introspect.call_configs(("dgrad_post4", N, H, W, 64, 0, 64, 3, 3, 1, 1, 64, 0)))
     for direction, shape, _ in HALO_CASES.values():
         keys.update(_key_list(direction, shape))
     for direction, shape, expect in CASES.values():

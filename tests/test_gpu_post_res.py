@@ -8,7 +8,8 @@ same way -- and its row partials must merge to the float64 sums of d and d * xha
 (tolerance 1e-4 of the sum of |terms|).  Shapes: the bench's conv1 data gradients at the three tile
 configurations the fused epilogue exists for (1 K step: 128x128 single stage; 2-4 steps: the short-K
 single-stage tile; 8 steps at 16x16: the 256x128 ring with one tap), with and without the downsample
-branch.  Model level: a bf16 unet_resnet50 train step with the fusion on and off gives the same forward,
+branch, and each layer's block-0 conv1, whose dx is a channel slice of the decoder's skip-concat gradient
+(pixel stride = the concat width; the other channels must stay untouched).  Model level: a bf16 unet_resnet50 train step with the fusion on and off gives the same forward,
 bit-identical gradients for every parameter the backward reaches before the first fused block, and
 elsewhere gradients as close to the fp32 HIP step as the unfused bf16 step's (median and mean of the
 per-tensor relative L2 within 10 %), while the on/off difference stays below bf16's own deviation from
@@ -39,22 +40,29 @@ def _P(t):
     return 0 if t is None else t.data_ptr()
 
 
-# (N, H, W, K (conv1 output = reduction), C (block channels = dgrad output), second branch, expected config)
+# (N, H, W, K (conv1 output = reduction), C (block channels = dgrad output), second branch, expected config,
+# pixel stride of dx: C, or the decoder's skip-concat width when the gradient is a channel slice of it)
 SHAPES = [
-    (16, 128, 128, 64, 256, False, "tn128x128_1step"),   # layer1 blocks 1-2
-    (4, 64, 64, 128, 512, True, "tn128x128_1st"),        # layer2 block 1 (block 0 below it has a downsample)
-    (16, 32, 32, 256, 1024, False, "tn128x128_1st"),     # layer3
-    (16, 16, 16, 512, 2048, True, "ring256x128_t1"),     # layer4
-    (1, 15, 17, 64, 256, False, None),                   # ragged rows
+    (16, 128, 128, 64, 256, False, "tn128x128_1step", 256),   # layer1 blocks 1-2
+    (4, 64, 64, 128, 512, True, "tn128x128_1st", 512),        # layer2 block 1 (block 0 below it has a downsample)
+    (16, 32, 32, 256, 1024, False, "tn128x128_1st", 1024),    # layer3
+    (16, 16, 16, 512, 2048, True, "ring256x128_t1", 2048),    # layer4
+    (1, 15, 17, 64, 256, False, None, 256),                   # ragged rows
+    # a layer's block 0 conv1, fusing the previous layer's last block (its output is also the decoder's
+    # skip input, up_concat2/3/4 in = 512 / 1024 / 3072 channels: dx is the first C channels of that
+    # gradient, after the downsample branch accumulated onto it)
+    (16, 128, 128, 128, 256, False, "fused", 512),            # layer2.0 conv1 <- layer1.2
+    (16, 64, 64, 256, 512, False, "fused", 1024),             # layer3.0 conv1 <- layer2.3
+    (16, 32, 32, 512, 1024, False, "fused", 3072),            # layer4.0 conv1 <- layer3.5
 ]
 
 
-@pytest.mark.parametrize("N,H,W,K,C,two,cfg", SHAPES)
-def test_dgrad_post_res_kernel(N, H, W, K, C, two, cfg):
+@pytest.mark.parametrize("N,H,W,K,C,two,cfg,ldx", SHAPES)
+def test_dgrad_post_res_kernel(N, H, W, K, C, two, cfg, ldx):
     from unetseg_hip import introspect
     from unetseg_hip.lib import DT_BF16, lib
 
-    if cfg is not None:
+    if cfg is not None and cfg != "fused":
         keys = introspect.call_configs(("dgrad", N, H, W, C, 0, K, 1, 1, 1, 0, C, 0))
         assert keys == [f"dgrad:{cfg}"], keys
     g = torch.Generator(device=DEV).manual_seed(N * 7 + K)
@@ -62,7 +70,8 @@ def test_dgrad_post_res_kernel(N, H, W, K, C, two, cfg):
     dy = torch.randn(N, H, W, K, generator=g, device=DEV).bfloat16()
     w = (torch.randn(K, C, generator=g, device=DEV) / K ** 0.5).bfloat16()
     wt = w.t().contiguous()  # [C][K]: the dgrad B operand image (wt [C][R][S][K] with R = S = 1)
-    old = torch.randn(N, H, W, C, generator=g, device=DEV).bfloat16()
+    wide = torch.randn(N, H, W, ldx, generator=g, device=DEV).bfloat16()
+    old = wide[..., :C].contiguous()
     y1 = torch.randn(N, H, W, C, generator=g, device=DEV).bfloat16()
     mean1 = 0.1 * torch.randn(C, generator=g, device=DEV)
     inv1 = 0.5 + torch.rand(C, generator=g, device=DEV)
@@ -71,8 +80,8 @@ def test_dgrad_post_res_kernel(N, H, W, K, C, two, cfg):
     inv2 = 0.5 + torch.rand(C, generator=g, device=DEV) if two else None
     mbits = torch.randint(0, 256, (M * (C // 8),), generator=g, device=DEV, dtype=torch.uint8)
     st = _st()
-    rows = lib.conv2d_dgrad_post_res(DT_BF16, _P(dy), K, N, H, W, _P(wt), K, C, 0, C, _P(y1), C, 0, 0, 0, 0, 0, 0, 0,
-                                     0, 0, st)
+    rows = lib.conv2d_dgrad_post_res(DT_BF16, _P(dy), K, N, H, W, _P(wt), K, C, 0, ldx, _P(y1), C, 0, 0, 0, 0, 0, 0,
+                                     0, 0, 0, st)
     if cfg is None and rows == 0:
         pytest.skip("no fused kernel for this shape (the op layer falls back)")
     assert rows > 0
@@ -83,10 +92,12 @@ def test_dgrad_post_res_kernel(N, H, W, K, C, two, cfg):
     dref = torch.where(bits, ref.reshape(M, C).float(), torch.zeros(()).to(DEV))
     nq = 3 if two else 2
     part = torch.full((rows, nq, C), float("nan"), device=DEV)
-    dx = old.clone()
-    lib.conv2d_dgrad_post_res(DT_BF16, _P(dy), K, N, H, W, _P(wt), K, C, _P(dx), C, _P(y1), C, _P(mean1), _P(inv1),
+    buf = wide.clone()
+    dx = buf[..., :C]
+    lib.conv2d_dgrad_post_res(DT_BF16, _P(dy), K, N, H, W, _P(wt), K, C, _P(dx), ldx, _P(y1), C, _P(mean1), _P(inv1),
                               _P(mbits), _P(y2), C, _P(mean2), _P(inv2), _P(part), rows, st)
     torch.cuda.synchronize()
+    assert torch.equal(buf[..., C:], wide[..., C:]), "channels past C were written"
     assert torch.equal(dx.reshape(M, C).float(), dref), (dx.reshape(M, C).float() - dref).abs().max().item()
     d64 = dref.double()
     terms = [d64, d64 * ((y1.reshape(M, C).double() - mean1.double()) * inv1.double())]

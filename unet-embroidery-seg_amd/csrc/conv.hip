@@ -943,6 +943,25 @@ UNETSEG_API int unetseg_conv2d_fwd_head(int dtype, const void* x1, int ldc1, int
   return 0;
 }
 
+// 3x3 conv, 64 -> 64 channels, + bias + ReLU (the decoder's 512^2 up_conv conv1,
+// model/unet_resnet.py:90-97) that also stores its output's ReLU mask as bits, mbits[pixel][8] (bit e
+// of byte b = channel 8b + e > 0): the consumer conv's data gradient masks with them (post 4 of
+// unetseg_conv2d_dgrad_post) instead of re-reading the 64-channel activation.  mbits == NULL: returns 1
+// when the shape has this kernel (the halo path), else 0; nothing is launched.
+UNETSEG_API int unetseg_conv2d_fwd_mask(int dtype, const void* x1, int ldc1, int n, int h, int w, const void* wk,
+                                        const float* bias, void* y, int ldy, unsigned char* mbits, void* stream) {
+  FastTNArgs f;
+  const bool ok = dtype == DT_BF16 && ldy >= 64 && ldy % 8 == 0 && ldc1 % 8 == 0 &&
+                  head_args(x1 ? x1 : kSomePtr, ldc1, n, h, w, wk ? wk : kSomePtr, ldy, f);
+  if (!mbits) return ok ? 1 : 0;
+  US_CHECK_ARG(ok, "conv2d_fwd_mask: needs bf16, 64 -> 64 channels on the halo path");
+  US_CHECK_ARG(x1 && wk && bias && y, "conv2d_fwd_mask: null pointer");
+  f.y = y; f.bias = bias; f.relu = 1; f.mbits_out = mbits;
+  US_CHECK_ARG(launch_halo3(f, (hipStream_t)stream) == 0, "conv2d_fwd_mask: launch refused");
+  US_LAUNCH_CHECK("conv2d_fwd_mask");
+  return 0;
+}
+
 // Weight gradient of that conv: X = relu(x1 * in_sc + in_sh) staged on the fly (fast bf16 wgrad),
 // then the usual deterministic split-K reduce into dw (fp32 [cout][dw_c], (+)= with accumulate).
 UNETSEG_API int unetseg_conv2d_wgrad_bnrelu_in(int dtype, const void* x1, int c1, int ldc1, int n, int h, int w,
@@ -1112,7 +1131,8 @@ UNETSEG_API int unetseg_conv2d_dgrad_post(int dtype, const void* dy, int ldy, in
                                           int h, int w, int post, const void* aux, int ld_aux, const float* psc,
                                           const float* psh, const float* pmean, const float* pinv, float* part,
                                           int rows, void* stream) {
-  US_CHECK_ARG(post == 1 || post == 2, "conv2d_dgrad_post: post must be 1 (ReLU) or 2 (BN-ReLU)");
+  US_CHECK_ARG(post == 1 || post == 2 || post == 4,
+               "conv2d_dgrad_post: post must be 1 (ReLU), 2 (BN-ReLU) or 4 (ReLU from mask bits)");
   if (dtype != DT_BF16 || stride < 1 || stride > 2 || cout % 8 || ldy % 8) return -1;
   // every parity class must take the fast path (the generic kernel has no post-op epilogue)
   int total = 0;
@@ -1126,6 +1146,10 @@ UNETSEG_API int unetseg_conv2d_dgrad_post(int dtype, const void* dy, int ldy, in
       FastTNArgs f;
       if (!fast_tn_args(a, f)) return -1;
       f.post = post; f.aux = aux; f.ld_aux = ld_aux; f.psc = psc; f.psh = psh; f.pmean = pmean; f.pinv = pinv;
+      if (post == 4) {  // mask bits (unetseg_conv2d_fwd_mask): the 64-channel halo kernel only
+        if (tn_fast_config(f, nullptr) != 0) return -1;
+        f.mbits = static_cast<const unsigned char*>(aux);
+      }
       fs[ncls++] = f;
       total += tn_fast_post_rows(f);
     }
@@ -1139,7 +1163,7 @@ UNETSEG_API int unetseg_conv2d_dgrad_post(int dtype, const void* dy, int ldy, in
   if (!part) return total;
   US_CHECK_ARG(dy && wt && dx && aux, "conv2d_dgrad_post: null pointer");
   US_CHECK_ARG(rows == total, "conv2d_dgrad_post: rows %d != %d", rows, total);
-  US_CHECK_ARG(post == 1 || (psc && psh && pmean && pinv), "conv2d_dgrad_post: BN post needs its coefficients");
+  US_CHECK_ARG(post != 2 || (psc && psh && pmean && pinv), "conv2d_dgrad_post: BN post needs its coefficients");
   hipStream_t st = (hipStream_t)stream;
   int off = 0;
   FastTNArgs m[4];
@@ -1168,7 +1192,8 @@ UNETSEG_API int unetseg_conv2d_dgrad_post_res(int dtype, const void* dy, int ldy
                                               const float* mean1, const float* inv1, const unsigned char* mbits,
                                               const void* y2, int ld2, const float* mean2, const float* inv2,
                                               float* part, int rows, void* stream) {
-  if (dtype != DT_BF16 || n <= 0 || p <= 0 || q <= 0 || cout % 8 || ldy % 8 || cin % 8 || ldx != cin) return 0;
+  if (dtype != DT_BF16 || n <= 0 || p <= 0 || q <= 0 || cout % 8 || ldy % 8 || cin % 8 || ldx < cin || ldx % 8)
+    return 0;
   IgemmArgs a;
   if (!dgrad_classes(dy ? dy : kSomePtr, ldy, n, p, q, wt ? wt : kSomePtr, cout, cin, 1, 1, 1, 0,
                      dx ? dx : const_cast<void*>(kSomePtr), ldx, p, q, 0, 0, a) || a.M <= 0)

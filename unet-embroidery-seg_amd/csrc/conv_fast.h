@@ -68,6 +68,9 @@ struct FastTNArgs {
   // a TN configuration chosen by the caller instead of tn_config's rule (0: the rule) -- the stem's
   // experiments (UNETSEG_STEM_CFG)
   int force_cfg;
+  // halo forward with bias + ReLU: also store the output's ReLU mask as bits, [M][Ng/8] (bit e of byte
+  // b = channel 8b + e > 0); post 4 = post 1 with the mask read from such bits (mbits, halo path only)
+  unsigned char* mbits_out;
 };
 
 struct FastWgradArgs {

@@ -1356,6 +1356,7 @@ static int launch_tn_post_res(const FastTNArgs& a, hipStream_t st) {
 int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
   if (a.M <= 0 || a.Ng <= 0) return 0;
   if (a.post == 3) return a.in_sc ? -1 : launch_tn_post_res(a, st);
+  if (a.post == 4) return tn_config(a) == 0 ? launch_halo3(a, st) : -1;  // mask bits: halo path only
   if (a.in_sc) {  // input prologue (fwd only: no post-op), register-staged configurations
     switch (tn_config(a)) {
       case 1: return launch_tn_cfg<256, 64, 4, 1, 2, false, 0, true>(a, st);

@@ -39,7 +39,10 @@ __device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, unsigned off,
 // kEpiHead1 / kEpiHead2: the model's final 1x1 conv (64 -> 1 or 2 logits) on the rounded outputs
 // (model/unet_resnet.py:99-103 `final`, model/unet_multitask.py seg_head): the 512^2 activation is
 // not read back by a separate head pass.
-constexpr int kEpiBias = 1, kEpiRelu = 2, kEpiStats = 4, kEpiAcc = 8, kEpiDyn = 16, kEpiHead1 = 32, kEpiHead2 = 64;
+// kEpiMask: the ReLU mask of the stored output packed to bits, mbits_out[pixel][Ng/8] (bit e of byte b =
+// channel 8b + e > 0) -- the consumer's data gradient (post 4) reads 1/16 of what the activation costs.
+constexpr int kEpiBias = 1, kEpiRelu = 2, kEpiStats = 4, kEpiAcc = 8, kEpiDyn = 16, kEpiHead1 = 32, kEpiHead2 = 64,
+              kEpiMask = 128;
 
 __device__ __forceinline__ void bstore32(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
   asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
@@ -55,6 +58,9 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   const bool do_acc = kDyn ? a.accumulate != 0 : (EPI & kEpiAcc) != 0;
   constexpr int HK = (EPI & kEpiHead2) ? 2 : (EPI & kEpiHead1) ? 1 : 0;  // fused head logits
   static_assert(HK == 0 || (!kDyn && POST == 0), "the fused head rides on a fixed bias + ReLU epilogue");
+  constexpr bool kMask = (EPI & kEpiMask) != 0;
+  static_assert(!kMask || (!kDyn && POST == 0 && HK == 0 && (EPI & kEpiRelu)), "mask bits of a ReLU output");
+  // POST 4: post 1 with the ReLU mask read from packed bits (a.mbits, the kEpiMask layout)
   // wave w owns output rows [w*TH/NW, (w+1)*TH/NW)
   constexpr int RPW = TH / NW;               // rows per wave
   constexpr int FP = RPW * (HW_TW / 16);     // 16-pixel groups per wave
@@ -85,6 +91,8 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   const unsigned hw_img = (unsigned)(a.OH * a.OW);
   const __amdgpu_buffer_rsrc_t rh = srd(HK ? (const void*)a.head_y : a.y,
                                         HK ? (unsigned)(a.M / (a.OH * a.OW)) * HK * hw_img * 4u : 0u);
+  const __amdgpu_buffer_rsrc_t rmb =
+      srd(kMask ? (const void*)a.mbits_out : a.y, kMask ? (unsigned)a.M * (unsigned)(a.Ng >> 3) : 0u);
 
   if (kDyn && a.bias && tid < 64) sbias[tid] = a.bias[n0 + tid];
   // BN post-op coefficients of this block's 64 channels live in `red` (free in dgrad: no stats)
@@ -178,7 +186,19 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     if (t + 1 < my_tiles) issue_halo(t + 1, stage ^ 1);
     // post-op: this tile's aux values are loaded now, so their latency hides under the tap loop
     uint2 zr[FC][FP];
-    if (POST) {
+    uint2 zb[FP];  // POST 4: the 8 mask bytes (64 channels) of this lane's pixel
+    if (POST == 4) {
+      const int sp = slot + t * G_per;
+      const int tw = sp % tiles_w, rest = sp / tiles_w;
+      const int th = rest % tiles_h, nb = rest / tiles_h;
+#pragma unroll
+      for (int p = 0; p < FP; ++p) {
+        const int r = wid * RPW + p / (HW_TW / 16);
+        const int col = (p % (HW_TW / 16)) * 16 + j16;
+        const long opix = ((long)nb * a.OH + th * TH + r) * a.OW + tw * HW_TW + col;
+        zb[p] = *reinterpret_cast<const uint2*>(a.mbits + opix * (a.Ng >> 3) + (n0 >> 3));
+      }
+    } else if (POST) {
       const int sp = slot + t * G_per;
       const int tw = sp % tiles_w, rest = sp / tiles_w;
       const int th = rest % tiles_h, nb = rest / tiles_h;
@@ -237,13 +257,15 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
 #pragma unroll
       for (int e = 0; e < 4; ++e) csum[c][e] = 0.f;
     uint2 outv[FC][FP];
-    unsigned outo[FP];
+    unsigned outo[FP], mko[FP], mkx[FP], mky[FP];
 #pragma unroll
     for (int p = 0; p < FP; ++p) {
       const int r = wid * RPW + p / (HW_TW / 16);
       const int col = (p % (HW_TW / 16)) * 16 + j16;
       const long opix = ((long)nb * a.OH + th * TH + r) * a.OW + tw * HW_TW + col;
       outo[p] = (unsigned)(opix * a.ldy + n0) * 2u;
+      mko[p] = (unsigned)(opix * (a.Ng >> 3) + (n0 >> 3));
+      mkx[p] = mky[p] = 0u;
 #pragma unroll
       for (int c = 0; c < FC; ++c) {
         const int cb = c * 16 + kg * 4;
@@ -264,12 +286,15 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
           o[e] = (bf16)v[e];
           v[e] = (float)o[e];
         }
-        if (POST) {  // mask with the producer's ReLU (from aux) and accumulate backward partials
+        if (POST) {  // mask with the producer's ReLU (from aux or its bits) and accumulate backward partials
           const bf16* z = reinterpret_cast<const bf16*>(&zr[c][p]);
+          // POST 4: byte 2c + kg/2 of the pixel's 8, high nibble for odd kg
+          const unsigned nib =
+              POST == 4 ? ((c < 2 ? zb[p].x : zb[p].y) >> ((((2 * c + (kg >> 1)) & 3) * 8) + (kg & 1) * 4)) & 15u : 0u;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float zf = (float)z[e];
-            bool on = zf > 0.f;
+            const float zf = POST == 4 ? 0.f : (float)z[e];
+            bool on = POST == 4 ? ((nib >> e) & 1u) != 0u : zf > 0.f;
             float xh = 0.f;
             if (POST == 2) {
               const int ch = cb + e;
@@ -288,6 +313,23 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
           acc[c][p][e] = v[e];
         }
         outv[c][p] = *reinterpret_cast<uint2*>(o);
+        if (kMask) {  // this lane's 4 channels -> its nibble of byte 2c + kg/2 (word x: c < 2, y: c >= 2)
+          unsigned nb4 = 0u;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) nb4 |= (v[e] > 0.f ? 1u : 0u) << e;
+          const unsigned sh = (((2 * c + (kg >> 1)) & 3) * 8) + (kg & 1) * 4;
+          if (c < 2) mkx[p] |= nb4 << sh;
+          else mky[p] |= nb4 << sh;
+        }
+      }
+    }
+    if (kMask) {  // OR the four channel groups' nibbles (lanes j16 + 16 kg): disjoint bits
+#pragma unroll
+      for (int p = 0; p < FP; ++p) {
+        mkx[p] |= __shfl_xor(mkx[p], 16);
+        mkx[p] |= __shfl_xor(mkx[p], 32);
+        mky[p] |= __shfl_xor(mky[p], 16);
+        mky[p] |= __shfl_xor(mky[p], 32);
       }
     }
     if (HK) {
@@ -367,9 +409,14 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     for (int p = 0; p < FP; ++p)
 #pragma unroll
       for (int c = 0; c < FC; ++c) bstore64(ry, outo[p] + (c * 16 + kg * 4) * 2, outv[c][p]);
-    // next halo landed (all but this tile's FP*FC stores retired) and every wave is done with
-    // both the current stage (WAR for the DMA after next) and `red`
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(FP * FC + FP * HK) : "memory");
+    // mask bytes: lanes kg == 0 store the pixel's 8 bytes, the others' stores go out of range (every
+    // wave issues exactly FP of them)
+    if (kMask)
+#pragma unroll
+      for (int p = 0; p < FP; ++p) bstore64(rmb, kg == 0 ? mko[p] : kOOB, uint2{mkx[p], mky[p]});
+    // next halo landed (all but this tile's stores retired) and every wave is done with both the
+    // current stage (WAR for the DMA after next) and `red`
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(FP * FC + FP * HK + (kMask ? FP : 0)) : "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (POST) {
@@ -1087,6 +1134,11 @@ int launch_halo3(const FastTNArgs& a, hipStream_t st) {
     return a.head_k == 2 ? launch_halo3_cfg<8, 8, 0, kEpiBias | kEpiRelu | kEpiHead2>(a, st)
                          : launch_halo3_cfg<8, 8, 0, kEpiBias | kEpiRelu | kEpiHead1>(a, st);
   }
+  if (a.mbits_out) {  // ReLU mask bits: bias + ReLU epilogue only (checked by the caller)
+    if (a.post || epi != (kEpiBias | kEpiRelu)) return -1;
+    return launch_halo3_cfg<8, 8, 0, kEpiBias | kEpiRelu | kEpiMask>(a, st);
+  }
+  if (a.post == 4) return epi == 0 ? launch_halo3_cfg<8, 8, 4, 0>(a, st) : -1;
   // fused dgrad post-ops come with a plain epilogue (no bias / ReLU / stats / accumulate)
   if (a.post == 1) return epi == 0 && !dyn ? launch_halo3_cfg<8, 8, 1, 0>(a, st) : launch_halo3_cfg<8, 8, 1, kEpiDyn>(a, st);
   if (a.post == 2) return epi == 0 && !dyn ? launch_halo3_cfg<8, 8, 2, 0>(a, st) : launch_halo3_cfg<8, 8, 2, kEpiDyn>(a, st);

@@ -49,13 +49,15 @@ class Bottleneck(nn.Module):
 
 
 def run_bottleneck(ctx, b, x):
-    # the downsample conv is recorded first so that, in the reversed tape, conv1's full-coverage
-    # data gradient initialises x.grad and the (stride-2, one-parity-class) downsample gradient
-    # only accumulates into the pixels it reaches
+    # conv1 is recorded before the downsample conv: in the reversed tape it delivers the last
+    # contribution to x.grad (after the decoder's skip concat and the downsample branch), so it can
+    # run the previous block's residual BN backward pass 1 in its epilogue (ops._dgrad_fused_res).
+    # A stride-2 downsample data gradient that initialises x.grad writes zeros on the parity
+    # classes it does not reach.
+    a1 = ops.conv_bn(ctx, x, b.conv1._pc, b.bn1)
     yd = sd = None
     if b.downsample is not None:
         yd, sd = ops.conv(ctx, x, b.downsample[0]._pc, stats=True)
-    a1 = ops.conv_bn(ctx, x, b.conv1._pc, b.bn1)
     a2 = ops.conv_bn(ctx, a1, b.conv2._pc, b.bn2, lazy=True)  # conv3 applies bn2-ReLU on load
     y3, s3 = ops.conv(ctx, a2, b.conv3._pc, stats=True)
     if b.downsample is not None:

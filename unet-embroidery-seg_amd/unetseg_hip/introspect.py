@@ -40,7 +40,7 @@ def call_configs(desc, dt=DT_BF16):
     if d == "fwd_bnrelu_in":  # 1x1 conv applying the producer's BN-ReLU on load (register-staged)
         cfg = _lib.load().unetseg_conv2d_fwd_bnrelu_in_config(dt, C1, ld1 or C1, N, H, W, K)
         return ["fwd_bnrelu_in:" + _lib.CFG_NAMES.get(cfg, str(cfg))]
-    if d in ("dgrad", "dgrad_post1", "dgrad_post2", "dgrad_post3"):
+    if d in ("dgrad", "dgrad_post1", "dgrad_post2", "dgrad_post3", "dgrad_post4"):
         tag = "dgrad" if d == "dgrad" else d
         return [f"{tag}:{c}" for c in _lib.dgrad_config(dt, K, N, Pq, Qq, K, cin, R, S, stride, pad, cin, H, W)]
     if d == "dgrad_padk":

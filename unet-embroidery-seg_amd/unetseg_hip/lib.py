@@ -42,6 +42,7 @@ SIGNATURES = {
     "unetseg_upsample2x_bwd_tiles": (I, [I, I, I, I, I]),
     "unetseg_upsample2x_bwd_relu": (I, [I, P, I, I, I, I, I, I, P, I, P, I, P, I, P]),
     "unetseg_conv2d_fwd_head": (I, [I, P, I, I, I, I, P, P, P, I, I, P, P, P, P]),
+    "unetseg_conv2d_fwd_mask": (I, [I, P, I, I, I, I, P, P, P, I, P, P]),
     "unetseg_conv2d_wgrad_bnrelu_in": (I, [I, P, I, I, I, I, I, P, I, I, P, P, P, SZ, P, I, I, P]),
     "unetseg_conv2d_fwd_affine": (I, [I, P, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P, P, I, P, I, P]),
     "unetseg_bn_finalize": (I, [P, I, I, L, I, P, P, P, P, P, F, F, P, P, P, P, P]),
@@ -123,7 +124,7 @@ SIGNATURES = {
 }
 
 #: functions returning a value rather than a status (no RuntimeError on non-zero)
-VALUE_FUNCS = {"reduce_tiles", "pw_small_tiles", "conv_tile_m", "abi_version", "conv2d_fwd_tile_m",
+VALUE_FUNCS = {"conv2d_fwd_mask", "reduce_tiles", "pw_small_tiles", "conv_tile_m", "abi_version", "conv2d_fwd_tile_m",
                "conv2d_dgrad_post", "conv2d_dgrad_post_res", "stem_fwd_tile_m", "attn_bwd1_tiles", "pw_small_tile", "conv2d_fwd_config",
                "conv2d_dgrad_config", "conv2d_wgrad_config", "stem_config", "pw_head_tiles", "channel_stats_tiles",
                "augment_tables_len", "pack_tiles",

@@ -37,7 +37,7 @@ class Node:
     ``lazy`` (a BNState): the node stands for relu(BN(data)) that was never stored -- ``data`` is the
     BN input and the consuming conv applies BN-ReLU on load (``bn(..., lazy=True)``)."""
 
-    __slots__ = ("data", "grad", "need_grad", "uses", "fuse", "fused", "lazy", "head")
+    __slots__ = ("data", "grad", "need_grad", "uses", "fuse", "fused", "lazy", "head", "mbits")
 
     def __init__(self, data, need_grad=True):
         self.data = data
@@ -48,6 +48,7 @@ class Node:
         self.fused = None
         self.lazy = None
         self.head = None  # (head Conv2d, fp32 logits) computed by the producing conv's epilogue
+        self.mbits = None  # packed ReLU mask of data (unetseg_conv2d_fwd_mask), read by post 4
 
     @property
     def shape(self):
@@ -66,6 +67,9 @@ FUSE = os.environ.get("UNETSEG_NO_FUSE", "0") != "1"
 FUSE_HEAD = os.environ.get("UNETSEG_NO_HEAD_FUSE", "0") != "1"
 #: the ReLU backward of an upsample's input inside the upsample backward (UNETSEG_NO_UP_FUSE=1 disables)
 FUSE_UP = os.environ.get("UNETSEG_NO_UP_FUSE", "0") != "1"
+#: a 64-channel halo conv + bias + ReLU stores its ReLU mask as bits for the consumer's data gradient
+#: (post 4) instead of that dgrad re-reading the activation (UNETSEG_NO_RELU_BITS=1 disables)
+RELU_BITS = os.environ.get("UNETSEG_NO_RELU_BITS", "0") != "1"
 
 
 _WORKSPACES = {}
@@ -347,6 +351,8 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
         _materialize(ctx, x1)
         lazy = None
     use(x1, x2)
+    # x1's first consumer in the forward delivers the last contribution to its gradient in the backward
+    last_grad = x1.uses == 1
     X1 = x1.data
     N, H, W, C1 = X1.shape
     X2 = x2.data if x2 is not None else None
@@ -366,6 +372,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
     # probe descriptor: (N, H, W, C1, C2, K, R, S, stride, pad, ld1, ld2); bench/tools map it to the
     # kernel configuration through the unetseg_conv2d_*_config queries
     desc = (N, H, W, C1, C2, K, R, S, stride, pad, ldp(X1), ldp(X2))
+    mbits = None
     if lazy is not None:
         with _probe("igemm_tn", flops, 1, ("fwd_bnrelu_in",) + desc):
             lib.conv2d_fwd_bnrelu_in(ctx.dt, P(X1), C1, ldp(X1), N, H, W, P(pc.wk), K, P(lazy.sc), P(lazy.sh), P(b),
@@ -382,11 +389,24 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
         head = (head, logits)
     else:
         head = None
-        with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
-            lib.conv2d_fwd(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride, pad,
-                           P(b), int(relu), P(y), ldp(y), P(st[0] if st else None), ctx.stream)
+        mbits = None
+        if (RELU_BITS and FUSE and relu and b is not None and x2 is None and st is None and ctx.training and
+                ctx.tape is not None and K == 64 and C1 == 64 and (R, S, stride, pad) == (3, 3, 1, 1) and
+                lib.conv2d_fwd_mask(ctx.dt, 0, ldp(X1), N, H, W, 0, 0, 0, ldp(y), 0, 0) == 1):
+            mbits = torch.empty(M * 8, dtype=torch.uint8, device=ctx.device)
+            with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
+                rc = lib.conv2d_fwd_mask(ctx.dt, P(X1), ldp(X1), N, H, W, P(pc.wk), P(b), P(y), ldp(y), P(mbits),
+                                         ctx.stream)
+            if rc != 0:
+                raise RuntimeError(f"unetseg_conv2d_fwd_mask failed ({rc}): {lib_last_error()}")
+        else:
+            with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
+                lib.conv2d_fwd(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(pc.wk), K, R, S, stride,
+                               pad, P(b), int(relu), P(y), ldp(y), P(st[0] if st else None), ctx.stream)
     out = Node(y)
     out.head = head
+    if mbits is not None:
+        out.mbits = mbits
     if relu:
         out.fuse = (1, y, None)
 
@@ -469,7 +489,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                     lib.conv2d_dgrad(ctx.dt, P(dY), Kp, N, Pq, Qq, P(wtp), Kp, C1, 1, 1, 1, 0, P(g), ldp(g), H, W, acc,
                                      ctx.stream)
         elif x2 is None:
-            if x1.need_grad and not _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
+            if x1.need_grad and not _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc, last_grad):
                 g, acc = gbuf(ctx, x1)
                 with _probe("igemm_tn", flops, _dgrad_launches(ctx, ldp(dY), N, Pq, Qq, K, C1, R, S, stride, pad, H, W),
                             ("dgrad",) + desc):
@@ -533,40 +553,44 @@ def conv_bn(ctx, x, pc, bnm, x2=None, lazy=False):
 #: the residual BN-add-ReLU backward's first pass in the next block's conv1 data gradient
 #: (unetseg_conv2d_dgrad_post_res; UNETSEG_NO_POST_RES=1: separate bn_bwd_reduce pass)
 FUSE_RES = os.environ.get("UNETSEG_NO_POST_RES", "0") != "1"
+#: ... also when the block output has more consumers than the next block (a layer's last block: the next
+#: layer's downsample conv and the decoder's skip concat) (UNETSEG_NO_POST_RES_MULTI=1: next block only)
+FUSE_RES_MULTI = os.environ.get("UNETSEG_NO_POST_RES_MULTI", "0") != "1"
 
 
-def _dgrad_fused_res(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
+def _dgrad_fused_res(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc, last_grad):
     """x1 is a bottleneck output relu(BN3(y3) + residual) (model/resnet_backbone.py:110-113) consumed by
-    this 1x1 conv (the next block's conv1) and by that block's residual add, whose gradient is already
-    in x1.grad: accumulate the dgrad onto it, mask with the stored ReLU bits and write BN3's backward
-    partials in the epilogue (and the downsample BN's, block 0) -- the producer's bn_bwd_reduce pass
-    over the gradient is not run."""
-    if not (FUSE_RES and x1.fuse is not None and x1.fuse[0] == 3 and x1.grad is not None and x1.uses == 2 and
-            ctx.dt == DT_BF16 and (pc.R, pc.S) == (1, 1) and pc.conv.stride in (1, (1, 1)) and
-            x1.grad.is_contiguous() and ldp(x1.grad) == C1 and H == Pq and W == Qq):
+    this 1x1 conv (the next block's conv1) and by others whose gradients are already in x1.grad (the
+    next block's residual add; for a layer's last block, the next layer's downsample conv and the
+    decoder's skip concat): when this conv delivers the last contribution, accumulate the dgrad onto
+    x1.grad, mask with the stored ReLU bits and write BN3's backward partials in the epilogue (and the
+    downsample BN's, block 0) -- the producer's bn_bwd_reduce pass over the gradient is not run."""
+    if not (FUSE_RES and x1.fuse is not None and x1.fuse[0] == 3 and x1.grad is not None and last_grad and
+            (x1.uses == 2 or (FUSE_RES_MULTI and x1.uses > 2)) and ctx.dt == DT_BF16 and (pc.R, pc.S) == (1, 1) and pc.conv.stride in (1, (1, 1)) and
+            x1.grad.stride(-1) == 1 and ldp(x1.grad) % 8 == 0 and H == Pq and W == Qq):
         return False
     _, y3, s1, mbits, y2, s2 = x1.fuse
     K = pc.K
-    rows = lib.conv2d_dgrad_post_res(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, 0, C1, P(y3), ldp(y3), 0, 0,
-                                     0, 0, 0, 0, 0, 0, 0, ctx.stream)
+    g = x1.grad
+    rows = lib.conv2d_dgrad_post_res(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, 0, ldp(g), P(y3), ldp(y3),
+                                     0, 0, 0, 0, 0, 0, 0, 0, 0, ctx.stream)
     if rows <= 0:
         return False
     nq = 3 if y2 is not None else 2
     part = ctx.f32(rows, nq, C1)
-    g = x1.grad
     with _probe("igemm_tn", flops, 1, ("dgrad_post3",) + desc):
-        lib.conv2d_dgrad_post_res(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, P(g), C1, P(y3), ldp(y3),
+        lib.conv2d_dgrad_post_res(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, P(g), ldp(g), P(y3), ldp(y3),
                                   P(s1.mean), P(s1.inv), P(mbits), P(y2), ldp(y2), P(s2.mean if s2 else None),
                                   P(s2.inv if s2 else None), P(part), rows, ctx.stream)
     x1.fused = (part, rows, nq)
     return True
 
 
-def _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
+def _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc, last_grad=False):
     """dgrad into x1.grad with the backward mask + first reduction of the ReLU / BN-ReLU that
     produced x1 fused into the epilogue.  Only when this conv is x1's sole consumer (so its dgrad
     is x1's whole gradient) and the shape has a fused kernel; returns False otherwise."""
-    if _dgrad_fused_res(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
+    if _dgrad_fused_res(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc, last_grad):
         return True
     if not (FUSE and x1.fuse is not None and x1.fuse[0] != 3 and x1.grad is None and x1.uses == 1 and
             ctx.dt == DT_BF16):
@@ -576,14 +600,22 @@ def _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc):
     stride, pad = pc.conv.stride, pc.conv.padding
     args = [ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, R, S, stride, pad]
     coeffs = [P(st.sc), P(st.sh), P(st.mean), P(st.inv)] if kind == 2 else [0, 0, 0, 0]
-    rows = lib.conv2d_dgrad_post(*args, 0, C1, H, W, kind, P(aux), ldp(aux), *coeffs, 0, 0, ctx.stream)
+    rows = -1
+    if kind == 1 and x1.mbits is not None:
+        # the producer stored its ReLU mask as bits: post 4 reads them instead of the activation
+        rows = lib.conv2d_dgrad_post(*args, 0, C1, H, W, 4, P(x1.mbits), 0, *coeffs, 0, 0, ctx.stream)
+        if rows > 0:
+            kind, aux = 4, x1.mbits
+    if rows <= 0:
+        rows = lib.conv2d_dgrad_post(*args, 0, C1, H, W, kind, P(aux), ldp(aux), *coeffs, 0, 0, ctx.stream)
     if rows <= 0:
         return False
     g = ctx.empty(N, H, W, C1)
     part = ctx.f32(rows, 2, C1)
     with _probe("igemm_tn", flops, _dgrad_launches(ctx, ldp(dY), N, Pq, Qq, K, C1, R, S, stride, pad, H, W),
                 (f"dgrad_post{kind}",) + desc):
-        rc = lib.conv2d_dgrad_post(*args, P(g), C1, H, W, kind, P(aux), ldp(aux), *coeffs, P(part), rows, ctx.stream)
+        rc = lib.conv2d_dgrad_post(*args, P(g), C1, H, W, kind, P(aux), 0 if kind == 4 else ldp(aux), *coeffs,
+                                   P(part), rows, ctx.stream)
     if rc != 0:
         raise RuntimeError(f"unetseg_conv2d_dgrad_post failed ({rc}): {lib_last_error()}")
     x1.grad = g
