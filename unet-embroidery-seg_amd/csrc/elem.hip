@@ -552,6 +552,137 @@ __global__ void maxpool_fwd_kernel(const T* x, int ldx, int N, int H, int W, int
   }
 }
 
+// The ResNet stem's pool (model/resnet_backbone.py:135: 3x3, stride 2, ceil mode) with the window
+// compile-time: unrolled taps, 32-bit indexing, the 8 (bf16) argmax bytes of a pixel stored with one
+// 8-B store.  Same comparisons in the same order as maxpool_fwd_kernel (bit-identical).
+template <typename T>
+__global__ void maxpool_fwd_k3s2_kernel(const T* x, int ldx, int N, int H, int W, int C, int P, int Q, T* y, int ldy,
+                                        uint8_t* idx) {
+  constexpr int V = VE<T>;
+  const int cv = C / V;
+  const int total = N * P * Q * cv;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    int t = i;
+    const int v = t % cv; t /= cv;
+    const int q = t % Q; t /= Q;
+    const int p = t % P;
+    const int n = t / P;
+    const int c0 = v * V;
+    float best[V];
+    uint8_t bi[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int h = p * 2 + r;
+      if (h >= H) break;
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int w = q * 2 + u;
+        if (w >= W) break;
+        float xv[V];
+        load_vec(x + (size_t)((n * H + h) * W + w) * ldx + c0, xv);
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          if (xv[e] > best[e] || isnan(xv[e])) {
+            if (!isnan(best[e])) { best[e] = xv[e]; bi[e] = (uint8_t)(r * 3 + u); }
+          }
+      }
+    }
+    const size_t opix = (size_t)((n * P + p) * Q + q);
+    store_vec(y + opix * ldy + c0, best);
+    if constexpr (V == 8) {
+      uint2 pk;
+      __builtin_memcpy(&pk, bi, 8);
+      *reinterpret_cast<uint2*>(idx + opix * C + c0) = pk;
+    } else {
+      unsigned pk;
+      __builtin_memcpy(&pk, bi, 4);
+      *reinterpret_cast<unsigned*>(idx + opix * C + c0) = pk;
+    }
+  }
+}
+
+// Its gradient: one thread per 2x2 input block (h = 2i + a, w = 2j + b) and V channels.  The windows
+// that contain the block are (i-1 | i) x (j-1 | j); window (p, q) reaches row a of the block as window
+// row r = a + 2 (p = i - 1, a = 0 only) or r = a (p = i), likewise columns.  Each window's dy and
+// argmax bytes are loaded once per block (the per-pixel gather loaded them up to 9 times and the
+// bytes one at a time); every pixel sums its windows in the same (p, q) order as maxpool_bwd_kernel.
+template <typename T>
+__global__ void maxpool_bwd_k3s2_kernel(const T* dy, int ldy, const uint8_t* idx, int N, int H, int W, int C, int P,
+                                        int Q, T* dx, int ldx, int accumulate) {
+  constexpr int V = VE<T>;
+  const int cv = C / V;
+  const int Hh = (H + 1) >> 1, Wh = (W + 1) >> 1;
+  const int total = N * Hh * Wh * cv;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    int t = i;
+    const int v = t % cv; t /= cv;
+    const int bj = t % Wh; t /= Wh;
+    const int bi = t % Hh;
+    const int n = t / Hh;
+    const int c0 = v * V;
+    float acc[4][V];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[k][e] = 0.f;
+#pragma unroll
+    for (int dp = 0; dp < 2; ++dp) {
+      const int p = bi - 1 + dp;
+      if (p < 0 || p >= P) continue;
+#pragma unroll
+      for (int dq = 0; dq < 2; ++dq) {
+        const int q = bj - 1 + dq;
+        if (q < 0 || q >= Q) continue;
+        const size_t opix = (size_t)((n * P + p) * Q + q);
+        float g[V];
+        load_vec(dy + opix * ldy + c0, g);
+        uint8_t ib[V];
+        if constexpr (V == 8) {
+          const uint2 pk = *reinterpret_cast<const uint2*>(idx + opix * C + c0);
+          __builtin_memcpy(ib, &pk, 8);
+        } else {
+          const unsigned pk = *reinterpret_cast<const unsigned*>(idx + opix * C + c0);
+          __builtin_memcpy(ib, &pk, 4);
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const int r = dp ? a : a + 2;
+          if (r >= 3) continue;
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int u = dq ? b : b + 2;
+            if (u >= 3) continue;
+            const uint8_t want = (uint8_t)(r * 3 + u);
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+              if (ib[e] == want) acc[a * 2 + b][e] += g[e];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int h = 2 * bi + a;
+      if (h >= H) continue;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int w = 2 * bj + b;
+        if (w >= W) continue;
+        T* o = dx + (size_t)((n * H + h) * W + w) * ldx + c0;
+        if (accumulate) {
+          float old[V];
+          load_vec(o, old);
+#pragma unroll
+          for (int e = 0; e < V; ++e) acc[a * 2 + b][e] += old[e];
+        }
+        store_vec(o, acc[a * 2 + b]);
+      }
+    }
+  }
+}
+
 // gather form: dx[h][w] (+)= sum over windows containing (h,w) whose argmax is (h,w)
 template <typename T>
 __global__ void maxpool_bwd_kernel(const T* dy, int ldy, const uint8_t* idx, int N, int H, int W, int C, int k, int s,
@@ -1553,9 +1684,15 @@ UNETSEG_API int unetseg_maxpool_fwd(int dtype, const void* x, int ldx, int n, in
   if (p_out) *p_out = p;
   if (q_out) *q_out = q;
   if (!y) return 0;  // shape query
-  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(grid_for((long)n * p * q * c / VE<T>)), dim3(256),
-                                       0, (hipStream_t)stream, (const T*)x, ldx, n, h, w, c, k, s, p, q, (T*)y, ldy,
-                                       idx));
+  if (k == 3 && s == 2 && (long)n * h * w * c < (1L << 31) && (long)n * h * w * ldx < (1L << 31) &&
+      (long)n * p * q * ldy < (1L << 31) && !getenv("UNETSEG_MAXPOOL_GENERIC"))
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_k3s2_kernel<T>, dim3(grid_for((long)n * p * q * c / VE<T>)),
+                                         dim3(256), 0, (hipStream_t)stream, (const T*)x, ldx, n, h, w, c, p, q, (T*)y,
+                                         ldy, idx));
+  else
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(grid_for((long)n * p * q * c / VE<T>)), dim3(256),
+                                         0, (hipStream_t)stream, (const T*)x, ldx, n, h, w, c, k, s, p, q, (T*)y, ldy,
+                                         idx));
   US_LAUNCH_CHECK("maxpool_fwd");
   return 0;
 }
@@ -1565,9 +1702,16 @@ UNETSEG_API int unetseg_maxpool_bwd(int dtype, const void* dy, int ldy, const ui
                                     void* stream) {
   CHECK_VEC(dtype, c, "maxpool_bwd");
   US_CHECK_ARG(dy && idx && dx && k >= 1 && s >= 1 && n >= 0 && h >= 0 && w >= 0, "maxpool_bwd: bad args");
-  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for((long)n * h * w * c / VE<T>)), dim3(256),
-                                       0, (hipStream_t)stream, (const T*)dy, ldy, idx, n, h, w, c, k, s, p, q, (T*)dx,
-                                       ldx, accumulate));
+  if (k == 3 && s == 2 && (long)n * h * w * c < (1L << 31) && (long)n * h * w * ldx < (1L << 31) &&
+      (long)n * p * q * ldy < (1L << 31) && !getenv("UNETSEG_MAXPOOL_GENERIC"))
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_k3s2_kernel<T>,
+                                         dim3(grid_for((long)n * ((h + 1) / 2) * ((w + 1) / 2) * c / VE<T>)), dim3(256),
+                                         0, (hipStream_t)stream, (const T*)dy, ldy, idx, n, h, w, c, p, q, (T*)dx, ldx,
+                                         accumulate));
+  else
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for((long)n * h * w * c / VE<T>)), dim3(256),
+                                         0, (hipStream_t)stream, (const T*)dy, ldy, idx, n, h, w, c, k, s, p, q, (T*)dx,
+                                         ldx, accumulate));
   US_LAUNCH_CHECK("maxpool_bwd");
   return 0;
 }
