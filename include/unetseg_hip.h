@@ -156,7 +156,9 @@ int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1, const void
 int unetseg_pack_input_stem(const float* x, int n, int c, int h, int w, void* xp, void* stream);
 int unetseg_stem_pack_weight(const float* w, int K, int C, void* wk, void* stream);
 int unetseg_stem_fwd_tile_m(int n, int h, int w, int K);
-/* TN configuration of unetseg_stem_fwd (-1: unsupported) and split-K slabs of unetseg_stem_wgrad */
+/* configuration of unetseg_stem_fwd (30 = the persistent-halo stem kernel: 64 output channels, even
+   input sizes whose output tiles into 16 x 32 pixels; else a TN code, -1: unsupported) and split-K
+   slabs of unetseg_stem_wgrad */
 int unetseg_stem_config(int n, int h, int w, int K, int* splits_out);
 int unetseg_stem_fwd(const void* xp, int n, int h, int w, const void* wk, int K, void* y, int ldy, float* stats,
                      void* stream);

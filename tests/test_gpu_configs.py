@@ -489,15 +489,20 @@ def _bnrelu_in_case(cid, direction, shape, op, wk, lib, st):
     assert torch.equal(dw, dw2), f"{cid}: fused wgrad differs from the wgrad of the stored activation"
 
 
-@pytest.mark.parametrize("N,H", [(16, 512), (2, 200)])
-def test_stem_bench_size(N, H):
+@pytest.mark.parametrize("N,H,tn,expect", [(16, 512, False, "stem_halo"), (16, 512, True, "tn128x64"),
+                                           (2, 200, False, "tn128x64"), (3, 256, False, "stem_halo")])
+def test_stem_bench_size(N, H, tn, expect, monkeypatch):
     """ResNet stem at the benchmark size (model/resnet_backbone.py:126-131): 7x7/s2/p3 3->64 on the
-    width-packed fast kernels (stem_fwd: TN 128x64 tile; stem_wgrad: 64x256 split-K ring + reduce)."""
+    width-packed fast kernels (stem_fwd: the persistent-halo stem kernel when the output tiles into
+    16 x 32 pixels, else -- or with UNETSEG_STEM_TN=1 -- the TN 128x64 tile; stem_wgrad: 64x256 split-K
+    ring + reduce); y and the BN statistics' inputs against float64."""
     from unetseg_hip import ops
     from unetseg_hip.lib import DT_BF16, stem_config
     from unetseg_hip.nn import Conv2d
+    if tn:
+        monkeypatch.setenv("UNETSEG_STEM_TN", "1")
     cfg, splits = stem_config(N, H, H, 64)
-    assert cfg == "tn128x64" and splits >= 16, (cfg, splits)
+    assert cfg == expect and splits >= 16, (cfg, splits)
     g = torch.Generator(device=DEV).manual_seed(N + H)
     conv = Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(DEV)
     with torch.no_grad():
@@ -509,6 +514,17 @@ def test_stem_bench_size(N, H):
     xr = _bf(x).double()
     ref = _ref_fwd(xr, conv.weight.detach().double(), 2, 3)
     _check_bf16(_nchw(y.data), ref, "stem y")
+    # the BN partials (sum, M2 about the tile mean per row tile) merge to the stored output's statistics
+    M = y.data.shape[0] * y.data.shape[1] * y.data.shape[2]
+    G = stt.shape[0]
+    st_ = stt.double()
+    cnt = torch.tensor([min(tile, M - g_ * tile) for g_ in range(G)], dtype=torch.float64, device=DEV)
+    tot = st_[:, 0].sum(0)
+    mean = tot / M
+    m2 = (st_[:, 1] + cnt[:, None] * (st_[:, 0] / cnt[:, None] - mean) ** 2).sum(0)
+    o = y.data.reshape(M, -1).double().t()
+    torch.testing.assert_close(tot, o.sum(1), rtol=1e-4, atol=1e-4 * o.abs().sum(1).max().item() / M * 10)
+    torch.testing.assert_close(m2 / M, o.var(1, unbiased=False), rtol=1e-4, atol=1e-6)
     dy = _bf(torch.randn(ref.shape, generator=g, device=DEV))
     y.grad = _nhwc(dy)
     ctx.backward()
@@ -559,6 +575,6 @@ def test_bench_configs_covered(model_name, batch):
     torch.cuda.empty_cache()
     assert np.isfinite(loss.item())
     used.discard(None)
-    stem = {"stem_fwd:tn128x64", "stem_wgrad:wgrad_ring64x256"}  # test_stem_bench_size
+    stem = {"stem_fwd:tn128x64", "stem_fwd:stem_halo", "stem_wgrad:wgrad_ring64x256"}  # test_stem_bench_size
     missing = sorted(used - covered_keys() - stem)
     assert not missing, f"{model_name} B={batch}: configurations without a parity case: {missing}"

@@ -1513,6 +1513,7 @@ static bool stem_fast_args(const IgemmArgs& a, FastTNArgs& f) {
 }
 
 UNETSEG_API int unetseg_stem_fwd_tile_m(int n, int h, int w, int K) {
+  if (stem_halo_ok(n, h, w, K, K)) return stem_halo_tile_m();  // 16 x 32-pixel tiles, all full
   IgemmArgs a = stem_args(nullptr, n, h, w, nullptr, K);
   FastTNArgs f;
   if (!stem_fast_args(a, f)) return -1;
@@ -1529,6 +1530,7 @@ UNETSEG_API int unetseg_stem_config(int n, int h, int w, int K, int* splits_out)
     FastWgradArgs g = stem_wgrad_args(kSomePtr, n, h, w, kSomePtr, K, K);
     *splits_out = wgrad_fast_splits(K, g.Ng, g.Kpix);
   }
+  if (stem_halo_ok(n, h, w, K, K)) return kCfgStemHalo;
   if (!stem_fast_args(a, f)) return -1;
   return tn_fast_config(f, nullptr);
 }
@@ -1536,6 +1538,11 @@ UNETSEG_API int unetseg_stem_config(int n, int h, int w, int K, int* splits_out)
 UNETSEG_API int unetseg_stem_fwd(const void* xp, int n, int h, int w, const void* wk, int K, void* y, int ldy,
                                  float* stats, void* stream) {
   US_CHECK_ARG(xp && wk && y && K % 8 == 0 && ldy >= K, "stem_fwd: bad args");
+  if (stem_halo_ok(n, h, w, K, ldy) && stats) {
+    launch_stem_halo(xp, n, h, w, wk, y, ldy, stats, (hipStream_t)stream);
+    US_LAUNCH_CHECK("stem_fwd");
+    return 0;
+  }
   IgemmArgs a = stem_args(xp, n, h, w, wk, K);
   a.y = y; a.ldy = ldy; a.accumulate = 0; a.bias = nullptr; a.relu = 0; a.stats = stats;
   FastTNArgs f;

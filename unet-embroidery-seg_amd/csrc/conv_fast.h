@@ -108,7 +108,7 @@ struct HaloWgradArgs {
 // 1..14: TN tile configurations of tn_config (conv_fast.hip); 17 / 18: stride-2 dgrad parity classes
 // merged into one launch on 128x128 / 64x128 register-staged tiles (launch_tn_multi); 19 / 20: short K
 // (2-4 steps) on one LDS stage, 128x128 / 128x64
-enum { kCfgHalo = 0, kCfgMulti128 = 17, kCfgMulti64 = 18, kCfgGeneric = 100 };
+enum { kCfgHalo = 0, kCfgMulti128 = 17, kCfgMulti64 = 18, kCfgStemHalo = 30, kCfgGeneric = 100 };
 enum { kWgHalo = 0, kWgFastRow64x256 = 1, kWgFastRow128 = 2, kWgFast64x256 = 3, kWgFast128 = 4, kWgGeneric = 5,
        kWgRing64x256 = 6, kWgRing128 = 7 };
 
@@ -126,6 +126,13 @@ int halo3_blocks(const FastTNArgs& a);
 bool halo3_ok(const FastTNArgs& a);
 int launch_halo3(const FastTNArgs& a, hipStream_t st);
 int halo_tile_m();
+// the ResNet stem forward on the persistent-halo kernel (conv_halo.hip): eligibility, BN-stat tiles
+// (stats [tiles][2][64], stem_halo_tile_m() pixels each) and launch
+bool stem_halo_ok(int n, int h, int w, int K, int ldy);
+int stem_halo_tiles(int n, int h, int w);
+int stem_halo_tile_m();
+int launch_stem_halo(const void* xp, int n, int h, int w, const void* wk, void* y, int ldy, float* stats,
+                     hipStream_t st);
 bool halo3_wgrad_ok(const HaloWgradArgs& a);
 int halo3_wgrad_splits(const HaloWgradArgs& a);
 int launch_halo3_wgrad(const HaloWgradArgs& a, int G_per, hipStream_t st);

@@ -446,6 +446,239 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
 
 
 // ------------------------------------------------------------------------------------------
+// The ResNet stem forward (model/resnet_backbone.py:126-131: 7x7 / stride 2 / pad 3, 3 -> 64) on the
+// same persistent-halo plan.  The input is the width-packed xp bf16 [N][H][W+8][8] (conv.hip: image
+// column w at packed column w+3, channels 3..7 and the 3+5 border columns zero), so filter row fr of
+// output (p, q) is the 8 consecutive packed pixels 2q .. 2q+7 of input row 2p+fr-3: one 64-wide K
+// chunk (8 taps x 8 channels, tap 7 has zero weight).  The TN stem gathered those 128 B per output
+// pixel and filter row from L2 (7 x 128 B per pixel, 14x the input) and re-read its 57 KB of weights
+// per 128-pixel tile; here a block keeps the weights (7 x 64 x 64 bf16) in LDS and streams one
+// (2*TH+5) x 70 packed-pixel patch per TH x 32 output tile (TH = 16: 40.5 KB; each input pixel is
+// fetched ~1.3 times instead of 14).  MFMA roles as in halo3_kernel: weights = A (16 output channels per MFMA row
+// block), pixels = B (lane j16 + 16 kg reads packed pixel 2*col + 4*kk + kg of its patch row).
+// Epilogue: the BN partial statistics of each tile (sum, M2 about the tile mean) -> stats[tile][2][64].
+// ------------------------------------------------------------------------------------------
+constexpr int kStemTH = 16;                  // output rows per tile (two per wave: each weight
+                                             // fragment read from LDS feeds 4 pixel groups)
+constexpr int kStemPR = 2 * kStemTH + 5;     // patch rows
+constexpr int kStemPC = 2 * HW_TW + 6;       // patch columns (packed pixels)
+// A patch row is stored even packed columns first, then odd ones: the 16 lanes of a pixel fragment
+// read columns 2*col + ch (col = 16 consecutive pixels), i.e. 16 consecutive LDS units -- with the
+// natural order they were 32 B apart and lanes j16 and j16 + 8 hit the same banks.
+__device__ __forceinline__ int stem_pos(int hc) { return (hc & 1) ? kStemPC / 2 + (hc >> 1) : hc >> 1; }
+__device__ __forceinline__ int stem_col(int pos) { return pos < kStemPC / 2 ? 2 * pos : 2 * (pos - kStemPC / 2) + 1; }
+
+template <int NW, int NST>
+__global__ __launch_bounds__(64 * NW) void stem_halo_kernel(const bf16* xp, unsigned x_bytes, const bf16* wk, int H,
+                                                            int Wp, int P, int Q, int n_sp, bf16* y, int ldy,
+                                                            unsigned y_bytes, float* stats) {
+  constexpr int TH = kStemTH;
+  constexpr int RPW = TH / NW;
+  constexpr int FP = RPW * (HW_TW / 16);
+  constexpr int FC = 4;
+  constexpr int HP = kStemPR * kStemPC;            // 16-B units (packed pixels) per patch
+  constexpr int HI = (HP + 64 * NW - 1) / (64 * NW);
+  constexpr int HPP = HI * 64 * NW;                // a stage padded to whole DMA instructions: every
+                                                   // wave issues exactly HI per patch (exact vmcnt)
+  constexpr int ST_PER_TILE = FP * FC + 2;         // stores per wave and tile (outputs + 2 stats)
+  constexpr int WCH = 7 * 64 * 8;                  // 16-B chunks of resident weights
+  constexpr int WI = WCH / (64 * NW);
+  static_assert(TH % NW == 0 && WCH % (64 * NW) == 0, "tile shape");
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];
+  uint4* wl = lds;                  // [7*64 rows][8 chunks]
+  uint4* hl = lds + WCH;            // [NST][HPP]
+  float* red = reinterpret_cast<float*>(hl + NST * HPP);  // [NW][64]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int slot = blockIdx.x, G_per = gridDim.x;
+  const int my_tiles = slot < n_sp ? (n_sp - slot + G_per - 1) / G_per : 0;
+  const int tiles_w = Q / HW_TW, tiles_h = P / TH;
+  const __amdgpu_buffer_rsrc_t rx = srd(xp, x_bytes);
+  const __amdgpu_buffer_rsrc_t rw = srd(wk, 64u * 7u * 128u);
+  const __amdgpu_buffer_rsrc_t ry = srd(y, y_bytes);
+  const __amdgpu_buffer_rsrc_t rs = srd(stats, (unsigned)n_sp * 128u * 4u);
+
+  // resident weights: LDS row (fr, k) = wk[k][fr][0..63]
+  {
+    const unsigned base = lds_addr(wl);
+#pragma unroll 2
+    for (int i = 0; i < WI; ++i) {
+      const int inst = i * NW + wid;
+      const int idx = inst * 64 + lane;
+      const int row = idx >> 3, pc = idx & 7;
+      const int fr = row >> 6, k = row & 63;
+      dma16(rw, base + (unsigned)inst * 1024u, (unsigned)(k * 7 + fr) * 128u + (unsigned)swz8(row, pc) * 16u);
+    }
+  }
+  // patch geometry of this lane's DMA slots: offset from the patch origin and whether the unit lies in
+  // the 3 rows above or the 2 rows below the image (only those can leave it; columns never do)
+  unsigned hoff[HI], hflag[HI];
+#pragma unroll
+  for (int i = 0; i < HI; ++i) {
+    const int idx = (i * NW + wid) * 64 + lane;
+    const int hr = idx / kStemPC, hc = stem_col(idx - hr * kStemPC);  // LDS position -> packed column
+    hoff[i] = (unsigned)(hr * Wp + hc) * 16u;
+    hflag[i] = idx >= HP ? 16u : (hr < 3 ? 1u : 0u) | (hr >= 2 * TH + 3 ? 2u : 0u);
+  }
+  auto issue_patch = [&](int t, int stage) {
+    const int sp = slot + t * G_per;
+    const int tw = sp % tiles_w, rest = sp / tiles_w;
+    const int th = rest % tiles_h, nb = rest / tiles_h;
+    const int h0 = th * TH, w0 = tw * HW_TW;
+    const unsigned base = __builtin_amdgcn_readfirstlane(lds_addr(hl + stage * HPP));
+    // origin row 2*h0 - 3 wraps below zero on the first tile row; those lanes are killed
+    const unsigned hb = __builtin_amdgcn_readfirstlane((unsigned)((nb * H + 2 * h0 - 3) * Wp + 2 * w0) * 16u);
+    const unsigned kill = __builtin_amdgcn_readfirstlane(16u | (h0 == 0 ? 1u : 0u) | (h0 + TH >= P ? 2u : 0u));
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const unsigned off = (hflag[i] & kill) ? kOOB : hb + hoff[i];  // padding units: zeros
+      dma16(rx, base + (unsigned)((i * NW + wid) * 1024), off);
+    }
+  };
+
+  f32x4 acc[FC][FP];
+  // NST-stage patch ring: patches 0 .. NST-2 in flight before the first tile, patch t + NST - 1 issued
+  // as tile t starts (a tile's MFMA work is ~0.8 us, far below the DMA latency under load)
+#pragma unroll
+  for (int q = 0; q < NST - 1; ++q)
+    if (q < my_tiles) issue_patch(q, q);
+  if (my_tiles >= NST - 1)  // weights and patch 0 landed (patches 1 .. NST-2 may still fly)
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((NST - 2) * HI) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  const int j16 = lane & 15, kg = lane >> 4;
+
+  for (int t = 0; t < my_tiles; ++t) {
+    const int stage = t % NST;
+    if (t + NST - 1 < my_tiles) issue_patch(t + NST - 1, (t + NST - 1) % NST);
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int p = 0; p < FP; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint4* hs = hl + stage * HPP;
+#pragma unroll
+    for (int fr = 0; fr < 7; ++fr) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ch = kk * 4 + kg;
+        bf16x8 wf[FC], pf[FP];
+#pragma unroll
+        for (int c = 0; c < FC; ++c) {
+          const int row = fr * 64 + c * 16 + j16;
+          uint4 v = wl[row * 8 + swz8(row, ch)];
+          wf[c] = *reinterpret_cast<bf16x8*>(&v);
+        }
+#pragma unroll
+        for (int p = 0; p < FP; ++p) {
+          const int r = wid * RPW + p / (HW_TW / 16);
+          const int col = (p % (HW_TW / 16)) * 16 + j16;
+          uint4 v = hs[(2 * r + fr) * kStemPC + stem_pos(2 * col + ch)];
+          pf[p] = *reinterpret_cast<bf16x8*>(&v);
+        }
+#pragma unroll
+        for (int c = 0; c < FC; ++c)
+#pragma unroll
+          for (int p = 0; p < FP; ++p)
+            acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], pf[p], acc[c][p], 0, 0, 0);
+      }
+    }
+
+    // epilogue: round to bf16, BN partials of the rounded values, stores last
+    const int sp = slot + t * G_per;
+    const int tw = sp % tiles_w, rest = sp / tiles_w;
+    const int th = rest % tiles_h, nb = rest / tiles_h;
+    float csum[FC][4];
+    uint2 outv[FC][FP];
+    unsigned outo[FP];
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) csum[c][e] = 0.f;
+#pragma unroll
+    for (int p = 0; p < FP; ++p) {
+      const int r = wid * RPW + p / (HW_TW / 16);
+      const int col = (p % (HW_TW / 16)) * 16 + j16;
+      const long opix = ((long)nb * P + th * TH + r) * Q + tw * HW_TW + col;
+      outo[p] = (unsigned)(opix * ldy) * 2u;
+#pragma unroll
+      for (int c = 0; c < FC; ++c) {
+        bf16 o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = (bf16)acc[c][p][e];
+          const float v = (float)o[e];
+          acc[c][p][e] = v;
+          csum[c][e] += v;
+        }
+        outv[c][p] = *reinterpret_cast<uint2*>(o);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float s = row16_sum(csum[c][e]);
+        if (j16 == 0) red[wid * 64 + c * 16 + kg * 4 + e] = s;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float qv[FC][4];
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int col = c * 16 + kg * 4 + e;
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) tot += red[w * 64 + col];
+        const float mean = tot * (1.0f / (TH * HW_TW));
+        float q = 0.f;
+#pragma unroll
+        for (int p = 0; p < FP; ++p) {
+          const float d = acc[c][p][e] - mean;
+          q += d * d;
+        }
+        qv[c][e] = row16_sum(q);
+      }
+    float stot = 0.f;
+    if (tid < 64)
+#pragma unroll
+      for (int w = 0; w < NW; ++w) stot += red[w * 64 + tid];
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (j16 == 0) red[wid * 64 + c * 16 + kg * 4 + e] = qv[c][e];
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    {
+      float q = 0.f;
+      if (tid < 64)
+#pragma unroll
+        for (int w = 0; w < NW; ++w) q += red[w * 64 + tid];
+      // every wave issues both stats stores (only wave 0's lanes land): exact per-wave counts
+      const unsigned so = tid < 64 ? (unsigned)(sp * 128 + tid) * 4u : kOOB;
+      bstore32(rs, so, stot);
+      bstore32(rs, tid < 64 ? so + 256u : kOOB, q);
+    }
+#pragma unroll
+    for (int p = 0; p < FP; ++p)
+#pragma unroll
+      for (int c = 0; c < FC; ++c) bstore64(ry, outo[p] + (c * 16 + kg * 4) * 2, outv[c][p]);
+    // patch t + 1 landed and every wave is done with the current stage and `red`.  In the steady
+    // state (patch t + 1 issued inside the loop, patches t + 2 .. t + NST - 1 issued) exactly
+    // (NST - 2) patches and (NST - 1) tiles' stores were issued after it; near either end, wait for
+    // all but this tile's stores (conservative)
+    if (t >= NST - 2 && t + NST - 1 < my_tiles)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((NST - 2) * HI + (NST - 1) * ST_PER_TILE)
+                   : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(ST_PER_TILE) : "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ------------------------------------------------------------------------------------------
 // wgrad of the same convolutions: dW[k][tap][c] = sum_pix dY[pix][k] * X[pix + off(tap)][c].
 // Block group = (64 output channels, 64 input channels); persistent over TH x 32 spatial tiles,
 // each tile = dY tile (256 px x 64 ch) + X halo (340 px x 64 ch) by LDS-DMA, double buffered.
@@ -1153,6 +1386,39 @@ int launch_halo3(const FastTNArgs& a, hipStream_t st) {
       default: break;
     }
   return launch_halo3_cfg<8, 8, 0, kEpiDyn>(a, st);
+}
+
+// the stem forward on stem_halo_kernel: 64 output channels, even input sizes with P % 16 == 0 and
+// Q % 32 == 0 (UNETSEG_STEM_TN=1: the TN stem)
+bool stem_halo_ok(int n, int h, int w, int K, int ldy) {
+  if (getenv("UNETSEG_STEM_TN")) return false;
+  if (K != 64 || ldy < 64 || ldy % 4 || n <= 0 || h % 2 || w % 2) return false;
+  const int P = h / 2, Q = w / 2;
+  if (P % kStemTH || Q % HW_TW) return false;
+  return (long)n * h * (w + 8) * 16 < (1L << 31) && (long)n * P * Q * ldy * 2 < (1L << 31);
+}
+
+int stem_halo_tiles(int n, int h, int w) { return n * (h / 2 / kStemTH) * (w / 2 / HW_TW); }
+int stem_halo_tile_m() { return kStemTH * HW_TW; }
+
+int launch_stem_halo(const void* xp, int n, int h, int w, const void* wk, void* y, int ldy, float* stats,
+                     hipStream_t st) {
+  constexpr int NW = 8, NST = 2;
+  const int P = h / 2, Q = w / 2, Wp = w + 8;
+  const int n_sp = stem_halo_tiles(n, h, w);
+  const int blocks = n_sp < 256 ? n_sp : 256;
+  constexpr int HPP = (kStemPR * kStemPC + 64 * NW - 1) / (64 * NW) * (64 * NW);
+  const size_t lds = (size_t)7 * 64 * 128 + (size_t)NST * HPP * 16 + NW * 64 * 4;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_halo_kernel<NW, NST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((stem_halo_kernel<NW, NST>), dim3(blocks), dim3(64 * NW), lds, st, (const bf16*)xp,
+                     (unsigned)((long)n * h * Wp * 16), (const bf16*)wk, h, Wp, P, Q, n_sp, (bf16*)y, ldy,
+                     (unsigned)((long)n * P * Q * ldy * 2), stats);
+  return 0;
 }
 
 bool halo3_wgrad_ok(const HaloWgradArgs& a) {
