@@ -10,10 +10,16 @@ FusedAdam(overlap=True)); every parameter is updated inside each timed step.  Ra
 `roofline` covers the dominant kernel (igemm_tn: conv fwd + dgrad), measured with HIP events around
 each of its launches in one probe step right after the timed region.  `cpu_baseline` times the CPU
 oracle (oracle/ref_cpu.py, fp32, the reference's op sequence) on the host on a bounded sample.
+`configs` times BASELINE.json's other GPU configurations the same way in the same process (C4
+attention_unet B=8 at N=1, C5 multitask_unet B=8 BCE + CE at every N); `card` records the GPU's
+clocks / power in the middle of the timed region and its own bf16 GEMM and HBM copy rates, so a slow
+box can be told from a code change.  `median_gpu_ms_per_step` is the median of per-step HIP-event
+times over the K timed steps.
 """
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -50,6 +56,9 @@ def parse():
     ap.add_argument("--overlap-adam", type=int, default=1,
                     help="Adam + weight re-pack per gradient bucket on the weight-gradient stream during backward")
     ap.add_argument("--bucket-mb", type=float, default=8.0, help="gradient bucket size (MB)")
+    ap.add_argument("--extra-configs", type=int, default=1,
+                    help="also time C4 (attention_unet B=8, N=1 only) and C5 (multitask_unet B=8) after the headline")
+    ap.add_argument("--card-probe", type=int, default=1, help="bf16 GEMM + HBM copy rate of this card (rank 0)")
     return ap.parse_args()
 
 
@@ -158,44 +167,95 @@ def pmc_mfma(workload, kind):
     return best
 
 
-def main():
-    args = parse()
-    from unetseg_hip.ddp import GradBuckets, init_from_env, local_device
+def _pci_dir(dev):
+    """sysfs directory of this process's GPU (matched by PCI bus id), or None"""
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = "%04x:%02x:%02x.0" % (getattr(p, "pci_domain_id", 0), p.pci_bus_id, p.pci_device_id)
+        d = os.path.join("/sys/bus/pci/devices", bdf)
+        return d if os.path.isdir(d) else None
+    except Exception:  # noqa: BLE001 - best effort
+        return None
 
-    rank, world, local = init_from_env("nccl")
-    if world != args.gpus:
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    dev = torch.device("cuda", local_device(local))
-    torch.cuda.set_device(dev)
-    torch.manual_seed(11)
-    if args.stream:
-        # the legacy default stream synchronises implicitly with other streams, which makes the
-        # compute stream's final join with the weight-gradient stream slow; work on a created one
-        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=args.priority))
+
+def card_state(dev):
+    """current shader / memory clock (the '*' level of pp_dpm_sclk / pp_dpm_mclk), power and edge
+    temperature from sysfs, as readable by an ordinary user; None fields when not exposed"""
+    out = {"sclk_mhz": None, "mclk_mhz": None, "power_w": None, "temp_c": None}
+    d = _pci_dir(dev)
+    if d is None:
+        return out
+    for key, f in (("sclk_mhz", "pp_dpm_sclk"), ("mclk_mhz", "pp_dpm_mclk")):
+        try:
+            for line in open(os.path.join(d, f)):
+                if line.rstrip().endswith("*"):
+                    out[key] = int("".join(ch for ch in line.split(":")[1] if ch.isdigit()))
+        except (OSError, ValueError, IndexError):
+            pass
+    try:
+        import glob
+        for hw in glob.glob(os.path.join(d, "hwmon", "hwmon*")):
+            for key, f, scale in (("power_w", "power1_average", 1e-6), ("power_w", "power1_input", 1e-6),
+                                  ("temp_c", "temp1_input", 1e-3)):
+                fp = os.path.join(hw, f)
+                if out[key] is None and os.path.exists(fp):
+                    out[key] = round(int(open(fp).read().strip()) * scale, 1)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def card_probe(dev):
+    """the card's own speed, to tell a slow box from a code change: a bf16 GEMM (hipBLASLt, 8192^3)
+    and a 2 GiB device copy, each timed with HIP events on the current stream"""
+    a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    b = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    src = torch.empty(1 << 30, dtype=torch.int16, device=dev).fill_(1)
+    dst = torch.empty_like(src)
+    res = {}
+    for name, fn, work in (("gemm_bf16_tflops", lambda: torch.mm(a, b), 2 * 8192 ** 3 / 1e12),
+                           ("hbm_copy_gbs", lambda: dst.copy_(src), 2 * src.numel() * 2 / 1e9)):
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        res[name] = round(work * 10 / (e0.elapsed_time(e1) * 1e-3), 1)
+    del a, b, src, dst
+    torch.cuda.empty_cache()
+    return res
+
+
+def build_step(model_name, batch, size, loss_name, dev, rank, world, args):
+    """(model, step fn) of one configuration: synthetic batches resident in HBM, fused Adam with the
+    per-bucket overlapped update, the RCCL bucket all-reduce when world > 1"""
+    import contextlib
 
     from model.model_factory import create_model
-    from unetseg_hip import ops
     from unetseg_hip.arena import FusedAdam
+    from unetseg_hip.ddp import GradBuckets
     from unetseg_hip.losses import binary_segmentation_loss, multitask_loss
     from utils.synthetic import make_batch
 
-    kw = dict(num_classes=1) if args.model == "multitask_unet" else dict(num_classes=2)
-    import contextlib
-
+    torch.manual_seed(11)
+    kw = dict(num_classes=1) if model_name == "multitask_unet" else dict(num_classes=2)
     with contextlib.redirect_stdout(sys.stderr):  # weights_init's banner (reference behaviour) -> stderr
-        model = create_model(args.model, weights="", **kw).to(dev).train()
+        model = create_model(model_name, weights="", **kw).to(dev).train()
     model.compute_dtype = "bf16"
-    buckets = GradBuckets(model, bucket_mb=args.bucket_mb) if world > 1 else None
+    if world > 1:
+        GradBuckets(model, bucket_mb=args.bucket_mb)
     use_graph = bool(args.graph) and world == 1  # N>1: RCCL collectives stay eager
     overlap = bool(args.overlap_adam) and not use_graph
     opt = FusedAdam(model, lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4, capturable=use_graph, overlap=overlap,
                     bucket_mb=args.bucket_mb)
     nbatches = 2
-    multitask = args.model == "multitask_unet"
+    multitask = model_name == "multitask_unet"
     data = []
     for i in range(nbatches):
-        x, y, c = make_batch(args.batch, args.size, seed=1234 + 100000 * rank + i, with_cls=True)
+        x, y, c = make_batch(batch, size, seed=1234 + 100000 * rank + i, with_cls=True)
         data.append((x.to(dev), y.to(dev), c.to(dev)))
 
     def step(i):
@@ -204,9 +264,9 @@ def main():
         with torch.autocast("cuda", dtype=torch.bfloat16):
             if multitask:  # seg BCE/Lovasz + 1.0 * CE (train.py:213-219 defaults)
                 seg, cls = model(x)
-                loss = multitask_loss(seg, cls, y, c, 1.0, args.loss)[0]
+                loss = multitask_loss(seg, cls, y, c, 1.0, loss_name)[0]
             else:
-                loss = binary_segmentation_loss(model(x), y, args.loss)
+                loss = binary_segmentation_loss(model(x), y, loss_name)
         loss.backward()
         opt.step()
         return loss
@@ -233,33 +293,76 @@ def main():
             gr, li = graphs[i % nbatches]
             gr.replay()
             return li
+    return model, step, run, use_graph, overlap
 
-    for i in range(args.warmup):
+
+def timed(run, steps, warmup, world, dev, sample=None):
+    """W untimed steps, then K steps between barrier + synchronize; the wall time is the max over
+    ranks.  HIP events between consecutive steps (compute stream: each step ends with the join of
+    the weight-gradient stream) give the per-step GPU times for the median."""
+    for i in range(warmup):
         run(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     t0 = time.perf_counter()
-    ev0.record()
-    for i in range(args.steps):
+    evs[0].record()
+    loss = None
+    card = None
+    for i in range(steps):
         loss = run(i)
-    ev1.record()
+        evs[i + 1].record()
+        if i == steps // 2 and sample is not None:
+            card = sample()  # the host runs ahead of the GPU: this reads the clocks under load
+    if sample is not None and card is None:
+        card = sample()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    gpu_ms = ev0.elapsed_time(ev1)
+    per = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(steps))
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall = float(t.item())
+    return float(t.item()), per[len(per) // 2], evs[0].elapsed_time(evs[-1]), loss, card
+
+
+#: the other GPU configurations of BASELINE.json, timed in the same process after the headline line
+#: (C4 is a one-GPU configuration; C5 is data-parallel, so it runs at every N)
+EXTRA = (("c4_attention_unet_b8", "attention_unet", 8, "lovasz_hinge", False),
+         ("c5_multitask_unet_b8", "multitask_unet", 8, "bce", True))
+
+
+def main():
+    args = parse()
+    from unetseg_hip.ddp import init_from_env, local_device
+
+    rank, world, local = init_from_env("nccl")
+    if world != args.gpus:
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    dev = torch.device("cuda", local_device(local))
+    torch.cuda.set_device(dev)
+    torch.manual_seed(11)
+    if args.stream:
+        # the legacy default stream synchronises implicitly with other streams, which makes the
+        # compute stream's final join with the weight-gradient stream slow; work on a created one
+        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=args.priority))
+
+    from unetseg_hip import ops
+
+    model, step, run, use_graph, overlap = build_step(args.model, args.batch, args.size, args.loss, dev, rank, world,
+                                                      args)
+    wall, median_ms, gpu_ms, loss, card_mid = timed(run, args.steps, args.warmup, world, dev,
+                                                    sample=lambda: card_state(dev))
     ms_per_step = 1000.0 * wall / args.steps
     imgs_per_s = args.batch * world * args.steps / wall
     final_loss = float(loss.item())
 
+    multitask = args.model == "multitask_unet"
     task = "seg+cls multitask" if multitask else "binary seg"
     workload = f"{args.model} {task} {args.size}x{args.size}, per-GPU batch {args.batch}, {args.loss} + Adam"
     roof = None
@@ -302,6 +405,32 @@ def main():
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         in_sync = bool(float(hi.item()) == float(lo.item()))
+    del model, step, run
+    gc.collect()  # the model and its gradient buckets reference each other
+    torch.cuda.empty_cache()
+
+    configs = {}
+    if args.extra_configs:
+        for tag, name, batch, loss_name, dp in EXTRA:
+            if world > 1 and not dp:
+                continue
+            m2, _, run2, _, _ = build_step(name, batch, args.size, loss_name, dev, rank, world, args)
+            w2, med2, _, _, _ = timed(run2, args.steps, args.warmup, world, dev)
+            ips = batch * world * args.steps / w2
+            configs[tag] = {"workload": f"{name} {args.size}x{args.size}, per-GPU batch {batch}, "
+                                        f"{loss_name}{' + ce' if name == 'multitask_unet' else ''} + Adam",
+                            "value": round(ips, 2), "unit": "images/s", "ms_per_step": round(1000.0 * w2 / args.steps, 3),
+                            "median_gpu_ms_per_step": round(med2, 3),
+                            "step_mfma_frac": round(ips / world * GFLOP_PER_IMG[name] / 1e3 / PEAK_BF16_TFLOPS, 4)}
+            del m2, run2
+            gc.collect()
+            torch.cuda.empty_cache()
+
+    card = None
+    if rank == 0:
+        card = {"during": card_mid, "device": torch.cuda.get_device_name(dev)}
+        if args.card_probe:
+            card.update(card_probe(dev))
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
@@ -319,8 +448,10 @@ def main():
             "roofline": roof, "cpu_baseline": cpu,
             "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
             "step_tflops_per_gpu": round(step_tflops, 2),
-            "gpu_event_ms_per_step": round(gpu_ms / args.steps, 3), "final_loss": round(final_loss, 5),
+            "gpu_event_ms_per_step": round(gpu_ms / args.steps, 3),
+            "median_gpu_ms_per_step": round(median_ms, 3), "final_loss": round(final_loss, 5),
             "hip_graph": use_graph, "overlap_adam": overlap, "params_in_sync": in_sync,
+            "configs": configs, "card": card,
         }
         print(json.dumps(line))
     if world > 1:

@@ -106,6 +106,7 @@ class ResNet(nn.Module):
 
 def run_resnet(ctx, r, x):
     """resnet_backbone.py:182-201 -> [feat1, ..., feat5] Nodes"""
+    ops.tap_mark(ctx, "stem")
     if ctx.dt == DT_BF16 and ops.STEM_FAST:
         y, st = ops.stem_conv(ctx, x, r.conv1)
     else:
@@ -117,6 +118,7 @@ def run_resnet(ctx, r, x):
     for name, layer in (("layer1", r.layer1), ("layer2", r.layer2), ("layer3", r.layer3), ("layer4", r.layer4)):
         ops.flush_point(ctx, name)
         for i in range(len(layer)):
+            ops.tap_mark(ctx, f"{name}.{i}")
             h = run_bottleneck(ctx, layer[i], h)
         feats.append(h)
     return feats

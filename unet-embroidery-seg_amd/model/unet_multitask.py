@@ -44,10 +44,12 @@ class MultiTaskUNet(HipModel):
         self._pack_weights(ctx, ctx.tape is not None)
         feats = run_resnet(ctx, self.encoder, x)
         self._drop_step += 1
+        ops.tap_mark(ctx, "cls_head")
         cls, cls_holder, _ = ops.cls_head(ctx, feats[4], self.cls_head, self.dropout_mask,
                                           seed=0x5EED0000 + self._drop_step)
         u = run_resnet_decoder(ctx, self, feats, head=self.seg_head)
         seg, seg_holder = ops.pw_head(ctx, u, self.seg_head)
+        ops.tap_mark(ctx, "end")
         ctx.out_holders = [seg_holder, cls_holder]
         return seg, cls
 

@@ -67,15 +67,21 @@ class UNetPlain(HipModel):
 
     def _run(self, ctx, x):
         self._pack_weights(ctx, ctx.tape is not None)
+        ops.tap_mark(ctx, "inc")
         xs = [run_double_conv(ctx, self.inc, ops.pack_input(ctx, x, 8))]
-        for d in (self.down1, self.down2, self.down3, self.down4):
+        for i, d in enumerate((self.down1, self.down2, self.down3, self.down4), start=1):
+            ops.tap_mark(ctx, f"down{i}")
             h = ops.maxpool(ctx, xs[-1], 2, 2, False)
             xs.append(run_double_conv(ctx, d.net[1], h))
         h = xs[4]
-        for up, skip in ((self.up1, xs[3]), (self.up2, xs[2]), (self.up3, xs[1]), (self.up4, xs[0])):
+        for i, (up, skip) in enumerate(((self.up1, xs[3]), (self.up2, xs[2]), (self.up3, xs[1]), (self.up4, xs[0])),
+                                       start=1):
+            ops.tap_mark(ctx, f"up{i}")
             u = ops.upsample2x(ctx, h, align_corners=False)
             u = ops.match_hw(ctx, u, skip, "pad")  # unet_plain.py:42-45 (odd sizes)
             h = run_double_conv(ctx, up.conv, skip, x2=u)
+        ops.tap_mark(ctx, "outc")
         logits, holder = ops.pw_head(ctx, h, self.outc)
+        ops.tap_mark(ctx, "end")
         ctx.out_holders = [holder]
         return logits

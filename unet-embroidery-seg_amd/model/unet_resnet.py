@@ -38,10 +38,11 @@ def run_resnet_decoder(ctx, m, feats, head=None):
     the last conv's epilogue where the shape allows (ops.pw_head then reuses those logits)"""
     f1, f2, f3, f4, f5 = feats
     ops.flush_point(ctx, "decoder")
-    u = run_unet_up(ctx, m.up_concat4, f4, f5)
-    u = run_unet_up(ctx, m.up_concat3, f3, u)
-    u = run_unet_up(ctx, m.up_concat2, f2, u)
-    u = run_unet_up(ctx, m.up_concat1, f1, u)
+    u = f5
+    for name, skip in (("up_concat4", f4), ("up_concat3", f3), ("up_concat2", f2), ("up_concat1", f1)):
+        ops.tap_mark(ctx, name)
+        u = run_unet_up(ctx, getattr(m, name), skip, u)
+    ops.tap_mark(ctx, "up_conv")
     u = ops.upsample2x(ctx, u, align_corners=True)
     u, _ = ops.conv(ctx, u, m.up_conv[1]._pc, relu=True)
     u, _ = ops.conv(ctx, u, m.up_conv[3]._pc, relu=True, head=head)
@@ -72,5 +73,6 @@ class Unet(HipModel):
         feats = run_resnet(ctx, self.resnet, x)
         u = run_resnet_decoder(ctx, self, feats, head=self.final)
         logits, holder = ops.pw_head(ctx, u, self.final)
+        ops.tap_mark(ctx, "end")
         ctx.out_holders = [holder]
         return logits

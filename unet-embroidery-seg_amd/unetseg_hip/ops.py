@@ -79,6 +79,24 @@ _WORKSPACES = {}
 PROBE = None
 
 
+#: test hook (tests/test_gpu_teacher.py): an object with ``op(ctx, kind, out, ins, info)`` and
+#: ``mark(ctx, name)``, told about every op a recording forward runs and about the model's block
+#: boundaries, so a test can rebuild each block's backward in float64 from the tensors this path
+#: stored; None outside that test (no cost)
+TAP = None
+
+
+def _tap(ctx, kind, out, ins, **info):
+    if TAP is not None and ctx.tape is not None:
+        TAP.op(ctx, kind, out, ins, info)
+
+
+def tap_mark(ctx, name):
+    """block boundary (model code): the ops recorded since the previous mark form one block"""
+    if TAP is not None and ctx.tape is not None:
+        TAP.mark(ctx, name)
+
+
 class _probe:
     """HIP events around one op's launches, recorded on the stream the kernels run on."""
 
@@ -320,7 +338,9 @@ def pack_input(ctx, x, cpad=8):
     N, C, H, W = x.shape
     y = ctx.empty(N, H, W, cpad)
     lib.pack_input(ctx.dt, P(x), N, C, H, W, cpad, P(y), ctx.stream)
-    return Node(y, need_grad=False)
+    out = Node(y, need_grad=False)
+    _tap(ctx, "input", out, [], image=x)
+    return out
 
 
 #: narrow 1x1 conv gradients through a 64-channel zero-padded dY (UNETSEG_NO_PADK=1: generic kernels)
@@ -409,6 +429,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
         out.mbits = mbits
     if relu:
         out.fuse = (1, y, None)
+    _tap(ctx, "conv", out, [x1, x2], conv=pc.conv, relu=relu)
 
     def bwd():
         dA = out.grad
@@ -656,6 +677,7 @@ def stem_conv(ctx, x, conv_mod):
     with _probe("igemm_tn", flops, 1, ("stem_fwd",) + desc):
         lib.stem_fwd(P(xp), N, H, W, P(wk), K, P(y), K, P(st[0]), ctx.stream)
     out = Node(y)
+    _tap(ctx, "stem", out, [], conv=conv_mod, image=x)
 
     def bwd():
         dY = out.grad
@@ -760,6 +782,8 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None, lazy=False):
         lib.bn_apply(ctx.dt, P(Y), ldp(Y), P(s1.sc), P(s1.sh), P(R), ldp(R), P(s2.sc if s2 else None),
                      P(s2.sh if s2 else None), mode, int(relu), P(a), C, M, C, ctx.stream)
         out = Node(a)
+    _tap(ctx, "bn", out, [y, res, res_bn[0] if res_bn is not None else None], bn=bnm,
+         bn2=res_bn[2] if res_bn is not None else None, relu=relu, lazy=out.lazy is not None)
     plain_relu = relu and res is None and res_bn is None
     if plain_relu and ctx.training:
         out.fuse = (2, Y, s1)
@@ -869,6 +893,7 @@ def maxpool(ctx, x, k, s, ceil_mode):
     idx = torch.empty((N, Pq, Qq, C), dtype=torch.uint8, device=ctx.device)
     lib.maxpool_fwd(ctx.dt, P(X), ldp(X), N, H, W, C, k, s, int(ceil_mode), P(y), C, P(idx), 0, 0, ctx.stream)
     out = Node(y)
+    _tap(ctx, "maxpool", out, [x], k=k, s=s, ceil_mode=ceil_mode)
 
     def bwd():
         if out.grad is None or not x.need_grad:
@@ -888,6 +913,7 @@ def upsample2x(ctx, x, align_corners):
     y = ctx.empty(N, 2 * H, 2 * W, C)
     lib.upsample2x_fwd(ctx.dt, P(X), ldp(X), N, H, W, C, int(align_corners), P(y), C, ctx.stream)
     out = Node(y)
+    _tap(ctx, "resize", out, [x], size=(2 * H, 2 * W), align_corners=bool(align_corners))
 
     def bwd():
         if out.grad is None or not x.need_grad:
@@ -921,6 +947,7 @@ def resize_bilinear(ctx, x, oh, ow, align_corners):
     y = ctx.empty(N, oh, ow, C)
     lib.resize_bilinear_fwd(ctx.dt, P(X), ldp(X), N, H, W, C, oh, ow, int(align_corners), P(y), C, ctx.stream)
     out = Node(y)
+    _tap(ctx, "resize", out, [x], size=(oh, ow), align_corners=bool(align_corners))
 
     def bwd():
         if out.grad is None or not x.need_grad:
@@ -941,6 +968,7 @@ def pad2d(ctx, x, top, left, oh, ow):
     y = ctx.empty(N, oh, ow, C)
     lib.pad2d_fwd(ctx.dt, P(X), ldp(X), N, H, W, C, top, left, oh, ow, P(y), C, ctx.stream)
     out = Node(y)
+    _tap(ctx, "pad", out, [x], top=top, left=left, size=(oh, ow))
 
     def bwd():
         if out.grad is None or not x.need_grad:
@@ -987,6 +1015,7 @@ def pw_head(ctx, x, conv_mod):
         lib.pw_small_fwd(ctx.dt, P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(conv_mod.bias), P(y), 0,
                          ctx.stream)
     holder = {}
+    _tap(ctx, "head", y, [x], conv=conv_mod, holder=holder)
 
     def bwd():
         dy = holder.get("grad")
@@ -1052,6 +1081,7 @@ def attention_gate(ctx, skip, gate, gm, pth, pph):
     gated = ctx.empty(N, H, W, Cs)
     lib.attn_apply(ctx.dt, P(S_), ldp(S_), P(psi), P(s.sc), P(s.sh), P(alpha), P(gated), Cs, M, Cs, ctx.stream)
     out = Node(gated)
+    _tap(ctx, "attn", out, [f, skip], psi_conv=psi_conv, psi_bn=psi_bn, psi=psi, alpha=alpha)
 
     def bwd():
         dg = out.grad
@@ -1099,6 +1129,7 @@ def cls_head(ctx, feat, head, dropout_mask=None, seed=0):
     y = torch.empty((N, O2), dtype=torch.float32, device=ctx.device)
     lib.linear_fwd(P(h), P(fc2.weight), P(fc2.bias), N, O1, O2, 0, 0.0, 0, 0, 0, 0, P(y), ctx.stream)
     holder = {}
+    _tap(ctx, "cls", y, [feat], fc1=fc1, fc2=fc2, p_drop=p_drop, keep=mask, pre=pre, hidden=h, holder=holder)
 
     def bwd():
         dy = holder.get("grad")
