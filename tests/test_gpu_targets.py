@@ -5,7 +5,8 @@
   [0, K) gives a NaN loss and gradient instead of an out-of-range read;
 * float segmentation targets (MultiTaskLoss passes seg_targets.float(), unet_multitask.py:131) are
   accepted when they are 0/1; a soft label (BCE would take it as given, the kernels take 0/1 labels)
-  turns the seg loss and its gradient into NaN on the device -- no host sync (ADVICE round 2);
+  turns the seg loss and its gradient into NaN on the device -- no host sync -- and
+  is reported as a ValueError by the multitask loops' once-per-epoch read (ADVICE round 3);
 * binary_segmentation_loss reads float targets as (targets == 1), the reference's own mapping
   (utils/train_and_eval.py:163);
 * the multiclass CE / Focal treat a target outside [0, C) other than ignore_index the way
@@ -55,8 +56,31 @@ def test_float_seg_targets():
     _, _, _, sl_f, _ = _mt(ct, t01)
     _, _, _, sl_i, _ = _mt(ct, t01.long())
     torch.testing.assert_close(sl_f, sl_i)
+    from unetseg_hip.losses import raise_if_soft_targets
+    raise_if_soft_targets(DEV)  # 0/1 float targets: nothing flagged
     seg, _, _, sl, cl = _mt(ct, t01 * 0.7)
     assert torch.isnan(sl).item() and torch.isnan(seg.grad).all().item() and torch.isfinite(cl).item()
+    with pytest.raises(ValueError, match="seg targets must be 0 or 1"):
+        raise_if_soft_targets(DEV)
+    raise_if_soft_targets(DEV)  # the flag is cleared by the report
+
+
+def test_soft_seg_target_two_reported_by_loop():
+    """a float target of 2 in the multitask loop raises at the epoch's end instead of
+    leaving a silent NaN loss (model/unet_multitask.py:131 feeds seg_targets.float() to BCE)"""
+    from model.model_factory import build_model
+    from model.unet_multitask import MultiTaskLoss
+    from unetseg_hip.arena import FusedAdam
+    from utils.train_and_eval import train_one_epoch_multitask
+    torch.manual_seed(0)
+    m = build_model("multitask_unet", 1).to(DEV)
+    opt = FusedAdam(m, lr=1e-4)
+    x = torch.rand(2, 3, 64, 64, device=DEV)
+    seg_t = torch.zeros(2, 64, 64, device=DEV)
+    seg_t[:, 10:20, 10:20] = 2.0
+    loader = [(x, seg_t, None, torch.tensor([0, 2], device=DEV))]
+    with pytest.raises(ValueError, match="seg targets must be 0 or 1"):
+        train_one_epoch_multitask(m, opt, loader, torch.device(DEV), MultiTaskLoss(), None, amp=True)
 
 
 def test_binary_loss_float_targets_as_reference():

@@ -63,3 +63,19 @@ def test_train_refuses_cpu_and_real_data():
 
     with pytest.raises((RuntimeError, NotImplementedError)):
         train.train(train.parse_args(["--device", "cpu", "--epochs", "1"]))
+
+
+def test_binary_epoch_empty_loader_returns_zero(capsys):
+    """an empty train loader returns 0 like the reference (utils/train_and_eval.py:
+    185-263 divides by max(seen, 1)) instead of reading the image size of a batch that never came"""
+    import contextlib
+    import io
+
+    import torch
+    from model.model_factory import build_model
+    from utils.train_and_eval import train_one_epoch_binary
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = build_model("unet_plain", 2)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-4)
+    out = train_one_epoch_binary(m, opt, [], torch.device("cpu"), "bce", None, False, None, 0, 1)
+    assert out == 0.0

@@ -2,8 +2,9 @@
 
     python tools/tail_probe.py [--model unet_resnet50] [--batch 16] [--steps 6]
 
-Wraps ops.Ctx.backward to record, per step: c = the compute stream's last backward kernel done,
-s = the weight-gradient stream's last kernel done (both before the join), a = Adam done, and the
+Hooks the end of ops.Ctx.backward (ops.ON_JOIN) to record, per step: c = the compute stream's last
+backward kernel done, s = the weight-gradient stream's last kernel done (held-back weight gradients
+and the last buckets' overlapped Adam included; both before the join), a = opt.step() done, and the
 next step's first forward kernel start f.  Prints the averages of s - c (the side-stream tail the
 join waits for), a - max(c, s) (Adam), f - a (step boundary: zero_grad + host) and the step time.
 """
@@ -27,7 +28,6 @@ def main():
     ap.add_argument("--steps", type=int, default=6)
     a = ap.parse_args()
     from model.model_factory import create_model
-    from unetseg_hip import lib as L
     from unetseg_hip import ops
     from unetseg_hip.arena import FusedAdam
     from unetseg_hip.losses import binary_segmentation_loss
@@ -38,28 +38,20 @@ def main():
     with contextlib.redirect_stdout(io.StringIO()):
         m = create_model(a.model, num_classes=2, weights="").to(dev).train()
     m.compute_dtype = "bf16"
-    opt = FusedAdam(m, lr=1e-4, weight_decay=1e-4)
+    opt = FusedAdam(m, lr=1e-4, weight_decay=1e-4, overlap=True)  # bench.py's optimizer
     x, y = make_batch(a.batch, 512, seed=5)
     x, y = x.to(dev), y.to(dev)
     marks = []
-    orig = ops.Ctx.backward
 
-    def backward(self):
-        tape, self.tape = self.tape, None
-        self.side = ops.side_stream(self.device)
-        L.lib.stream_wait(self.side.cuda_stream, self.stream)
-        while tape:
-            fn = tape.pop()
-            fn()
-            del fn
+    def on_join(ctx):
+        # the real Ctx.backward (tape, held-back weight gradients, last buckets' Adam) has run;
+        # the compute stream joins the side stream right after this
         ec, es = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ec.record(torch.cuda.current_stream(self.device))
-        es.record(self.side)
+        ec.record(torch.cuda.current_stream(ctx.device))
+        es.record(ctx.side if ctx.side is not None else torch.cuda.current_stream(ctx.device))
         marks[-1]["c"], marks[-1]["s"] = ec, es
-        L.lib.stream_wait(self.stream, self.side.cuda_stream)
-        self.side = None
 
-    ops.Ctx.backward = backward
+    ops.ON_JOIN = on_join
     for i in range(a.steps + 2):
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -72,7 +64,7 @@ def main():
         ea.record()
         marks[-1]["a"] = ea
     torch.cuda.synchronize()
-    ops.Ctx.backward = orig
+    ops.ON_JOIN = None
     tails, adams, bounds, steps = [], [], [], []
     for i in range(2, len(marks) - 1):
         mk, nx = marks[i], marks[i + 1]

@@ -40,11 +40,37 @@ def _prep(outputs, targets, ignore_index=None):
 
 
 def _poison(soft, *ts):
-    """NaN-fill ts in place where `soft` (device bool) is set (no host sync)"""
+    """NaN-fill ts in place where `soft` (device bool) is set (no host sync), and remember it in the
+    device's soft-label flag (raise_if_soft_targets reads it once per epoch / evaluation)"""
     if soft is not None:
         for t in ts:
             if t is not None:
                 t.masked_fill_(soft, float("nan"))
+        flag = _SOFT_SEEN.get(soft.device)
+        if flag is None:
+            flag = _SOFT_SEEN[soft.device] = torch.zeros((), dtype=torch.bool, device=soft.device)
+        flag.logical_or_(soft)
+
+
+#: per device: a MultiTaskLoss BCE call has seen a seg target that is neither 0 nor 1 since the last check
+_SOFT_SEEN = {}
+
+
+def raise_if_soft_targets(device=None):
+    """ValueError if a MultiTaskLoss BCE call saw a seg target other than 0 / 1 since the last call
+    (one host read; the loss itself was NaN-poisoned on the device).  The reference's
+    BCEWithLogitsLoss would train on such soft labels (model/unet_multitask.py:131); the fused
+    0/1 kernels cannot, so the data error is reported instead of training on NaN silently.  The
+    multitask train / eval loops call this once per epoch / evaluation."""
+    devs = [torch.device(device)] if device is not None else list(_SOFT_SEEN)
+    for d in devs:
+        if d.type == "cuda" and d.index is None:
+            d = torch.device("cuda", torch.cuda.current_device())
+        flag = _SOFT_SEEN.get(d)
+        if flag is not None and bool(flag.item()):
+            flag.zero_()
+            raise ValueError("MultiTaskLoss: seg targets must be 0 or 1 (the fused BCE kernel takes binary "
+                             "labels; a soft / out-of-range target was seen and the loss was set to NaN)")
 
 
 def _seg_forward(kind, out, nch, tgt, B, Pn, pos_weight, need_grad, ignore_index=None):

@@ -143,6 +143,11 @@ def workspace(nbytes, device, stream_key=0):
     return lst[-1]
 
 
+#: measurement hook (tools/tail_probe.py): called with the Ctx at the end of backward, after the tape,
+#: the held-back weight gradients and the finish hook, right before the compute stream joins the side
+ON_JOIN = None
+
+
 class Ctx:
     def __init__(self, dt, training, record, device):
         self.dt = dt
@@ -187,6 +192,8 @@ class Ctx:
                 # the last buckets' collectives / optimizer updates, enqueued before the join below
                 self.finish_hook()
         finally:
+            if ON_JOIN is not None:
+                ON_JOIN(self)
             if self.side is not None:
                 # everything after backward (optimizer, frees of tape tensors) follows the wgrads
                 lib.stream_wait(self.stream, self.side.cuda_stream)

@@ -145,8 +145,9 @@ def train_one_epoch_binary(model, optimizer, train_loader, device, loss_name: st
                   iteration == 0)
         if max_batches is not None and seen_batches >= max_batches:
             break
-    _progress(epoch, train_epoch, seen_batches, n_batches, gpu_used, lag.flush(), get_lr(optimizer), imgs.shape[2],
-              False)
+    if seen_batches:  # an empty loader returns 0 like the reference (nothing to report)
+        _progress(epoch, train_epoch, seen_batches, n_batches, gpu_used, lag.flush(), get_lr(optimizer), imgs.shape[2],
+                  False)
     print(f"{LogColor.GREEN}")
     time.sleep(0.2)
     return float(epoch_loss.item()) / max(seen_batches, 1)
@@ -206,7 +207,8 @@ def train_one_epoch_multitask(model, optimizer, train_loader, device, criterion,
         if hook is not None:
             hook(batch_idx)
     n = max(len(train_loader), 1)
-    l, sl, cl = (float(v) / n for v in sums.tolist())
+    l, sl, cl = (float(v) / n for v in sums.tolist())  # the epoch's one host read ...
+    losses.raise_if_soft_targets(device)  # ... and the check of the no-sync soft-label flag
     return l, sl, cl, 100.0 * float(correct.item()) / max(total, 1)
 
 
@@ -231,6 +233,7 @@ def evaluate_multitask(model, loader, device, criterion, max_batches=None):
             correct += cls_logits.argmax(1).eq(cls_targets).sum()
             total += cls_targets.size(0)
     tp, fp, fn, _tn = (float(v) for v in conf.tolist())
+    losses.raise_if_soft_targets(device)
     n = max(len(loader), 1)
     l, sl, cl = (float(v) / n for v in sums.tolist())
     return {"Loss": l, "Seg Loss": sl, "Cls Loss": cl, "IoU": tp / (tp + fp + fn + 1e-6),
