@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--extra-configs", type=int, default=1,
                     help="also time C4 (attention_unet B=8, N=1 only) and C5 (multitask_unet B=8) after the headline")
     ap.add_argument("--card-probe", type=int, default=1, help="bf16 GEMM + HBM copy rate of this card (rank 0)")
+    ap.add_argument("--ddp-bf16", type=int, default=0,
+                    help="N>1: all-reduce bf16 copies of the gradient buckets (half the bytes; opt-in)")
     return ap.parse_args()
 
 
@@ -246,7 +248,7 @@ def build_step(model_name, batch, size, loss_name, dev, rank, world, args):
         model = create_model(model_name, weights="", **kw).to(dev).train()
     model.compute_dtype = "bf16"
     if world > 1:
-        GradBuckets(model, bucket_mb=args.bucket_mb)
+        GradBuckets(model, bucket_mb=args.bucket_mb, reduce_dtype=torch.bfloat16 if args.ddp_bf16 else None)
     use_graph = bool(args.graph) and world == 1  # N>1: RCCL collectives stay eager
     overlap = bool(args.overlap_adam) and not use_graph
     opt = FusedAdam(model, lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4, capturable=use_graph, overlap=overlap,
@@ -451,6 +453,7 @@ def main():
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 3),
             "median_gpu_ms_per_step": round(median_ms, 3), "final_loss": round(final_loss, 5),
             "hip_graph": use_graph, "overlap_adam": overlap, "params_in_sync": in_sync,
+            "grad_reduce_dtype": ("bf16" if args.ddp_bf16 else "fp32") if world > 1 else None,
             "configs": configs, "card": card,
         }
         print(json.dumps(line))

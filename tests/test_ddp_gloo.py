@@ -48,7 +48,7 @@ class ArenaModel(torch.nn.Module):
         self.register_buffer("running_mean", torch.randn(7, generator=g))
 
 
-def _worker(rank, world, port, shapes, out_q):
+def _worker(rank, world, port, shapes, out_q, reduce_dtype=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -59,7 +59,7 @@ def _worker(rank, world, port, shapes, out_q):
         from utils.synthetic import make_batch
 
         model = ArenaModel(shapes, seed=100 + rank)  # ranks start from different weights
-        buckets = GradBuckets(model, bucket_mb=0.05)  # several buckets
+        buckets = GradBuckets(model, bucket_mb=0.05, reduce_dtype=reduce_dtype)  # several buckets
         # after the broadcast every rank holds rank 0's parameters and buffers
         ref0 = ArenaModel(shapes, seed=100)
         assert torch.equal(model._flat, ref0._flat)
@@ -86,7 +86,12 @@ def _worker(rank, world, port, shapes, out_q):
 
 
 @pytest.mark.timeout(600)
-def test_grad_buckets_average_matches_oracle_shards():
+@pytest.mark.parametrize("reduce_dtype", [None, torch.bfloat16], ids=["fp32", "bf16"])
+def test_grad_buckets_average_matches_oracle_shards(reduce_dtype):
+    """fp32 buckets: the average equals the mean of the per-shard oracle gradients to fp32 rounding;
+    bf16 buckets (GradBuckets(reduce_dtype=torch.bfloat16), opt-in): to a few bf16 roundings of the
+    per-rank magnitudes (<= 8 * 2^-9 * max_r |g_r| per element; gloo's bf16 AVG measured 3.6 * 2^-9),
+    identical on both ranks"""
     from oracle import ref_cpu
     from oracle.weights import make_torch_state
 
@@ -96,7 +101,7 @@ def test_grad_buckets_average_matches_oracle_shards():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, shapes, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, shapes, q, reduce_dtype)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -110,5 +115,9 @@ def test_grad_buckets_average_matches_oracle_shards():
     for n in names:
         want = 0.5 * (torch.from_numpy(res[0][1][n]) + torch.from_numpy(res[1][1][n]))
         got0, got1 = torch.from_numpy(res[0][0][n]), torch.from_numpy(res[1][0][n])
-        torch.testing.assert_close(got0, want, rtol=1e-6, atol=1e-7)
+        if reduce_dtype is None:
+            torch.testing.assert_close(got0, want, rtol=1e-6, atol=1e-7)
+        else:
+            scale = torch.maximum(torch.from_numpy(res[0][1][n]).abs(), torch.from_numpy(res[1][1][n]).abs())
+            assert ((got0 - want).abs() <= 8 * 2.0 ** -9 * scale + 1e-30).all(), n
         torch.testing.assert_close(got1, got0, rtol=0, atol=0)

@@ -227,6 +227,11 @@ WG_DEFER_HW = int(os.environ.get("UNETSEG_WG_DEFER_HW", "1024"))
 WG_FLUSH = os.environ.get("UNETSEG_WG_FLUSH", "layer4")
 
 
+#: weight gradients of 3x3 convs whose output has >= this many pixels per image run on the compute stream
+#: right after their data gradient instead of beside it on the side stream (0 = never): two persistent
+#: one-block-per-CU halo kernels sharing the CUs each take ~2x their isolated time (UNETSEG_WG_SERIAL_HW)
+WG_SERIAL_HW = int(os.environ.get("UNETSEG_WG_SERIAL_HW", "0"))
+
 #: only the virtual-concat convs (the decoder's unetUp conv1) are held back (UNETSEG_WG_DEFER_CAT=0: every 3x3)
 WG_DEFER_CAT = os.environ.get("UNETSEG_WG_DEFER_CAT", "1") == "1"
 
@@ -470,11 +475,11 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
             dY = dYp
         cin = C1 + C2
 
-        def launch_wgrad():
+        def launch_wgrad(serial=False):
             # weight gradient: on the side stream when overlapping (it only needs dY and the inputs,
             # and nothing in the data-gradient chain reads its output)
             ws_bytes = lib.conv2d_wgrad_workspace(ctx.dt, N, Pq, Qq, Kp, cin, R, S)
-            side = ctx.side
+            side = None if serial else ctx.side
             if side is not None:
                 lib.stream_wait(side.cuda_stream, ctx.stream)
                 # dY, the inputs and the input prologue's BN coefficients may be freed (compute-stream
@@ -505,7 +510,8 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                                      stride, pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, wst)
 
         deferred = defer_wgrad(ctx, N, Pq, Qq, R, S, x2)
-        if not deferred:
+        serial = bool(WG_SERIAL_HW) and not deferred and Pq * Qq >= WG_SERIAL_HW and R * S > 1
+        if not deferred and not serial:
             launch_wgrad()
         # data gradient (reads the packed weight pc.wt: the parameter is reported done after it)
         if Kp != K:
@@ -531,6 +537,8 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                                  H, W, 0, ctx.stream)
             give_grad(ctx, x1, g[..., :C1])
             give_grad(ctx, x2, g[..., C1:])
+        if serial:
+            launch_wgrad(serial=True)  # after the data gradient, on the compute stream
         if deferred:
             def late():
                 launch_wgrad()
