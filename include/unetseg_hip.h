@@ -369,6 +369,19 @@ int unetseg_augment_batch(const long long* desc_host, const long long* desc, int
                           const uint8_t* msk, long long msk_bytes, uint8_t* tmp, long long tmp_bytes, uint8_t* rsz,
                           long long rsz_bytes, int H, int W, int num_classes, int binary, float* img, long long* png,
                           float* onehot, void* stream);
+/* The same with the per-sample tables built on the device (aug_tables: Resample.c precompute_coeffs /
+ * normalize_coeffs_8bpc, Geometry.c ImagingScaleAffine and the reference's HSV LUTs restated in
+ * float64, bit-identical to utils/augment_tables.py): hsv_r float64 [B][3] (device; the drawn HSV
+ * factors, hf_dataloader.py:166), tables: device int32 scratch of n_tables entries at the
+ * descriptors' offsets.  The host decodes, draws and packs pixels only. */
+int unetseg_augment_batch_dev(const long long* desc_host, const long long* desc, int B, const double* hsv_r,
+                              int* tables, long long n_tables, const uint8_t* src, long long src_bytes,
+                              const uint8_t* msk, long long msk_bytes, uint8_t* tmp, long long tmp_bytes,
+                              uint8_t* rsz, long long rsz_bytes, int H, int W, int num_classes, int binary, float* img,
+                              long long* png, float* onehot, void* stream);
+/* the device-built tables alone (parity tests); max_tasks >= max over samples of nw + nh + 2 (+768) */
+int unetseg_augment_tables_dev(const long long* desc, int B, const double* hsv_r, int* tables, int max_tasks,
+                               void* stream);
 
 /* ---- streams ---------------------------------------------------------------------------------- */
 /* `waiter` waits for everything enqueued so far on `signaler` (device-scope release event; no

@@ -22,7 +22,8 @@ from PIL import Image
 from augment_data import make_dataset
 from oracle import augment_ref
 from utils import augment_tables as at
-from utils.hf_dataloader import AUG_DESC, D_NW, D_SRC, HFUnetDataset, hf_unet_dataset_collate, make_collate, pack_batch
+from utils.hf_dataloader import (AUG_DESC, D_KSH, D_NW, D_SRC, HFUnetDataset, hf_unet_dataset_collate, make_collate,
+                                 pack_batch)
 
 
 def _emulate(src, nw, nh):
@@ -126,17 +127,35 @@ def test_pack_batch_layout(tmp_path):
     samples = [ds[i] for i in range(4)]
     b = make_collate(ds)(samples)
     assert b.desc.shape == (4, AUG_DESC) and b.input_shape == (48, 40) and not b.binary
-    assert b.src.size == sum(s.image.size for s in samples)
+    assert b.src.numel() == sum(s.image.size for s in samples)
     assert list(b.desc[:, D_NW]) == [s.nw for s in samples]
     assert b.desc[0, D_SRC] == 0 and b.desc[1, D_SRC] == samples[0].image.size
+    np.testing.assert_array_equal(b.src[:samples[0].image.size].numpy(), samples[0].image.ravel())
     # the reference's one-argument collate_fn (hf_dataloader.py:183): settings ride on the samples
     b1 = hf_unet_dataset_collate(samples)
     assert b1.input_shape == (48, 40) and b1.num_classes == 4 and not b1.binary
-    np.testing.assert_array_equal(b1.tables, b.tables)
     np.testing.assert_array_equal(b1.desc, b.desc)
     assert len(b1) == 3 and b1.batch_size == 4  # unpacks as (images, pngs, seg_labels)
     b2 = hf_unet_dataset_collate(samples, [48, 40], 4, "multiclass")
-    np.testing.assert_array_equal(b2.tables, b.tables)
+    np.testing.assert_array_equal(b2.desc, b.desc)
+    # the host-built tables (the device builder's reference): same descriptors, same table length
+    bh = pack_batch(samples, device_tables=False)
+    np.testing.assert_array_equal(bh.desc, b.desc)
+    assert b.tables is None and bh.tables.numel() == b.n_tables
+    np.testing.assert_array_equal(b.hsv_r.numpy(), np.stack([s.r for s in samples]))
+
+
+def test_device_table_descriptors_match_host_builder():
+    """the descriptor fields the device-table path computes on the host (taps per axis, the vertical
+    pass's source-row window) equal bicubic_coeffs' for random up- and down-scales"""
+    from utils.hf_dataloader import _ksize, _vertical_window
+    rng = np.random.default_rng(4)
+    for _ in range(400):
+        n_in = int(rng.integers(1, 1500))
+        n_out = int(rng.integers(1, 1500))
+        b, _, ks = at.bicubic_coeffs(n_in, n_out)
+        assert _ksize(n_in, n_out) == ks, (n_in, n_out)
+        assert _vertical_window(n_in, n_out) == (int(b[0, 0]), int(b[-1, 0] + b[-1, 1])), (n_in, n_out)
 
 
 def test_reference_dataloader_contract(tmp_path):
@@ -178,7 +197,9 @@ def test_augment_rejects_bad_descriptor_before_launch(tmp_path):
     make_dataset(str(tmp_path), "full", "train", n=2, seed=6)
     ds = HFUnetDataset(str(tmp_path), [32, 32], 2, split="train", config="full", task="binary")
     np.random.seed(1)
-    b = pack_batch([ds[0], ds[1]], (32, 32), 2, "binary")
+    s0, s1 = ds[0], ds[1]
+    b = pack_batch([s0, s1], (32, 32), 2, "binary", device_tables=False)
+    b.desc, b.tables, b.src, b.msk = b.desc.numpy(), b.tables.numpy(), b.src.numpy(), b.msk.numpy()
     raw = lib.load()
     fake = ctypes.c_void_p(16)  # never dereferenced: the host checks fail first
 
@@ -186,6 +207,21 @@ def test_augment_rejects_bad_descriptor_before_launch(tmp_path):
         return raw.unetseg_augment_batch(desc.ctypes.data, fake, 2, tables.ctypes.data, fake, tables.size, fake,
                                          src_bytes, fake, b.msk.size, fake, b.tmp_bytes, fake, b.rsz_bytes, 32, 32,
                                          2, 1, fake, fake, None, None)
+
+    # the device-table entry point validates the descriptors it builds the tables from
+    bd = pack_batch([s0, s1], (32, 32), 2, "binary")
+    dd = bd.desc.numpy()
+
+    def call_dev(desc, src_bytes, n_tables=bd.n_tables):
+        return raw.unetseg_augment_batch_dev(desc.ctypes.data, fake, 2, fake, fake, n_tables, fake, src_bytes, fake,
+                                             bd.msk.numel(), fake, bd.tmp_bytes, fake, bd.rsz_bytes, 32, 32, 2, 1,
+                                             fake, fake, None, None)
+
+    assert call_dev(dd, bd.src.numel() - 1) != 0 and b"image range" in raw.unetseg_last_error()
+    assert call_dev(dd, bd.src.numel(), bd.n_tables - 1) != 0 and b"table range" in raw.unetseg_last_error()
+    d2 = dd.copy()
+    d2[0, D_KSH] += 2  # taps that do not match the sizes
+    assert call_dev(d2, bd.src.numel()) != 0 and b"kernel sizes" in raw.unetseg_last_error()
 
     assert call(b.desc, b.tables, b.src.size - 1) != 0  # image range
     assert b"image range" in raw.unetseg_last_error()

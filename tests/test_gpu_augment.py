@@ -176,3 +176,56 @@ def test_reference_loop_contract(tmp_path, cls_label):
     item = tuple(s)
     assert len(item) == (4 if cls_label else 3)
     _check(ds, [s], tuple(torch.from_numpy(np.asarray(v))[None] for v in item[:3]))
+
+
+def _fake_samples(rng, n, hsv=True):
+    from utils.hf_dataloader import RawSample
+    out = []
+    for i in range(n):
+        iw, ih = int(rng.integers(1, 1400)), int(rng.integers(1, 1400))
+        mw, mh = (iw, ih) if i % 3 else (int(rng.integers(1, 900)), int(rng.integers(1, 900)))
+        nw, nh = int(rng.integers(1, 1100)), int(rng.integers(1, 1100))
+        r = (rng.uniform(-1, 1, 3) * [.1, .7, .3] + 1) if (hsv and i % 4) else None
+        out.append(RawSample(image=np.zeros((ih, iw, 3), np.uint8), mask=np.zeros((mh, mw), np.uint8), nw=nw, nh=nh,
+                             dx=0, dy=0, flip=False, r=r, input_shape=(64, 64), num_classes=2, task="binary"))
+    return out
+
+
+def test_device_tables_bit_exact():
+    """unetseg_augment_tables_dev (aug_tables) against the host builder utils/augment_tables.py (itself
+    pinned against Pillow by tests/test_augment_cpu.py): every BICUBIC window / tap, NEAREST index and
+    HSV LUT entry equal, for random up- and down-scales, masks of another size, with and without HSV"""
+    from unetseg_hip.lib import lib
+    from utils.hf_dataloader import pack_batch
+    rng = np.random.default_rng(21)
+    for rep in range(4):
+        samples = _fake_samples(rng, 24)
+        host = pack_batch(samples, device_tables=False)
+        devb = pack_batch(samples)
+        np.testing.assert_array_equal(devb.desc.numpy(), host.desc.numpy())
+        desc = devb.desc.cuda()
+        r = devb.hsv_r.cuda()
+        tab = torch.full((devb.n_tables,), -7, dtype=torch.int32, device="cuda")
+        tasks = max(s.nw + s.nh + 2 + 768 for s in samples)
+        lib.augment_tables_dev(desc.data_ptr(), len(samples), r.data_ptr(), tab.data_ptr(), tasks,
+                               torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        got, want = tab.cpu().numpy(), host.tables.numpy()
+        bad = np.flatnonzero(got != want)
+        assert bad.size == 0, (rep, bad[:8], got[bad[:8]], want[bad[:8]])
+
+
+def test_device_tables_batch_equals_host_tables(tmp_path):
+    """the bench-size batch through unetseg_augment_batch_dev equals unetseg_augment_batch with host
+    tables, bit for bit (images, labels, one-hot)"""
+    from utils.hf_dataloader import pack_batch
+    sizes = [(640, 480), (480, 640), (800, 600), (512, 512)] * 4
+    make_dataset(str(tmp_path), "full", "train", n=16, seed=6, sizes=sizes)
+    ds = HFUnetDataset(str(tmp_path), [512, 512], 2, split="train", config="full", task="binary")
+    np.random.seed(13)
+    samples = [ds[i] for i in range(16)]
+    a = pack_batch(samples).to_device("cuda")
+    b = pack_batch(samples, device_tables=False).to_device("cuda")
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)

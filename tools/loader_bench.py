@@ -22,6 +22,16 @@ for p in (REPO, os.path.join(REPO, "unet-embroidery-seg_amd"), os.path.join(REPO
 import torch  # noqa: E402
 
 
+def _cpu_quota():
+    """CPUs this process may use per the cgroup quota (the GPU box grants a share of a larger host:
+    more workers than this share contend with the main process and the pinning thread)"""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=256)
@@ -42,12 +52,15 @@ def main():
     ds = HFUnetDataset(root, [a.size, a.size], 2, split="train", config="full", task="binary")
     res = {"dataset": f"{a.n} synthetic images (JPEG and PNG, 640x480-class) + PNG masks, parquet (convert_and_upload layout)",
            "batch": a.batch, "input_size": a.size, "task": "binary", "augmentation": True,
-           "host_cpus_affinity": len(os.sched_getaffinity(0)), "make_dataset_s": round(t_make, 1), "runs": []}
+           "host_cpus_affinity": len(os.sched_getaffinity(0)), "cpu_quota": _cpu_quota(),
+           "make_dataset_s": round(t_make, 1), "runs": []}
     for w in a.workers:
         for onehot in (False, True):
+            # pin_memory=True as the reference's train.py:140-150 (RawBatch.pin_memory runs in the
+            # DataLoader's pinning thread, off the main thread)
             dl = torch.utils.data.DataLoader(ds, batch_size=a.batch, shuffle=True, num_workers=w,
                                              collate_fn=hf_unet_dataset_collate, drop_last=True,
-                                             persistent_workers=w > 0)
+                                             persistent_workers=w > 0, pin_memory=True)
             loader = DeviceLoader(dl, "cuda", onehot=onehot)
             times = []
             for p in range(a.passes + 1):

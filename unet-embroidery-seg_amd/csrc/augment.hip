@@ -200,6 +200,116 @@ int grid_for(long work) {
   return (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));
 }
 
+// ---- the per-sample tables built on the device (utils/augment_tables.py restated in float64) ----
+// Every float64 operation is the one numpy performs, in the same order, with contraction off, so the
+// int32 tables are bit-identical to the host builder's (which is pinned against Pillow).
+__device__ double bicubic_filter(double x) {
+#pragma clang fp contract(off)
+  const double a = -0.5;
+  x = fabs(x);
+  if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1;
+  if (x < 2.0) return (((x - 5) * x + 8) * x - 4) * a;
+  return 0.0;
+}
+
+// Resample.c precompute_coeffs + normalize_coeffs_8bpc for output coordinate i: bounds (xmin, n) and
+// ksize fixed-point taps (bicubic_coeffs); `shift` is subtracted from xmin and the window clamped to
+// [0, limit) (the vertical pass reads rows y0 .. y0 + rows of the horizontal pass)
+__device__ void bicubic_row(int in_size, int out_size, int ksize, int i, int shift, int limit, int* bounds, int* k) {
+#pragma clang fp contract(off)
+  const double scale = (double)in_size / (double)out_size;
+  const double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = 2.0 * filterscale;
+  const double ss = 1.0 / filterscale;
+  const double center = ((double)i + 0.5) * scale;
+  const double lo = center - support + 0.5;
+  const long long xmin = lo < 0 ? 0 : (long long)trunc(lo);
+  long long hi = (long long)trunc(center + support + 0.5);
+  hi = hi < in_size ? hi : in_size;
+  const long long xmax = hi - xmin;
+  // two passes over the taps (the filter re-evaluated, same values): the normalising sum first, in
+  // the C loop's order, then the fixed-point taps -- no per-thread array
+  double ww = 0.0;
+  for (int x = 0; x < ksize; ++x) ww += x < xmax ? bicubic_filter(((double)((long long)x + xmin) - center + 0.5) * ss) : 0.0;
+  for (int x = 0; x < ksize; ++x) {
+    const double w = x < xmax ? bicubic_filter(((double)((long long)x + xmin) - center + 0.5) * ss) : 0.0;
+    const double kx = ww != 0.0 ? w / ww : w;
+    const double scaled = kx * (double)(1 << kPrecision);
+    k[x] = (int)trunc(kx < 0 ? -0.5 + scaled : 0.5 + scaled);
+  }
+  long long b0 = xmin - shift, n = xmax;
+  if (b0 < 0) {
+    n += b0;
+    b0 = 0;
+  }
+  if (b0 + n > limit) n = limit - b0;
+  bounds[0] = (int)b0;
+  bounds[1] = (int)(n < 0 ? 0 : n);
+}
+
+// Geometry.c ImagingScaleAffine's accumulated source coordinate (nearest_index): one sequential loop
+__device__ void nearest_rows(int in_size, int out_size, int* idx) {
+#pragma clang fp contract(off)
+  const double a = (double)in_size / (double)out_size;
+  double xo = a * 0.5;
+  for (int i = 0; i < out_size; ++i) {
+    if (i) xo += a;
+    long long v = (long long)trunc(xo);
+    idx[i] = (int)(v < in_size - 1 ? v : in_size - 1);
+  }
+}
+
+// one block per (sample, part): tasks [0, nw) horizontal taps, [nw, nw + nh) vertical taps, then the
+// two nearest-index scans and the 768 LUT entries (hsv_luts)
+__global__ __launch_bounds__(256) void aug_tables(const long long* desc, const double* hsv_r, int* tables) {
+#pragma clang fp contract(off)
+  const int n = blockIdx.y;
+  const long long* d = desc + (long)n * AUG_DESC;
+  const int iw = (int)d[D_IW], ih = (int)d[D_IH], nw = (int)d[D_NW], nh = (int)d[D_NH];
+  const int ksh = (int)d[D_KSH], ksv = (int)d[D_KSV], y0 = (int)d[D_Y0], rows = (int)d[D_ROWS];
+  const int hsv = (int)d[D_HSV];
+  int* bh = tables + d[D_TAB];
+  int* kh = bh + (long)nw * 2;
+  int* bv = kh + (long)nw * ksh;
+  int* kv = bv + (long)nh * 2;
+  int* nx = kv + (long)nh * ksv;
+  int* ny = nx + nw;
+  int* lut = ny + nh;
+  const long tasks = (long)nw + nh + 2 + (hsv ? 768 : 0);
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < tasks; t += (long)gridDim.x * blockDim.x) {
+    if (t < nw) {
+      bicubic_row(iw, nw, ksh, (int)t, 0, iw, bh + 2 * t, kh + t * ksh);
+    } else if (t < (long)nw + nh) {
+      const int y = (int)(t - nw);
+      bicubic_row(ih, nh, ksv, y, y0, rows, bv + 2 * y, kv + (long)y * ksv);
+    } else if (t == (long)nw + nh) {
+      nearest_rows((int)d[D_MIW], nw, nx);
+    } else if (t == (long)nw + nh + 1) {
+      nearest_rows((int)d[D_MIH], nh, ny);
+    } else {
+      const int e = (int)(t - nw - nh - 2), c = e >> 8, x = e & 255;
+      const double r = hsv_r[n * 3 + c];
+      const double v = (double)x * r;
+      int o;
+      if (c == 0) {
+        o = (int)fmod(v, 180.0);  // (x * r0) % 180, x * r0 >= 0
+      } else {
+        const double cv = v < 0.0 ? 0.0 : (v > 255.0 ? 255.0 : v);
+        o = (int)cv;
+      }
+      lut[e] = o & 255;
+    }
+  }
+}
+
+// ksize of a BICUBIC axis (bicubic_coeffs), and the first / one-past-last source row the vertical
+// pass reads (resize_plan's ybox), recomputed on the host to validate a descriptor
+long long bicubic_ksize(long long in_size, long long out_size) {
+  double fs = (double)in_size / (double)out_size;
+  if (fs < 1.0) fs = 1.0;
+  return (long long)ceil(2.0 * fs) * 2 + 1;
+}
+
 }  // namespace
 
 UNETSEG_API int unetseg_augment_tables_len(long long nw, long long nh, long long ksh, long long ksv, long long hsv) {
@@ -251,5 +361,61 @@ UNETSEG_API int unetseg_augment_batch(const long long* desc_host, const long lon
   aug_compose<<<dim3(grid_for((long)H * W), B), 256, 0, stream>>>(desc, tables, rsz, msk, H, W, num_classes, binary,
                                                                   img, png, onehot);
   US_LAUNCH_CHECK("aug_compose");
+  return 0;
+}
+
+// The same batch with the per-sample tables built on the device (aug_tables) from the descriptors and
+// the HSV factors hsv_r (float64 [B][3], device): the host only decodes, draws and packs the pixels.
+// tables: device scratch of n_tables int32 laid out as desc[D_TAB] / unetseg_augment_tables_len say.
+UNETSEG_API int unetseg_augment_batch_dev(const long long* desc_host, const long long* desc, int B, const double* hsv_r,
+                                          int* tables, long long n_tables, const uint8_t* src, long long src_bytes,
+                                          const uint8_t* msk, long long msk_bytes, uint8_t* tmp, long long tmp_bytes,
+                                          uint8_t* rsz, long long rsz_bytes, int H, int W, int num_classes, int binary,
+                                          float* img, long long* png, float* onehot, hipStream_t stream) {
+  US_CHECK_ARG(B > 0 && H > 0 && W > 0 && num_classes > 0, "augment_batch_dev: bad sizes B=%d H=%d W=%d nc=%d", B, H,
+               W, num_classes);
+  US_CHECK_ARG(desc_host && desc && hsv_r && tables && src && msk && tmp && rsz && img && png,
+               "augment_batch_dev: null pointer");
+  long max_h = 1, max_v = 1, max_t = 1;
+  for (int i = 0; i < B; ++i) {
+    const long long* d = desc_host + (long)i * AUG_DESC;
+    const long long iw = d[D_IW], ih = d[D_IH], nw = d[D_NW], nh = d[D_NH], miw = d[D_MIW], mih = d[D_MIH];
+    US_CHECK_ARG(iw > 0 && ih > 0 && nw > 0 && nh > 0 && miw > 0 && mih > 0, "augment_batch_dev: sample %d is empty", i);
+    US_CHECK_ARG(d[D_KSH] == bicubic_ksize(iw, nw) && d[D_KSV] == bicubic_ksize(ih, nh),
+                 "augment_batch_dev: sample %d kernel sizes %lld / %lld", i, d[D_KSH], d[D_KSV]);
+    US_CHECK_ARG(d[D_Y0] >= 0 && d[D_ROWS] > 0 && d[D_Y0] + d[D_ROWS] <= ih, "augment_batch_dev: sample %d row window",
+                 i);
+    US_CHECK_ARG(d[D_SRC] >= 0 && d[D_SRC] + iw * ih * 3 <= src_bytes, "augment_batch_dev: sample %d image range", i);
+    US_CHECK_ARG(d[D_MSK] >= 0 && d[D_MSK] + miw * mih <= msk_bytes, "augment_batch_dev: sample %d mask range", i);
+    US_CHECK_ARG(d[D_TMP] >= 0 && d[D_TMP] + d[D_ROWS] * nw * 3 <= tmp_bytes, "augment_batch_dev: sample %d tmp range",
+                 i);
+    US_CHECK_ARG(d[D_RSZ] >= 0 && d[D_RSZ] + nh * nw * 3 <= rsz_bytes, "augment_batch_dev: sample %d rsz range", i);
+    const long long len = tab_len(nw, nh, d[D_KSH], d[D_KSV], d[D_HSV]);
+    US_CHECK_ARG(d[D_TAB] >= 0 && d[D_TAB] + len <= n_tables, "augment_batch_dev: sample %d table range", i);
+    max_h = max_h > d[D_ROWS] * nw ? max_h : (long)(d[D_ROWS] * nw);
+    max_v = max_v > nh * nw * 3 ? max_v : (long)(nh * nw * 3);
+    const long tasks = (long)(nw + nh + 2 + (d[D_HSV] ? 768 : 0));
+    max_t = max_t > tasks ? max_t : tasks;
+  }
+  // the kernels' indices are in range by construction: every window is clamped to its image (the
+  // vertical one to the row window), the nearest indices to [0, size)
+  aug_tables<<<dim3(grid_for(max_t), B), 256, 0, stream>>>(desc, hsv_r, tables);
+  US_LAUNCH_CHECK("aug_tables");
+  aug_hpass<<<dim3(grid_for(max_h), B), 256, 0, stream>>>(desc, tables, src, tmp);
+  US_LAUNCH_CHECK("aug_hpass");
+  aug_vpass<<<dim3(grid_for(max_v), B), 256, 0, stream>>>(desc, tables, tmp, rsz);
+  US_LAUNCH_CHECK("aug_vpass");
+  aug_compose<<<dim3(grid_for((long)H * W), B), 256, 0, stream>>>(desc, tables, rsz, msk, H, W, num_classes, binary,
+                                                                  img, png, onehot);
+  US_LAUNCH_CHECK("aug_compose");
+  return 0;
+}
+
+// the device-built tables alone (tests: compared with utils/augment_tables.py bit for bit)
+UNETSEG_API int unetseg_augment_tables_dev(const long long* desc, int B, const double* hsv_r, int* tables, int max_tasks,
+                                           hipStream_t stream) {
+  US_CHECK_ARG(B > 0 && desc && hsv_r && tables && max_tasks > 0, "augment_tables_dev: bad args");
+  aug_tables<<<dim3(grid_for(max_tasks), B), 256, 0, stream>>>(desc, hsv_r, tables);
+  US_LAUNCH_CHECK("aug_tables");
   return 0;
 }

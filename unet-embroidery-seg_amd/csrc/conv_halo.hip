@@ -1442,7 +1442,13 @@ int halo3_wgrad_splits(const HaloWgradArgs& a) {
   static const int maxg = getenv("UNETSEG_HALO_WG_MAXG") ? atoi(getenv("UNETSEG_HALO_WG_MAXG")) : 512;
   // seconds per (8 x 32)-pixel tile of one block (the makespan model; UNETSEG_HALO_WG_TILE_US overrides)
   static const double tile_s = (getenv("UNETSEG_HALO_WG_TILE_US") ? atof(getenv("UNETSEG_HALO_WG_TILE_US")) : 1.0) * 1e-6;
-  for (int g = 1; g <= maxg && g <= n_sp; ++g) {
+  // with several (cout, cin) groups, the blocks of one slot in different groups walk the same spatial
+  // tiles in step; G a multiple of 8 puts them on one XCD (block b runs on XCD b % 8), so a tile's dY
+  // (read by every cin group) or X halo (every cout group) comes from that XCD's L2 after the first
+  // read instead of from HBM (UNETSEG_HALO_WG_XCD=0: any G)
+  static const bool xcd = !getenv("UNETSEG_HALO_WG_XCD") || atoi(getenv("UNETSEG_HALO_WG_XCD")) != 0;
+  const int step = (xcd && groups > 1) ? 8 : 1;
+  for (int g = step; g <= maxg && g <= n_sp; g += step) {
     if (slab * g > 768.0 * (1 << 20)) break;  // workspace cap
     const double rounds = (double)((groups * g + 255) / 256);
     const double t = rounds * ((n_sp + g - 1) / g) * tile_s + slab * g / 4e12;

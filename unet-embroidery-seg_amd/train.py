@@ -110,7 +110,7 @@ def _loader(ds, args, shuffle, rank, world, device, workers=None):
     workers = args.workers if workers is None else workers
     hf = isinstance(ds, HFUnetDataset)
     dl = DataLoader(ds, batch_size=args.batch_size, shuffle=shuffle, sampler=sampler, num_workers=workers,
-                    pin_memory=not hf, drop_last=False, collate_fn=make_collate(ds) if hf else collate,
+                    pin_memory=True, drop_last=False, collate_fn=make_collate(ds) if hf else collate,
                     worker_init_fn=_SeededWorkerInit(args.seed) if workers else None)
     # the fp32 one-hot seg_labels are read by the multiclass Dice term only
     return DeviceLoader(dl, device, onehot=args.task == "multiclass") if hf else dl

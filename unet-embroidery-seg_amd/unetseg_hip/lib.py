@@ -121,6 +121,8 @@ SIGNATURES = {
     "unetseg_channel_stats": (I, [I, P, I, L, I, I, P, P]),
     "unetseg_augment_tables_len": (I, [LL, LL, LL, LL, LL]),
     "unetseg_augment_batch": (I, [P, P, I, P, P, LL, P, LL, P, LL, P, LL, P, LL, I, I, I, I, P, P, P, P]),
+    "unetseg_augment_batch_dev": (I, [P, P, I, P, P, LL, P, LL, P, LL, P, LL, P, LL, I, I, I, I, P, P, P, P]),
+    "unetseg_augment_tables_dev": (I, [P, I, P, P, I, P]),
 }
 
 #: functions returning a value rather than a status (no RuntimeError on non-zero)

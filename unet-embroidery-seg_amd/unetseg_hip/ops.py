@@ -163,6 +163,7 @@ class Ctx:
         self.deferred = []  # weight-gradient launches held back until a flush point (defer_wgrad)
         self.flushed = False  # the flush marker has run in this backward
         self.has_marker = False  # the forward recorded a flush marker (models without one defer nothing)
+        self.layer = None  # the encoder layer the forward is in (flush_point), for WG_SERIAL_LAYERS
 
     def push(self, fn):
         if self.tape is not None:
@@ -231,6 +232,9 @@ WG_FLUSH = os.environ.get("UNETSEG_WG_FLUSH", "layer4")
 #: right after their data gradient instead of beside it on the side stream (0 = never): two persistent
 #: one-block-per-CU halo kernels sharing the CUs each take ~2x their isolated time (UNETSEG_WG_SERIAL_HW)
 WG_SERIAL_HW = int(os.environ.get("UNETSEG_WG_SERIAL_HW", "0"))
+#: encoder layers ("stem", "layer1", ...) whose weight gradients run on the compute stream: at the end of
+#: the backward the weight-gradient stream lags the compute stream (UNETSEG_WG_SERIAL_LAYERS, comma list)
+WG_SERIAL_LAYERS = frozenset(v for v in os.environ.get("UNETSEG_WG_SERIAL_LAYERS", "stem,layer1").split(",") if v)
 
 #: only the virtual-concat convs (the decoder's unetUp conv1) are held back (UNETSEG_WG_DEFER_CAT=0: every 3x3)
 WG_DEFER_CAT = os.environ.get("UNETSEG_WG_DEFER_CAT", "1") == "1"
@@ -246,6 +250,7 @@ def defer_wgrad(ctx, N, Pq, Qq, R, S, x2):
 
 def flush_point(ctx, where):
     """forward marker: in backward, the deferred weight gradients are launched when the tape reaches it"""
+    ctx.layer = where
     if WG_DEFER_HW and where == WG_FLUSH and ctx.tape is not None:
         ctx.has_marker = True
 
@@ -385,6 +390,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
     use(x1, x2)
     # x1's first consumer in the forward delivers the last contribution to its gradient in the backward
     last_grad = x1.uses == 1
+    layer = ctx.layer
     X1 = x1.data
     N, H, W, C1 = X1.shape
     X2 = x2.data if x2 is not None else None
@@ -510,7 +516,8 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                                      stride, pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, wst)
 
         deferred = defer_wgrad(ctx, N, Pq, Qq, R, S, x2)
-        serial = bool(WG_SERIAL_HW) and not deferred and Pq * Qq >= WG_SERIAL_HW and R * S > 1
+        serial = not deferred and ((bool(WG_SERIAL_HW) and Pq * Qq >= WG_SERIAL_HW and R * S > 1) or
+                                   layer in WG_SERIAL_LAYERS)
         if not deferred and not serial:
             launch_wgrad()
         # data gradient (reads the packed weight pc.wt: the parameter is reported done after it)
@@ -699,7 +706,7 @@ def stem_conv(ctx, x, conv_mod):
         if dY is None:
             return
         ws_bytes = lib.stem_wgrad_workspace(N, H, W, K)
-        side = ctx.side
+        side = None if "stem" in WG_SERIAL_LAYERS else ctx.side
         if side is not None:
             lib.stream_wait(side.cuda_stream, ctx.stream)
             for t in (dY, xp):

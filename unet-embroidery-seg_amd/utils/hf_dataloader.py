@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import glob
 import io
+import math
 import os
 from dataclasses import dataclass, field
 
@@ -41,7 +42,7 @@ import numpy as np
 import torch
 from PIL import Image
 
-from utils.augment_tables import bicubic_coeffs, hsv_luts, nearest_index
+from utils import augment_tables as at
 
 AUG_DESC = 20  # csrc/augment.hip descriptor width (int64)
 (D_SRC, D_MSK, D_TMP, D_RSZ, D_IW, D_IH, D_NW, D_NH, D_DX, D_DY, D_FLIP, D_Y0, D_ROWS, D_KSH, D_KSV, D_TAB, D_HSV,
@@ -212,17 +213,22 @@ class HFUnetDataset(torch.utils.data.Dataset):
 
 @dataclass
 class RawBatch:
-    """host side of one batch: packed pixels + descriptors + tables, ready for unetseg_augment_batch"""
-    src: np.ndarray
-    msk: np.ndarray
-    desc: np.ndarray  # int64 [B][AUG_DESC]
-    tables: np.ndarray  # int32
+    """host side of one batch: packed pixels + descriptors (+ host-built tables, or the HSV factors
+    the device builds them from), ready for unetseg_augment_batch(_dev).  The arrays are torch CPU
+    tensors -- in a DataLoader worker they are allocated in shared memory, so the batch reaches the
+    main process as file descriptors instead of ~15 MB of pickled bytes."""
+    src: torch.Tensor  # uint8
+    msk: torch.Tensor  # uint8
+    desc: torch.Tensor  # int64 [B][AUG_DESC]
+    tables: torch.Tensor | None  # int32 (host-built), or None: built on the device from hsv_r
     tmp_bytes: int
     rsz_bytes: int
     input_shape: tuple
     num_classes: int
     binary: bool
     cls_labels: np.ndarray | None = None
+    hsv_r: torch.Tensor | None = None  # float64 [B][3] (device tables)
+    n_tables: int = 0
     pinned: dict = field(default_factory=dict)
     _tensors: tuple | None = None
 
@@ -233,8 +239,10 @@ class RawBatch:
     def pin(self):
         """page-lock the host arrays (once) so the uploads run asynchronously"""
         if not self.pinned:
-            for k in ("src", "msk", "tables", "desc"):
-                self.pinned[k] = torch.from_numpy(getattr(self, k)).pin_memory()
+            for k in ("src", "msk", "tables", "desc", "hsv_r"):
+                v = getattr(self, k)
+                if v is not None:
+                    self.pinned[k] = (v if torch.is_tensor(v) else torch.from_numpy(v)).pin_memory()
         return self
 
     def pin_memory(self, device=None):
@@ -276,13 +284,27 @@ class RawBatch:
             img = torch.empty(B, 3, H, W, dtype=torch.float32, device=device)
             png = torch.empty(B, H, W, dtype=torch.int64, device=device)
             seg = torch.empty(B, H, W, self.num_classes + 1, dtype=torch.float32, device=device) if onehot else None
-        lib.augment_batch(self.pinned["desc"].data_ptr(), dev["desc"].data_ptr(), B, self.pinned["tables"].data_ptr(),
-                          dev["tables"].data_ptr(), self.tables.size, dev["src"].data_ptr(), self.src.size,
-                          dev["msk"].data_ptr(), self.msk.size, tmp.data_ptr(), self.tmp_bytes, rsz.data_ptr(),
-                          self.rsz_bytes, H, W, self.num_classes, int(self.binary), img.data_ptr(), png.data_ptr(),
-                          seg.data_ptr() if seg is not None else None, stream.cuda_stream)
+        scratch = [tmp, rsz]
+        if self.tables is None:
+            # tables built on the device from the descriptors (unetseg_augment_batch_dev)
+            with torch.cuda.stream(stream):
+                tab = torch.empty(max(self.n_tables, 1), dtype=torch.int32, device=device)
+            scratch.append(tab)
+            lib.augment_batch_dev(self.pinned["desc"].data_ptr(), dev["desc"].data_ptr(), B, dev["hsv_r"].data_ptr(),
+                                  tab.data_ptr(), self.n_tables, dev["src"].data_ptr(), self.src.numel(),
+                                  dev["msk"].data_ptr(), self.msk.numel(), tmp.data_ptr(), self.tmp_bytes,
+                                  rsz.data_ptr(), self.rsz_bytes, H, W, self.num_classes, int(self.binary),
+                                  img.data_ptr(), png.data_ptr(), seg.data_ptr() if seg is not None else None,
+                                  stream.cuda_stream)
+        else:
+            lib.augment_batch(self.pinned["desc"].data_ptr(), dev["desc"].data_ptr(), B,
+                              self.pinned["tables"].data_ptr(), dev["tables"].data_ptr(), self.tables.numel(),
+                              dev["src"].data_ptr(), self.src.numel(), dev["msk"].data_ptr(), self.msk.numel(),
+                              tmp.data_ptr(), self.tmp_bytes, rsz.data_ptr(), self.rsz_bytes, H, W, self.num_classes,
+                              int(self.binary), img.data_ptr(), png.data_ptr(),
+                              seg.data_ptr() if seg is not None else None, stream.cuda_stream)
         # the scratch and the uploads must outlive the kernels queued on `stream`
-        for t in list(dev.values()) + [tmp, rsz]:
+        for t in list(dev.values()) + scratch:
             t.record_stream(stream)
         out = (img, png, seg)
         if self.cls_labels is not None:
@@ -292,9 +314,43 @@ class RawBatch:
         return out
 
 
-def pack_batch(samples, input_shape=None, num_classes=None, task=None):
-    """list[RawSample] -> RawBatch (descriptors + tables per utils/augment_tables.py).  The settings
-    default to the ones the samples carry (HFUnetDataset.__getitem__)."""
+def _host_buffer(n, dtype):
+    """a CPU tensor for a batch array: in shared memory inside a DataLoader worker (the batch then
+    crosses to the main process as a file descriptor, not as pickled bytes)"""
+    t = torch.empty(max(int(n), 1), dtype=dtype)
+    if torch.utils.data.get_worker_info() is not None:
+        t.share_memory_()
+    return t
+
+
+def _vertical_window(ih, nh):
+    """resize_plan's ybox: the first and one-past-last source rows of the vertical BICUBIC pass,
+    from bicubic_coeffs' bounds of output rows 0 and nh - 1 (the same float64 operations)"""
+    scale = float(ih) / nh
+    support = at.BICUBIC_SUPPORT * max(scale, 1.0)
+
+    def bounds(i):
+        center = (i + 0.5) * scale
+        lo = center - support + 0.5
+        xmin = 0 if lo < 0 else math.trunc(lo)
+        return xmin, min(math.trunc(center + support + 0.5), ih) - xmin
+
+    y0 = bounds(0)[0]
+    xl, nl = bounds(nh - 1)
+    return y0, xl + nl
+
+
+def _ksize(in_size, out_size):
+    """bicubic_coeffs' taps per output coordinate"""
+    return int(math.ceil(at.BICUBIC_SUPPORT * max(float(in_size) / out_size, 1.0))) * 2 + 1
+
+
+def pack_batch(samples, input_shape=None, num_classes=None, task=None, device_tables=True):
+    """list[RawSample] -> RawBatch.  The settings default to the ones the samples carry
+    (HFUnetDataset.__getitem__).  device_tables (default): the BICUBIC / NEAREST tables and HSV LUTs
+    are built on the device from the descriptors (csrc/augment.hip aug_tables, bit-identical to
+    utils/augment_tables.py); False builds them here (the reference builder the device one is tested
+    against)."""
     if samples and input_shape is None:
         input_shape, num_classes, task = samples[0].input_shape, samples[0].num_classes, task or samples[0].task
     if input_shape is None or num_classes is None:
@@ -302,40 +358,57 @@ def pack_batch(samples, input_shape=None, num_classes=None, task=None):
     task = task or "multiclass"
     B = len(samples)
     desc = np.zeros((B, AUG_DESC), np.int64)
-    srcs, msks, tabs = [], [], []
+    hsv_r = np.ones((B, 3), np.float64)
+    tabs = []
     src_off = msk_off = tmp_off = rsz_off = tab_off = 0
     for i, s in enumerate(samples):
         ih, iw = s.image.shape[:2]
         mh, mw = s.mask.shape[:2]
-        bh, kh, ksh = bicubic_coeffs(iw, s.nw)
-        bv, kv, ksv = bicubic_coeffs(ih, s.nh)
-        y0 = int(bv[0, 0])
-        y1 = int(bv[-1, 0] + bv[-1, 1])
-        bv = bv.copy()
-        bv[:, 0] -= y0  # ImagingResampleInner: the vertical pass reads the horizontal pass's rows
-        parts = [bh.ravel(), kh.ravel(), bv.ravel(), kv.ravel(), nearest_index(mw, s.nw), nearest_index(mh, s.nh)]
         hsv = s.r is not None
-        if hsv:
-            parts.append(hsv_luts(np.asarray(s.r)).astype(np.int32).ravel())
-        t = np.concatenate([np.asarray(p, np.int32) for p in parts])
+        if device_tables:
+            ksh, ksv = _ksize(iw, s.nw), _ksize(ih, s.nh)
+            y0, y1 = _vertical_window(ih, s.nh)
+            tlen = 2 * s.nw + s.nw * ksh + 2 * s.nh + s.nh * ksv + s.nw + s.nh + (768 if hsv else 0)
+            if hsv:
+                hsv_r[i] = np.asarray(s.r, np.float64)
+        else:
+            bh, kh, ksh = at.bicubic_coeffs(iw, s.nw)
+            bv, kv, ksv = at.bicubic_coeffs(ih, s.nh)
+            y0 = int(bv[0, 0])
+            y1 = int(bv[-1, 0] + bv[-1, 1])
+            bv = bv.copy()
+            bv[:, 0] -= y0  # ImagingResampleInner: the vertical pass reads the horizontal pass's rows
+            parts = [bh.ravel(), kh.ravel(), bv.ravel(), kv.ravel(), at.nearest_index(mw, s.nw),
+                     at.nearest_index(mh, s.nh)]
+            if hsv:
+                parts.append(at.hsv_luts(np.asarray(s.r)).astype(np.int32).ravel())
+            t = np.concatenate([np.asarray(p, np.int32) for p in parts])
+            tabs.append(t)
+            tlen = t.size
         rows = y1 - y0
         desc[i, [D_SRC, D_MSK, D_TMP, D_RSZ, D_IW, D_IH, D_NW, D_NH, D_DX, D_DY, D_FLIP, D_Y0, D_ROWS, D_KSH, D_KSV,
                  D_TAB, D_HSV, D_MIW, D_MIH]] = [src_off, msk_off, tmp_off, rsz_off, iw, ih, s.nw, s.nh, s.dx, s.dy,
                                                  int(s.flip), y0, rows, ksh, ksv, tab_off, int(hsv), mw, mh]
-        srcs.append(np.ascontiguousarray(s.image, np.uint8).ravel())
-        msks.append(np.ascontiguousarray(s.mask, np.uint8).ravel())
-        tabs.append(t)
         src_off += iw * ih * 3
         msk_off += mw * mh
         tmp_off += rows * s.nw * 3
         rsz_off += s.nh * s.nw * 3
-        tab_off += t.size
+        tab_off += tlen
+    # the pixels straight into the batch buffers (one copy each)
+    src, msk = _host_buffer(src_off, torch.uint8), _host_buffer(msk_off, torch.uint8)
+    sv, mv = src.numpy(), msk.numpy()
+    for i, s in enumerate(samples):
+        a, m = np.ascontiguousarray(s.image, np.uint8).ravel(), np.ascontiguousarray(s.mask, np.uint8).ravel()
+        sv[desc[i, D_SRC]:desc[i, D_SRC] + a.size] = a
+        mv[desc[i, D_MSK]:desc[i, D_MSK] + m.size] = m
     cls = None
     if samples and samples[0].cls_label is not None:
         cls = np.array([s.cls_label for s in samples], np.int64)
-    return RawBatch(src=np.concatenate(srcs), msk=np.concatenate(msks), desc=desc, tables=np.concatenate(tabs),
-                    tmp_bytes=tmp_off, rsz_bytes=rsz_off, input_shape=tuple(int(v) for v in input_shape),
-                    num_classes=num_classes, binary=(task == "binary"), cls_labels=cls)
+    tables = torch.from_numpy(np.concatenate(tabs)) if tabs else None
+    return RawBatch(src=src, msk=msk, desc=torch.from_numpy(desc), tables=tables, tmp_bytes=tmp_off,
+                    rsz_bytes=rsz_off, input_shape=tuple(int(v) for v in input_shape), num_classes=num_classes,
+                    binary=(task == "binary"), cls_labels=cls,
+                    hsv_r=torch.from_numpy(hsv_r) if device_tables else None, n_tables=tab_off)
 
 
 class _Collate:
