@@ -99,6 +99,31 @@ __device__ __forceinline__ F block_sum(F v, F* scratch /* >= 16 entries */) {
 
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
+// ---- bilinear x2 upsample (model/unet_resnet.py:21,71 align_corners=True; unet_plain.py:36 False) --
+// source index pair and weight of output index d: align_corners=True: src = d*(in-1)/(out-1);
+// False: src = max((d+0.5)/2 - 0.5, 0)  (ATen area_pixel_compute_source_index, scale 0.5)
+__device__ __forceinline__ void up_src(int d, int in, int out, int align, int& i0, int& i1, float& l1) {
+  float src;
+  if (align) {
+    const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;  // ATen area_pixel_compute_scale
+    src = scale * (float)d;
+  } else {
+    src = ((float)d + 0.5f) * 0.5f - 0.5f;
+    if (src < 0.f) src = 0.f;
+  }
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + 1 < in ? i0 + 1 : in - 1;
+  l1 = src - (float)i0;
+}
+// the blend of the four source values, as explicit products / fmas: the upsample kernel and the halo
+// conv that upsamples its input tile on the fly (kEpiUp) produce the same bits
+__device__ __forceinline__ float up_blend(float a, float b, float c, float d, float wl0, float lw, float hl0,
+                                          float lh) {
+  const float t0 = fmaf(lw, b, wl0 * a), t1 = fmaf(lw, d, wl0 * c);
+  return fmaf(lh, t1, hl0 * t0);
+}
+
 // one conv weight of a batched pack (unetseg_pack_conv_weights); layout shared with the host
 struct UnetsegPackDesc {
   const float* w;   // fp32 [K][C][R][S]

@@ -20,32 +20,117 @@ template <typename T>
 constexpr int VE = 16 / sizeof(T);
 
 // ------------------------------------------------------------------------------------------
-// BatchNorm finalize (train): partials [2][C][G] = (sum, M2 about the tile mean) with tile
+// Per-channel reductions of row partials part[g][q][C] (G row tiles, q = 0 .. nq-1) -- the BN
+// finalizes of the forward statistics and of the fused data-gradient post-ops.  They sit on the
+// compute stream between a producer and its consumer, so they are latency kernels: one wave per
+// channel (NWV = 1, four channels per block, no barrier) when G <= 512, the four waves of a block
+// per channel above that; every lane issues all its loads (kFinRPL rows x nq) before it adds, and
+// the lanes' fp64 partials are combined in a fixed order (deterministic).
+// ------------------------------------------------------------------------------------------
+constexpr int kFinRPL = 8;  // rows per lane per round
+
+static inline int fin_waves(int G) { return G > 512 ? 4 : 1; }
+static inline unsigned fin_blocks(int C, int nwv) { return nwv == 4 ? (unsigned)C : (unsigned)ceil_div(C, 4); }
+
+// sum over the channel's lanes (one wave, or the block's four waves through sc[NQ][4]); every lane
+// gets lane 0's / the fixed-order total
+template <int NWV, int NQ>
+__device__ __forceinline__ void fin_group_sum(double (&v)[NQ], double* sc) {
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) v[j] = __shfl(wave_sum_d(v[j]), 0, 64);
+  if constexpr (NWV == 4) {
+    const int wid = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) sc[j * 4 + wid] = v[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) v[j] = (sc[j * 4 + 0] + sc[j * 4 + 1]) + (sc[j * 4 + 2] + sc[j * 4 + 3]);
+  }
+}
+
+// t[j] = sum_g part[g * ldrow + (q0 + j) * C + c] for j < nq (NQ >= nq)
+template <int NWV, int NQ>
+__device__ __forceinline__ void fin_row_sums(const float* part, long ldrow, int C, int c, int G, int nq, int q0,
+                                             double (&t)[NQ], double* sc) {
+  constexpr int NL = 64 * NWV;
+  const int li = NWV == 1 ? (threadIdx.x & 63) : threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) t[j] = 0.0;
+  for (int g0 = 0; g0 < G; g0 += kFinRPL * NL) {
+    float v[NQ][kFinRPL];
+#pragma unroll
+    for (int k = 0; k < kFinRPL; ++k) {
+      const int g = g0 + li + k * NL;
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) v[j][k] = (g < G && j < nq) ? part[g * ldrow + (long)(q0 + j) * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < kFinRPL; ++k)
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) t[j] += (double)v[j][k];
+  }
+  fin_group_sum<NWV, NQ>(t, sc);
+}
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm finalize (train): partials [G][2][C] = (sum, M2 about the tile mean) with tile
 // count min(tile, M - g*tile).  Chan's parallel merge in fp64.  Updates running stats exactly as
 // nn.BatchNorm2d (momentum 0.1, unbiased running var) and emits scale/shift for the apply pass.
 // ------------------------------------------------------------------------------------------
-__global__ void bn_finalize_kernel(const float* part, int C, int G, long M, int tile, const float* gamma,
-                                   const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
-                                   float eps, float* mean_out, float* invstd_out, float* scale, float* shift) {
-  __shared__ double sc[16];
-  const int c = blockIdx.x;
-  // part: [G][2][C] (row tile g: column sums, then M2 about the tile mean)
-  const float* s = part + c;
-  const float* q = part + C + c;
+template <int NWV>
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* part, int C, int G, long M, int tile,
+                                                          const float* gamma, const float* beta, float* rmean,
+                                                          float* rvar, long long* nbt, float momentum, float eps,
+                                                          float* mean_out, float* invstd_out, float* scale,
+                                                          float* shift) {
+  __shared__ double sc[4];
+  constexpr int NL = 64 * NWV;
+  const int c = NWV == 1 ? (int)blockIdx.x * 4 + (threadIdx.x >> 6) : (int)blockIdx.x;
+  if (NWV == 1 && c >= C) return;  // whole waves: no barrier in the one-wave form
+  const int li = NWV == 1 ? (threadIdx.x & 63) : threadIdx.x;
   const long st = 2L * C;
-  double tsum = 0.0;
-  for (int g = threadIdx.x; g < G; g += blockDim.x) tsum += s[g * st];
-  tsum = block_sum(tsum, sc);
-  const double mean = tsum / (double)M;
-  double m2 = 0.0;
-  for (int g = threadIdx.x; g < G; g += blockDim.x) {
-    const long cnt = min((long)tile, M - (long)g * tile);
-    const double mg = (double)s[g * st] / (double)cnt;
-    m2 += (double)q[g * st] + (double)cnt * (mg - mean) * (mg - mean);
+  // pass 1 keeps this lane's rows in registers when one round covers G (pass 2 re-reads otherwise)
+  float sv[kFinRPL], qv[kFinRPL];
+  double tsum[1] = {0.0};
+  for (int g0 = 0; g0 < G; g0 += kFinRPL * NL) {
+#pragma unroll
+    for (int k = 0; k < kFinRPL; ++k) {
+      const int g = g0 + li + k * NL;
+      sv[k] = g < G ? part[g * st + c] : 0.f;
+      qv[k] = g < G ? part[g * st + C + c] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < kFinRPL; ++k) tsum[0] += (double)sv[k];
   }
-  m2 = block_sum(m2, sc);
-  if (threadIdx.x == 0) {
-    const double var = m2 / (double)M;
+  fin_group_sum<NWV, 1>(tsum, sc);
+  const double mean = tsum[0] / (double)M;
+  double m2[1] = {0.0};
+  const bool one_round = G <= kFinRPL * NL;
+  for (int g0 = 0; g0 < G; g0 += kFinRPL * NL) {
+    if (!one_round) {
+#pragma unroll
+      for (int k = 0; k < kFinRPL; ++k) {
+        const int g = g0 + li + k * NL;
+        sv[k] = g < G ? part[g * st + c] : 0.f;
+        qv[k] = g < G ? part[g * st + C + c] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kFinRPL; ++k) {
+      const int g = g0 + li + k * NL;
+      if (g < G) {
+        const long cnt = min((long)tile, M - (long)g * tile);
+        const double mg = (double)sv[k] / (double)cnt;
+        m2[0] += (double)qv[k] + (double)cnt * (mg - mean) * (mg - mean);
+      }
+    }
+  }
+  fin_group_sum<NWV, 1>(m2, sc);
+  if (li == 0) {
+    const double m2v = m2[0];
+    const double var = m2v / (double)M;
     const double inv = 1.0 / sqrt(var + (double)eps);
     mean_out[c] = (float)mean;
     invstd_out[c] = (float)inv;
@@ -53,7 +138,7 @@ __global__ void bn_finalize_kernel(const float* part, int C, int G, long M, int 
     scale[c] = sca;
     shift[c] = (float)(beta[c] - mean * gamma[c] * inv);
     if (rmean) {
-      const double unb = M > 1 ? m2 / (double)(M - 1) : var;
+      const double unb = M > 1 ? m2v / (double)(M - 1) : var;
       rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
       rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
     }
@@ -438,18 +523,17 @@ __global__ __launch_bounds__(256) void relu_bwd_bias_kernel(const T* dA, int ldd
 
 // The same coefficients from the row partials of a fused data-gradient post-op
 // (unetseg_conv2d_dgrad_post): part[g][2][C] = (sum dz, sum dz*xhat) per row tile.
-__global__ void bn_bwd_finalize_rows_kernel(const float* part, int C, int G, long M, const float* g1,
-                                            const float* inv1, float* dg1, float* db1, float* coef) {
-  __shared__ double sc[16];
-  const int c = blockIdx.x;
-  double a0 = 0.0, a1 = 0.0;
-  for (int g = threadIdx.x; g < G; g += blockDim.x) {
-    a0 += part[(long)g * 2 * C + c];
-    a1 += part[(long)g * 2 * C + C + c];
-  }
-  a0 = block_sum(a0, sc);
-  a1 = block_sum(a1, sc);
-  if (threadIdx.x == 0) {
+template <int NWV>
+__global__ __launch_bounds__(256) void bn_bwd_finalize_rows_kernel(const float* part, int C, int G, long M,
+                                                                   const float* g1, const float* inv1, float* dg1,
+                                                                   float* db1, float* coef) {
+  __shared__ double sc[2 * 4];
+  const int c = NWV == 1 ? (int)blockIdx.x * 4 + (threadIdx.x >> 6) : (int)blockIdx.x;
+  if (NWV == 1 && c >= C) return;
+  double t[2];
+  fin_row_sums<NWV, 2>(part, 2L * C, C, c, G, 2, 0, t, sc);
+  if ((NWV == 1 ? (threadIdx.x & 63) : threadIdx.x) == 0) {
+    const double a0 = t[0], a1 = t[1];
     dg1[c] += (float)a1;
     db1[c] += (float)a0;
     coef[0 * C + c] = g1[c] * inv1[c];
@@ -460,19 +544,19 @@ __global__ void bn_bwd_finalize_rows_kernel(const float* part, int C, int G, lon
 
 // The two-branch form for the residual post-op (unetseg_conv2d_dgrad_post_res): part[g][1+nbranch][C] =
 // (sum dz, sum dz*xhat1 [, sum dz*xhat2]) per row tile; coefficients as bn_bwd_finalize_kernel.
-__global__ void bn_bwd_finalize_rows_res_kernel(const float* part, int C, int G, long M, int nbranch, const float* g1,
-                                                const float* inv1, float* dg1, float* db1, const float* g2,
-                                                const float* inv2, float* dg2, float* db2, float* coef) {
-  __shared__ double sc[16];
-  const int c = blockIdx.x;
+template <int NWV>
+__global__ __launch_bounds__(256) void bn_bwd_finalize_rows_res_kernel(const float* part, int C, int G, long M,
+                                                                       int nbranch, const float* g1,
+                                                                       const float* inv1, float* dg1, float* db1,
+                                                                       const float* g2, const float* inv2, float* dg2,
+                                                                       float* db2, float* coef) {
+  __shared__ double sc[3 * 4];
+  const int c = NWV == 1 ? (int)blockIdx.x * 4 + (threadIdx.x >> 6) : (int)blockIdx.x;
+  if (NWV == 1 && c >= C) return;
   const int nq = 1 + nbranch;
-  double t[3] = {0, 0, 0};
-  for (int k = 0; k < nq; ++k) {
-    double acc = 0.0;
-    for (int g = threadIdx.x; g < G; g += blockDim.x) acc += part[((long)g * nq + k) * C + c];
-    t[k] = block_sum(acc, sc);
-  }
-  if (threadIdx.x == 0) {
+  double t[3];
+  fin_row_sums<NWV, 3>(part, (long)nq * C, C, c, G, nq, 0, t, sc);
+  if ((NWV == 1 ? (threadIdx.x & 63) : threadIdx.x) == 0) {
     const double sdz = t[0];
     dg1[c] += (float)t[1];
     db1[c] += (float)sdz;
@@ -490,13 +574,15 @@ __global__ void bn_bwd_finalize_rows_res_kernel(const float* part, int C, int G,
 }
 
 // out[c] (+)= sum_g part[g][k][c] for part [G][2][C] (bias gradient from the fused ReLU post-op)
-__global__ void colsum_rows_kernel(const float* part, int C, int G, int k, float* out, int accumulate) {
-  __shared__ double sc[16];
-  const int c = blockIdx.x;
-  double acc = 0.0;
-  for (int g = threadIdx.x; g < G; g += blockDim.x) acc += part[(long)g * 2 * C + k * C + c];
-  acc = block_sum(acc, sc);
-  if (threadIdx.x == 0) out[c] = accumulate ? out[c] + (float)acc : (float)acc;
+template <int NWV>
+__global__ __launch_bounds__(256) void colsum_rows_kernel(const float* part, int C, int G, int k, float* out,
+                                                          int accumulate) {
+  __shared__ double sc[4];
+  const int c = NWV == 1 ? (int)blockIdx.x * 4 + (threadIdx.x >> 6) : (int)blockIdx.x;
+  if (NWV == 1 && c >= C) return;
+  double t[1];
+  fin_row_sums<NWV, 1>(part, 2L * C, C, c, G, 1, k, t, sc);
+  if ((NWV == 1 ? (threadIdx.x & 63) : threadIdx.x) == 0) out[c] = accumulate ? out[c] + (float)t[0] : (float)t[0];
 }
 
 // out[c] (+)= sum_g part[c][g]   (fp64 accumulation, fixed order)
@@ -729,23 +815,8 @@ __global__ void maxpool_bwd_kernel(const T* dy, int ldy, const uint8_t* idx, int
 }
 
 // ------------------------------------------------------------------------------------------
-// Bilinear x2 upsample, NHWC.  align_corners=True: src = dst*(in-1)/(out-1);
-// False: src = max((dst+0.5)/2 - 0.5, 0)  (ATen area_pixel_compute_source_index, scale 0.5)
+// Bilinear x2 upsample, NHWC (source index / weight: up_src, the blend: up_blend in common.h).
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void up_src(int d, int in, int out, int align, int& i0, int& i1, float& l1) {
-  float src;
-  if (align) {
-    const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;  // ATen area_pixel_compute_scale
-    src = scale * (float)d;
-  } else {
-    src = ((float)d + 0.5f) * 0.5f - 0.5f;
-    if (src < 0.f) src = 0.f;
-  }
-  i0 = (int)src;
-  if (i0 > in - 1) i0 = in - 1;
-  i1 = i0 + 1 < in ? i0 + 1 : in - 1;
-  l1 = src - (float)i0;
-}
 
 // Row-blocked: a block covers (pixel, 8-channel) lanes of whole output rows, kRowsPB rows in turn,
 // so the per-row source index and weight are wave-uniform and the per-column ones are computed
@@ -788,7 +859,7 @@ __global__ void upsample_fwd_kernel(const T* x, int ldx, int N, int H, int W, in
     load_vec(x1 + (long)w1 * ldx, d);
     const float hl0 = 1.f - lh;
 #pragma unroll
-    for (int e = 0; e < V; ++e) o[e] = hl0 * (wl0 * a[e] + lw * b[e]) + lh * (wl0 * c[e] + lw * d[e]);
+    for (int e = 0; e < V; ++e) o[e] = up_blend(a[e], b[e], c[e], d[e], wl0, lw, hl0, lh);
     store_vec(y + ((long)r * OW + ow) * ldy + c0, o);
   }
 }
@@ -1152,10 +1223,11 @@ __global__ void pw_small_bwd_kernel(const float* dy, const T* x, int ldx, long M
     load_vec(x + p * ldx + c0, xv);
 #pragma unroll
     for (int e = 0; e < V; ++e) {
+      // explicit product then fma: the halo data gradient synthesises this value (syn_chunk)
       float s = 0.f;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        s += g[k] * wv[k][e];
+        s = k == 0 ? g[0] * wv[0][e] : fmaf(g[k], wv[k][e], s);
         sw[k][e] += g[k] * xv[e];
       }
       o[e] = s;
@@ -1455,8 +1527,14 @@ UNETSEG_API int unetseg_bn_finalize(const float* part, int C, int G, long M, int
                                     const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
                                     float eps, float* mean, float* invstd, float* scale, float* shift, void* stream) {
   US_CHECK_ARG(part && gamma && beta && mean && invstd && scale && shift && M > 0, "bn_finalize: bad args");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, C, G, M, tile, gamma, beta,
-                     rmean, rvar, nbt, momentum, eps, mean, invstd, scale, shift);
+  US_CHECK_ARG(C > 0 && G > 0 && tile > 0, "bn_finalize: bad sizes");
+  const int nwv = fin_waves(G);
+  if (nwv == 4)
+    hipLaunchKernelGGL(bn_finalize_kernel<4>, dim3(fin_blocks(C, 4)), dim3(256), 0, (hipStream_t)stream, part, C, G, M,
+                       tile, gamma, beta, rmean, rvar, nbt, momentum, eps, mean, invstd, scale, shift);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel<1>, dim3(fin_blocks(C, 1)), dim3(256), 0, (hipStream_t)stream, part, C, G, M,
+                       tile, gamma, beta, rmean, rvar, nbt, momentum, eps, mean, invstd, scale, shift);
   US_LAUNCH_CHECK("bn_finalize");
   return 0;
 }
@@ -1638,8 +1716,13 @@ UNETSEG_API int unetseg_relu_bwd_bias(int dtype, const void* dA, int ldd, const 
 UNETSEG_API int unetseg_bn_bwd_finalize_rows(const float* part, int C, int G, long M, const float* g1,
                                              const float* inv1, float* dg1, float* db1, float* coef, void* stream) {
   US_CHECK_ARG(part && g1 && inv1 && dg1 && db1 && coef && M > 0, "bn_bwd_finalize_rows: bad args");
-  hipLaunchKernelGGL(bn_bwd_finalize_rows_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, C, G, M, g1, inv1,
-                     dg1, db1, coef);
+  US_CHECK_ARG(C > 0 && G > 0, "bn_bwd_finalize_rows: bad sizes");
+  if (fin_waves(G) == 4)
+    hipLaunchKernelGGL(bn_bwd_finalize_rows_kernel<4>, dim3(fin_blocks(C, 4)), dim3(256), 0, (hipStream_t)stream, part,
+                       C, G, M, g1, inv1, dg1, db1, coef);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_rows_kernel<1>, dim3(fin_blocks(C, 1)), dim3(256), 0, (hipStream_t)stream, part,
+                       C, G, M, g1, inv1, dg1, db1, coef);
   US_LAUNCH_CHECK("bn_bwd_finalize_rows");
   return 0;
 }
@@ -1650,14 +1733,24 @@ UNETSEG_API int unetseg_bn_bwd_finalize_rows_res(const float* part, int C, int G
   US_CHECK_ARG(part && g1 && inv1 && dg1 && db1 && coef && M > 0 && C > 0 && G > 0 && (nbranch == 1 || nbranch == 2),
                "bn_bwd_finalize_rows_res: bad args");
   US_CHECK_ARG(nbranch == 1 || (g2 && inv2 && dg2 && db2), "bn_bwd_finalize_rows_res: branch 2 needs its pointers");
-  hipLaunchKernelGGL(bn_bwd_finalize_rows_res_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, C, G, M, nbranch,
-                     g1, inv1, dg1, db1, g2, inv2, dg2, db2, coef);
+  if (fin_waves(G) == 4)
+    hipLaunchKernelGGL(bn_bwd_finalize_rows_res_kernel<4>, dim3(fin_blocks(C, 4)), dim3(256), 0, (hipStream_t)stream,
+                       part, C, G, M, nbranch, g1, inv1, dg1, db1, g2, inv2, dg2, db2, coef);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_rows_res_kernel<1>, dim3(fin_blocks(C, 1)), dim3(256), 0, (hipStream_t)stream,
+                       part, C, G, M, nbranch, g1, inv1, dg1, db1, g2, inv2, dg2, db2, coef);
   US_LAUNCH_CHECK("bn_bwd_finalize_rows_res");
   return 0;
 }
 
 UNETSEG_API int unetseg_colsum_rows(const float* part, int C, int G, int k, float* out, int accumulate, void* stream) {
-  hipLaunchKernelGGL(colsum_rows_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, C, G, k, out, accumulate);
+  US_CHECK_ARG(part && out && C > 0 && G >= 0 && (k == 0 || k == 1), "colsum_rows: bad args");
+  if (fin_waves(G) == 4)
+    hipLaunchKernelGGL(colsum_rows_kernel<4>, dim3(fin_blocks(C, 4)), dim3(256), 0, (hipStream_t)stream, part, C, G, k,
+                       out, accumulate);
+  else
+    hipLaunchKernelGGL(colsum_rows_kernel<1>, dim3(fin_blocks(C, 1)), dim3(256), 0, (hipStream_t)stream, part, C, G, k,
+                       out, accumulate);
   US_LAUNCH_CHECK("colsum_rows");
   return 0;
 }
@@ -1869,7 +1962,9 @@ UNETSEG_API int unetseg_pw_small_bwd_relu(int dtype, const float* dy, const void
   CHECK_VEC(dtype, c, "pw_small_bwd_relu");
   US_CHECK_ARG(c / 8 <= 256 && 256 % (c / 8) == 0, "pw_small_bwd_relu: bad C");
   US_CHECK_ARG(k == 1 || k == 2, "pw_small_bwd_relu: k must be 1 or 2");
-  US_CHECK_ARG(dx != nullptr && part_d != nullptr, "pw_small_bwd_relu: dx and part_d required");
+  // dx == NULL: the masked gradient is not stored (the head input's producer conv synthesises it in
+  // its data / weight gradients, unetseg_conv2d_dgrad_post_syn / unetseg_conv2d_wgrad_syn)
+  US_CHECK_ARG(dy && x && w && part_w && part_b && part_d, "pw_small_bwd_relu: null pointer");
   const int G = unetseg_pw_small_tiles(M);
   hipStream_t st = (hipStream_t)stream;
   if (k == 1)
