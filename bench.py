@@ -358,8 +358,10 @@ def main():
 
     model, step, run, use_graph, overlap = build_step(args.model, args.batch, args.size, args.loss, dev, rank, world,
                                                       args)
+    torch.cuda.reset_peak_memory_stats(dev)
     wall, median_ms, gpu_ms, loss, card_mid = timed(run, args.steps, args.warmup, world, dev,
                                                     sample=lambda: card_state(dev))
+    peak_gib = torch.cuda.max_memory_allocated(dev) / 2 ** 30  # caching-allocator peak over warmup + timed steps
     ms_per_step = 1000.0 * wall / args.steps
     imgs_per_s = args.batch * world * args.steps / wall
     final_loss = float(loss.item())
@@ -417,12 +419,14 @@ def main():
             if world > 1 and not dp:
                 continue
             m2, _, run2, _, _ = build_step(name, batch, args.size, loss_name, dev, rank, world, args)
+            torch.cuda.reset_peak_memory_stats(dev)
             w2, med2, _, _, _ = timed(run2, args.steps, args.warmup, world, dev)
+            peak2 = torch.cuda.max_memory_allocated(dev) / 2 ** 30
             ips = batch * world * args.steps / w2
             configs[tag] = {"workload": f"{name} {args.size}x{args.size}, per-GPU batch {batch}, "
                                         f"{loss_name}{' + ce' if name == 'multitask_unet' else ''} + Adam",
                             "value": round(ips, 2), "unit": "images/s", "ms_per_step": round(1000.0 * w2 / args.steps, 3),
-                            "median_gpu_ms_per_step": round(med2, 3),
+                            "median_gpu_ms_per_step": round(med2, 3), "peak_alloc_gib": round(peak2, 2),
                             "step_mfma_frac": round(ips / world * GFLOP_PER_IMG[name] / 1e3 / PEAK_BF16_TFLOPS, 4)}
             del m2, run2
             gc.collect()
@@ -452,6 +456,7 @@ def main():
             "step_tflops_per_gpu": round(step_tflops, 2),
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 3),
             "median_gpu_ms_per_step": round(median_ms, 3), "final_loss": round(final_loss, 5),
+            "peak_alloc_gib": round(peak_gib, 2),
             "hip_graph": use_graph, "overlap_adam": overlap, "params_in_sync": in_sync,
             "grad_reduce_dtype": ("bf16" if args.ddp_bf16 else "fp32") if world > 1 else None,
             "configs": configs, "card": card,

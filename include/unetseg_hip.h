@@ -82,22 +82,6 @@ int unetseg_conv2d_fwd_head_ok(int dtype, int ldc1, int n, int h, int w, int ldy
 int unetseg_conv2d_fwd_head(int dtype, const void* x1, int ldc1, int n, int h, int w, const void* wk,
                             const float* bias, void* y, int ldy, int head_k, const float* head_w, const float* head_b,
                             float* logits, void* stream);
-/* unetseg_conv2d_fwd_head that also stores y's ReLU mask bits (mbits[pixel][8], the unetseg_conv2d_fwd_mask
- * layout): the head backward then need not store its input gradient (unetseg_pw_small_bwd_relu with
- * dx == NULL) -- this conv's data / weight gradients synthesise it (unetseg_conv2d_dgrad_post_syn,
- * unetseg_conv2d_wgrad_syn).  Replaces model/unet_resnet.py:77-79 up_conv[3..4] + final as
- * unetseg_conv2d_fwd_head does. */
-int unetseg_conv2d_fwd_head_mask(int dtype, const void* x1, int ldc1, int n, int h, int w, const void* wk,
-                                 const float* bias, void* y, int ldy, int head_k, const float* head_w,
-                                 const float* head_b, float* logits, unsigned char* mbits, void* stream);
-/* unetseg_conv2d_fwd_mask whose input is bilinear-x2(src) (model/unet_resnet.py:21,90-97 up_conv:
- * UpsamplingBilinear2d(2) -> Conv2d(64, 64, 3) -> ReLU): each input halo tile is blended from the source
- * by the conv itself, bit for bit as unetseg_upsample2x_fwd, and the upsampled tensor is never stored.
- * src NHWC [n][h/2][w/2][64] (pixel stride ld_src); h, w = the conv's grid; align = align_corners.
- * y == NULL: returns 1 when the shape has this kernel, else 0 (nothing launched). */
-int unetseg_conv2d_fwd_up_mask(int dtype, const void* src, int ld_src, int n, int h, int w, int align,
-                               const void* wk, const float* bias, void* y, int ldy, unsigned char* mbits,
-                               void* stream);
 /* The decoder's 512^2 up_conv conv1 (3x3, 64 -> 64, stride 1, pad 1, bias + ReLU; model/unet_resnet.py:
  * 90-97): y as unetseg_conv2d_fwd, plus the ReLU mask of the stored y packed to bits, mbits[pixel][8]
  * (bit e of byte b = y[pixel][8b + e] > 0), which its consumer's data gradient reads (post 4 of
@@ -148,14 +132,6 @@ int unetseg_conv2d_dgrad_post(int dtype, const void* dy, int ldy, int n, int p, 
                               int cin, int r, int s, int stride, int pad, void* dx, int ldx, int h, int w, int post,
                               const void* aux, int ld_aux, const float* psc, const float* psh, const float* pmean,
                               const float* pinv, float* part, int rows, void* stream);
-/* Data gradient (post 4, mask = its input's ReLU bits `mbits`) of the head's producer conv (3x3, 64 -> 64,
-   stride 1, pad 1) whose input gradient is synthesised instead of read: dY[pix][c] = bf16(bit c of
-   head_mbits[pix] ? sum_k dl[n][k][pix] * head_w[k][c] : 0), the dx unetseg_pw_small_bwd_relu would
-   store (dl fp32 planar [n][head_k][p*q], head_w fp32 [head_k][64]).  The reference's autograd of
-   model/unet_resnet.py:77-79 (final <- ReLU <- up_conv[3]).  part == NULL: rows, or -1 (no halo path). */
-int unetseg_conv2d_dgrad_post_syn(int dtype, const float* dl, int head_k, const float* head_w,
-                                  const unsigned char* head_mbits, int n, int p, int q, const void* wt, void* dx,
-                                  int ldx, const unsigned char* mbits, float* part, int rows, void* stream);
 /* 1x1 stride-1 data gradient accumulated onto the other consumers' gradient already in dx (pixel stride
    ldx >= cin, a multiple of 8: dx may be a channel slice of a skip-concat gradient), with the residual
    BN-add-ReLU backward's first pass in its epilogue (model/resnet_backbone.py:88,110-113: the next
@@ -173,16 +149,6 @@ size_t unetseg_conv2d_wgrad_workspace(int dtype, int n, int p, int q, int cout, 
 int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h,
                          int w, const void* dy, int ldy, int cout, int r, int s, int stride, int pad, float* ws,
                          size_t ws_bytes, float* dw, int dw_c, int accumulate, void* stream);
-/* weight gradient of the unetseg_conv2d_fwd_up_mask conv: X = bilinear-x2(src) blended per tile as in
-   the forward; dy NHWC [n][h][w][cout] (pixel stride ldy); dw fp32 [cout][64][3][3] (+)=; ws of
-   unetseg_conv2d_wgrad_workspace(dtype, n, h, w, cout, 64, 3, 3) */
-int unetseg_conv2d_wgrad_up(int dtype, const void* src, int ld_src, int n, int h, int w, int align, const void* dy,
-                            int ldy, int cout, float* ws, size_t ws_bytes, float* dw, int accumulate, void* stream);
-/* weight gradient of the unetseg_conv2d_dgrad_post_syn conv with the same synthesised dY: x1 NHWC
-   [n,h,w,64] (pixel stride ldc1), dw fp32 [64][64][3][3] (+)=; ws of unetseg_conv2d_wgrad_workspace */
-int unetseg_conv2d_wgrad_syn(int dtype, const void* x1, int ldc1, int n, int h, int w, const float* dl, int head_k,
-                             const float* head_w, const unsigned char* head_mbits, float* ws, size_t ws_bytes,
-                             float* dw, int accumulate, void* stream);
 
 /* ---- ResNet stem on the fast kernels (model/resnet_backbone.py:126-131, conv 7x7/s2/p3) -------
    xp: width-padded bf16 [n][h][w+8][8] from unetseg_pack_input_stem (image column at +3);
@@ -310,9 +276,7 @@ int unetseg_pw_small_bwd(int dtype, const float* dy, const void* x, int ldx, lon
                          const float* w, void* dx, int lddx, int dx_acc, float* part_w, float* part_b, void* stream);
 /* pw_small_bwd with the producer ReLU's backward fused (x = ReLU output, sole consumer; bf16):
  * dx = (x > 0) ? dy.W : 0; part_d [G][2][c], slot 0 = column sums of dx (replaces the
- * reference autograd's ReLU backward + conv bias grad of up_conv's last conv, model/unet_resnet.py:70-78,100-103).
- * dx == NULL: dx is not stored (the producer conv's gradients synthesise it: unetseg_conv2d_dgrad_post_syn,
- * unetseg_conv2d_wgrad_syn); the partials are unchanged. */
+ * reference autograd's ReLU backward + conv bias grad of up_conv's last conv, model/unet_resnet.py:70-78,100-103). */
 int unetseg_pw_small_bwd_relu(int dtype, const float* dy, const void* x, int ldx, long M, int hw, int c, int k,
                               const float* w, void* dx, int lddx, float* part_w, float* part_b, float* part_d,
                               void* stream);

@@ -144,33 +144,6 @@ static void argument_checks() {
     refused(unetseg_conv2d_dgrad_post(1, D, 64, 2, 32, 32, D, 64, 64, 3, 3, 1, 1, D, 64, 32, 32, 2, D, 64, nullptr,
                                       DF, DF, DF, DF, rows, nullptr), "dgrad_post BN without coefficients");
   }
-  // the head producer's synthesised-gradient entry points
-  {
-    unsigned char* const UB = static_cast<unsigned char*>(D);
-    refused(unetseg_conv2d_fwd_head_mask(1, D, 64, 1, 8, 32, D, DF, D, 64, 1, DF, DF, DF, nullptr, nullptr),
-            "fwd_head_mask null mbits");
-    refused(unetseg_conv2d_fwd_head_mask(1, D, 64, 1, 8, 32, D, DF, D, 64, 3, DF, DF, DF, UB, nullptr),
-            "fwd_head_mask k=3");
-    const int rows = unetseg_conv2d_dgrad_post_syn(1, nullptr, 1, nullptr, nullptr, 2, 32, 32, nullptr, nullptr, 64,
-                                                   nullptr, nullptr, 0, nullptr);
-    EXPECT(rows > 0, "dgrad_post_syn rows query %d", rows);
-    EXPECT(unetseg_conv2d_dgrad_post_syn(1, nullptr, 3, nullptr, nullptr, 2, 32, 32, nullptr, nullptr, 64, nullptr,
-                                         nullptr, 0, nullptr) == -1, "dgrad_post_syn k=3 has no path");
-    EXPECT(unetseg_conv2d_dgrad_post_syn(0, nullptr, 1, nullptr, nullptr, 2, 32, 32, nullptr, nullptr, 64, nullptr,
-                                         nullptr, 0, nullptr) == -1, "dgrad_post_syn fp32 has no path");
-    refused(unetseg_conv2d_dgrad_post_syn(1, DF, 1, DF, UB, 2, 32, 32, D, D, 64, UB, DF, rows + 1, nullptr),
-            "dgrad_post_syn wrong rows");
-    refused(unetseg_conv2d_dgrad_post_syn(1, DF, 1, DF, UB, 2, 32, 32, D, D, 64, nullptr, DF, rows, nullptr),
-            "dgrad_post_syn null mask bits");
-    refused(unetseg_conv2d_wgrad_syn(1, D, 64, 2, 32, 32, DF, 3, DF, UB, DF, 1 << 30, DF, 0, nullptr),
-            "wgrad_syn k=3");
-    refused(unetseg_conv2d_wgrad_syn(1, D, 64, 16, 128, 128, DF, 1, DF, UB, DF, 1, DF, 0, nullptr),
-            "wgrad_syn workspace too small");
-    refused(unetseg_conv2d_wgrad_syn(1, D, 64, 2, 32, 32, nullptr, 1, DF, UB, DF, 1 << 30, DF, 0, nullptr),
-            "wgrad_syn null dl");
-    refused(unetseg_conv2d_wgrad_syn(1, D, 64, 2, 30, 32, DF, 1, DF, UB, DF, 1 << 30, DF, 0, nullptr),
-            "wgrad_syn no halo path");
-  }
   refused(unetseg_conv2d_wgrad(1, D, 64, 64, nullptr, 0, 0, 1, 8, 8, D, 64, 64, 3, 3, 1, 1, DF, 0, nullptr, 64, 0,
                                nullptr), "wgrad null dw");
   refused(unetseg_conv2d_wgrad(1, D, 64, 64, nullptr, 0, 0, 16, 128, 128, D, 64, 64, 3, 3, 1, 1, DF, 1, DF, 64, 0,

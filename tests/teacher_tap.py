@@ -116,8 +116,7 @@ class Recorder:
         info = dict(info)
         if is_node:
             m["need_grad"] = out.need_grad
-            # a lazy node may have no tensor at all (ops.up_conv's upsampled input): its dtype rides in info
-            m["bf16"] = (out.data.dtype if out.data is not None else info.get("dtype")) == torch.bfloat16
+            m["bf16"] = out.data.dtype == torch.bfloat16
             m["lazy"] = bool(info.get("lazy"))
             if not m["lazy"]:
                 self.stored[o] = out.data.detach().clone()
@@ -262,12 +261,6 @@ def check_segment(rec, k, weights, hip_grads, emu=True, dt=F64):
             y = F.max_pool2d(xs[0], info["k"], info["s"], 0, ceil_mode=info["ceil_mode"])
         elif kind == "resize":
             y = F.interpolate(xs[0], size=info["size"], mode="bilinear", align_corners=info["align_corners"])
-            if m["lazy"]:
-                # never stored (ops.up_conv): the consuming conv blends it in bf16 from the source; its
-                # data gradient stores this node's gradient in bf16
-                y = _bf16_value(y)
-                vals[o] = _RoundGrad.apply(y) if emu else y
-                continue
         elif kind == "pad":
             x = xs[0]
             oh, ow = info["size"]

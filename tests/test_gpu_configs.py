@@ -228,16 +228,6 @@ def covered_keys():
     # ReLU-bit data gradients (dgrad_post4): tests/test_gpu_relu_bits.py's shapes
     for N, H, W in RELU_BITS_SHAPES:
         keys.update(introspect.call_configs(("dgrad_post4", N, H, W, 64, 0, 64, 3, 3, 1, 1, 64, 0)))
-    # the head producer's synthesised-gradient dgrad / wgrad: tests/test_gpu_head_syn.py's shapes
-    from test_gpu_head_syn import HEAD_SYN_SHAPES
-    for N, H, W, _ in HEAD_SYN_SHAPES:
-        for d in ("dgrad_syn", "wgrad_syn"):
-            keys.update(k for k in introspect.call_configs((d, N, H, W, 64, 0, 64, 3, 3, 1, 1, 64, 0)) if k)
-    # the conv blending its upsampled input: tests/test_gpu_up_conv.py's shapes
-    from test_gpu_up_conv import UP_SHAPES
-    for N, H, W, _ in UP_SHAPES:
-        for d in ("fwd_up", "wgrad_up"):
-            keys.update(k for k in introspect.call_configs((d, N, H, W, 64, 0, 64, 3, 3, 1, 1, 64, 0)) if k)
     for direction, shape, _ in HALO_CASES.values():
         keys.update(_key_list(direction, shape))
     for direction, shape, expect in CASES.values():

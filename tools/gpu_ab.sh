@@ -12,7 +12,7 @@ for i in $(seq 1 ${NB:-3}); do
     E="${v//+/ }"
     [ "$E" = "-" ] && E=""
     env $E timeout -k 10 300 python bench.py --cpu-baseline 0 --probe 0 --card-probe 0 --extra-configs $ex $BENCH_ARGS 2>/dev/null | tail -1 | \
-      python -c "import json,sys; d=json.load(sys.stdin); c=d.get('configs',{}); print('$k', d['value'], d['median_gpu_ms_per_step'], ' '.join(f'{t}={v[\"value\"]}' for t,v in c.items()), '[$v]')" || exit 1
+      python -c "import json,sys; d=json.load(sys.stdin); c=d.get('configs',{}); print('$k', d['value'], d['median_gpu_ms_per_step'], d.get('peak_alloc_gib'), ' '.join(f'{t}={v[\"value\"]}/{v.get(\"peak_alloc_gib\")}' for t,v in c.items()), '[$v]')" || exit 1
     k=$((k+1))
   done
 done

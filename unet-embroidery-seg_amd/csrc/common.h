@@ -116,8 +116,8 @@ __device__ __forceinline__ void up_src(int d, int in, int out, int align, int& i
   i1 = i0 + 1 < in ? i0 + 1 : in - 1;
   l1 = src - (float)i0;
 }
-// the blend of the four source values, as explicit products / fmas: the upsample kernel and the halo
-// conv that upsamples its input tile on the fly (kEpiUp) produce the same bits
+// the blend of the four source values, as explicit products / fmas (no contraction choice left to the
+// compiler: any kernel that recomputes an upsampled value gets the stored bits)
 __device__ __forceinline__ float up_blend(float a, float b, float c, float d, float wl0, float lw, float hl0,
                                           float lh) {
   const float t0 = fmaf(lw, b, wl0 * a), t1 = fmaf(lw, d, wl0 * c);

@@ -962,50 +962,6 @@ UNETSEG_API int unetseg_conv2d_fwd_mask(int dtype, const void* x1, int ldc1, int
   return 0;
 }
 
-// unetseg_conv2d_fwd_head that also stores the ReLU mask of y as bits (mbits[pixel][8], the
-// unetseg_conv2d_fwd_mask layout): with them the head backward need not store its input gradient --
-// the conv's data and weight gradients synthesise it (unetseg_conv2d_dgrad_post_syn / _wgrad_syn).
-UNETSEG_API int unetseg_conv2d_fwd_head_mask(int dtype, const void* x1, int ldc1, int n, int h, int w, const void* wk,
-                                             const float* bias, void* y, int ldy, int head_k, const float* head_w,
-                                             const float* head_b, float* logits, unsigned char* mbits,
-                                             void* stream) {
-  US_CHECK_ARG(x1 && wk && bias && y && head_w && head_b && logits && mbits, "conv2d_fwd_head_mask: null pointer");
-  US_CHECK_ARG(unetseg_conv2d_fwd_head_ok(dtype, ldc1, n, h, w, ldy, head_k) && ldy % 8 == 0,
-               "conv2d_fwd_head_mask: needs bf16, 64 -> 64 channels on the halo path and head_k 1 or 2");
-  FastTNArgs f;
-  head_args(x1, ldc1, n, h, w, wk, ldy, f);
-  f.y = y; f.bias = bias; f.relu = 1;
-  f.head_w = head_w; f.head_b = head_b; f.head_y = logits; f.head_k = head_k;
-  f.mbits_out = mbits;
-  US_CHECK_ARG(launch_halo3(f, (hipStream_t)stream) == 0, "conv2d_fwd_head_mask: launch refused");
-  US_LAUNCH_CHECK("conv2d_fwd_head_mask");
-  return 0;
-}
-
-// unetseg_conv2d_fwd_mask whose input is the bilinear x2 upsample of src (the decoder's up_conv,
-// model/unet_resnet.py:21,90-97: UpsamplingBilinear2d(2) -> Conv2d(64, 64, 3) -> ReLU): the conv
-// blends each input halo tile from the four source pixels itself (the arithmetic of
-// unetseg_upsample2x_fwd, bit for bit) so the full-resolution upsampled tensor is never stored.
-// src NHWC [n][h/2][w/2][64] (pixel stride ld_src); h, w = the conv's (upsampled) grid; align = the
-// upsample's align_corners.  y == NULL: returns 1 when the shape has this kernel, else 0.
-UNETSEG_API int unetseg_conv2d_fwd_up_mask(int dtype, const void* src, int ld_src, int n, int h, int w, int align,
-                                           const void* wk, const float* bias, void* y, int ldy, unsigned char* mbits,
-                                           void* stream) {
-  FastTNArgs f;
-  const long src_bytes = (long)n * (h / 2) * (w / 2) * ld_src * 2;
-  const bool ok = dtype == DT_BF16 && (align == 0 || align == 1) && n > 0 && h > 0 && w > 0 && h % 2 == 0 &&
-                  w % 2 == 0 && ld_src >= 64 && ld_src % 8 == 0 && ldy >= 64 && ldy % 8 == 0 &&
-                  src_bytes < (1L << 31) && head_args(kSomePtr, 64, n, h, w, wk ? wk : kSomePtr, ldy, f);
-  if (!y) return ok ? 1 : 0;
-  US_CHECK_ARG(ok, "conv2d_fwd_up_mask: needs bf16, 64 -> 64 channels on the halo path and an even grid");
-  US_CHECK_ARG(src && wk && bias && mbits, "conv2d_fwd_up_mask: null pointer");
-  f.x1 = src; f.x1_bytes = (unsigned)src_bytes; f.ldc1b = ld_src * 2; f.up = align ? 1 : 2;
-  f.y = y; f.bias = bias; f.relu = 1; f.mbits_out = mbits;
-  US_CHECK_ARG(launch_halo3(f, (hipStream_t)stream) == 0, "conv2d_fwd_up_mask: launch refused");
-  US_LAUNCH_CHECK("conv2d_fwd_up_mask");
-  return 0;
-}
-
 // Weight gradient of that conv: X = relu(x1 * in_sc + in_sh) staged on the fly (fast bf16 wgrad),
 // then the usual deterministic split-K reduce into dw (fp32 [cout][dw_c], (+)= with accumulate).
 UNETSEG_API int unetseg_conv2d_wgrad_bnrelu_in(int dtype, const void* x1, int c1, int ldc1, int n, int h, int w,
@@ -1224,38 +1180,6 @@ UNETSEG_API int unetseg_conv2d_dgrad_post(int dtype, const void* dy, int ldy, in
   return 0;
 }
 
-// Data gradient of the head's producer conv (3x3, 64 -> 64, stride 1, pad 1, bias + ReLU: up_conv's
-// last conv, model/unet_resnet.py:77-79) with post 4 (mask = its input's ReLU bits, mbits of
-// unetseg_conv2d_fwd_mask) and its input gradient SYNTHESISED, never stored: dY[pix][c] =
-// bf16(bit c of head_mbits[pix] ? sum_k dl[n][k][pix] * head_w[k][c] : 0) -- exactly the dx
-// unetseg_pw_small_bwd_relu would have written (dl: fp32 planar [n][head_k][p*q] logit gradient,
-// head_w fp32 [head_k][64], head_mbits of unetseg_conv2d_fwd_head_mask).  part / rows as
-// unetseg_conv2d_dgrad_post; part == NULL: returns rows, or -1 when the shape has no halo kernel.
-UNETSEG_API int unetseg_conv2d_dgrad_post_syn(int dtype, const float* dl, int head_k, const float* head_w,
-                                              const unsigned char* head_mbits, int n, int p, int q, const void* wt,
-                                              void* dx, int ldx, const unsigned char* mbits, float* part, int rows,
-                                              void* stream) {
-  if (dtype != DT_BF16 || (head_k != 1 && head_k != 2) || n <= 0 || ldx < 64 || ldx % 8) return -1;
-  IgemmArgs a;
-  if (!dgrad_classes(dl ? (const void*)dl : kSomePtr, 64, n, p, q, wt ? wt : kSomePtr, 64, 64, 3, 3, 1, 1,
-                     dx ? dx : const_cast<void*>(kSomePtr), ldx, p, q, 0, 0, a) || a.M <= 0)
-    return -1;
-  FastTNArgs f;
-  if (!fast_tn_args(a, f)) return -1;
-  f.post = 4;
-  if (tn_fast_config(f, nullptr) != 0) return -1;
-  const int total = tn_fast_post_rows(f);
-  if (!part) return total;
-  US_CHECK_ARG(dl && head_w && head_mbits && wt && dx && mbits, "conv2d_dgrad_post_syn: null pointer");
-  US_CHECK_ARG(rows == total, "conv2d_dgrad_post_syn: rows %d != %d", rows, total);
-  f.x1_bytes = 0;  // the input is synthesised: no DMA reads it
-  f.aux = mbits; f.mbits = mbits; f.ppart = part;
-  f.syn_dl = dl; f.syn_w = head_w; f.syn_mb = head_mbits; f.syn_k = head_k;
-  US_CHECK_ARG(launch_halo3(f, (hipStream_t)stream) == 0, "conv2d_dgrad_post_syn: launch refused");
-  US_LAUNCH_CHECK("conv2d_dgrad_post_syn");
-  return 0;
-}
-
 // Data gradient of a 1x1 stride-1 conv accumulated onto the residual gradient already in dx, with the
 // residual-BN backward's first pass in the epilogue (post 3, conv_fast.h): dx = mask * bf16(dgrad + dx),
 // mask = the block output's packed ReLU bits (unetseg_bn_apply_mask), part[tile][2 or 3][cin] = sum d,
@@ -1442,57 +1366,6 @@ UNETSEG_API int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1
   }
   US_CHECK_ARG(dw_c > 0 && dw_c <= a.cin, "conv2d_wgrad: bad dw_c");
   launch_wgrad_reduce(ws, splits, cout, a.cin, r * s, dw, dw_c, accumulate, st);
-  US_LAUNCH_CHECK("wgrad_reduce");
-  return 0;
-}
-
-// Weight gradient of the same conv with dY synthesised as in unetseg_conv2d_dgrad_post_syn: x1 NHWC
-// [n,h,w,64] (pixel stride ldc1), dw fp32 [64][64][3][3] (+)= with accumulate; ws as unetseg_conv2d_wgrad
-// (unetseg_conv2d_wgrad_workspace of the same shape).  Halo path only (-1 refused otherwise).
-UNETSEG_API int unetseg_conv2d_wgrad_syn(int dtype, const void* x1, int ldc1, int n, int h, int w, const float* dl,
-                                         int head_k, const float* head_w, const unsigned char* head_mbits,
-                                         float* ws, size_t ws_bytes, float* dw, int accumulate, void* stream) {
-  US_CHECK_ARG(x1 && dl && head_w && head_mbits && ws && dw, "conv2d_wgrad_syn: null pointer");
-  US_CHECK_ARG(head_k == 1 || head_k == 2, "conv2d_wgrad_syn: head_k must be 1 or 2");
-  HaloWgradArgs hw{};
-  US_CHECK_ARG(n > 0 && ldc1 >= 64 && ldc1 % 8 == 0 && halo_wgrad_args(dtype, 64, 64, n, h, w, 64, 3, 3, h, w, hw),
-               "conv2d_wgrad_syn: needs bf16, 64 -> 64 channels on the halo path");
-  const long b1 = (long)n * h * w * ldc1 * 2;
-  US_CHECK_ARG(b1 < (1L << 31), "conv2d_wgrad_syn: input too large");
-  hw.x1 = x1; hw.x2 = nullptr; hw.x1_bytes = (unsigned)b1; hw.x2_bytes = 0; hw.ldc1b = ldc1 * 2; hw.ldc2b = 0;
-  hw.dy = nullptr; hw.dy_bytes = 0; hw.ldyb = 128; hw.ws = ws;
-  hw.syn_dl = dl; hw.syn_w = head_w; hw.syn_mb = head_mbits; hw.syn_k = head_k;
-  const int splits = halo3_wgrad_splits(hw);
-  US_CHECK_ARG(ws_bytes >= (size_t)splits * 64 * 9 * 64 * sizeof(float), "conv2d_wgrad_syn: workspace too small");
-  hipStream_t st = (hipStream_t)stream;
-  US_CHECK_ARG(launch_halo3_wgrad(hw, splits, st) == 0, "conv2d_wgrad_syn: launch refused");
-  US_LAUNCH_CHECK("halo3_wgrad_syn");
-  launch_wgrad_reduce(ws, splits, 64, 64, 9, dw, 64, accumulate, st);
-  US_LAUNCH_CHECK("wgrad_reduce");
-  return 0;
-}
-
-// Weight gradient of the unetseg_conv2d_fwd_up_mask conv: X = upsample2x(src) blended per halo tile
-// as in the forward; dy NHWC [n][h][w][cout] (pixel stride ldy), dw fp32 [cout][64][3][3] (+)=; ws of
-// unetseg_conv2d_wgrad_workspace(dtype, n, h, w, cout, 64, 3, 3).
-UNETSEG_API int unetseg_conv2d_wgrad_up(int dtype, const void* src, int ld_src, int n, int h, int w, int align,
-                                        const void* dy, int ldy, int cout, float* ws, size_t ws_bytes, float* dw,
-                                        int accumulate, void* stream) {
-  US_CHECK_ARG(src && dy && ws && dw, "conv2d_wgrad_up: null pointer");
-  HaloWgradArgs hw{};
-  const long src_bytes = (long)n * (h / 2) * (w / 2) * ld_src * 2, dy_bytes = (long)n * h * w * ldy * 2;
-  US_CHECK_ARG((align == 0 || align == 1) && n > 0 && h % 2 == 0 && w % 2 == 0 && ld_src >= 64 && ld_src % 8 == 0 &&
-                   ldy >= cout && ldy % 8 == 0 && src_bytes < (1L << 31) && dy_bytes < (1L << 31) &&
-                   halo_wgrad_args(dtype, 64, 64, n, h, w, cout, 3, 3, h, w, hw),
-               "conv2d_wgrad_up: needs bf16, 64 input channels on the halo path and an even grid");
-  hw.x1 = src; hw.x2 = nullptr; hw.x1_bytes = (unsigned)src_bytes; hw.x2_bytes = 0; hw.ldc1b = ld_src * 2; hw.ldc2b = 0;
-  hw.dy = dy; hw.dy_bytes = (unsigned)dy_bytes; hw.ldyb = ldy * 2; hw.ws = ws; hw.up = align ? 1 : 2;
-  const int splits = halo3_wgrad_splits(hw);
-  US_CHECK_ARG(ws_bytes >= (size_t)splits * cout * 9 * 64 * sizeof(float), "conv2d_wgrad_up: workspace too small");
-  hipStream_t st = (hipStream_t)stream;
-  US_CHECK_ARG(launch_halo3_wgrad(hw, splits, st) == 0, "conv2d_wgrad_up: launch refused");
-  US_LAUNCH_CHECK("halo3_wgrad_up");
-  launch_wgrad_reduce(ws, splits, cout, 64, 9, dw, 64, accumulate, st);
   US_LAUNCH_CHECK("wgrad_reduce");
   return 0;
 }

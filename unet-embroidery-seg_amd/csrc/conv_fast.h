@@ -71,19 +71,6 @@ struct FastTNArgs {
   // halo forward with bias + ReLU: also store the output's ReLU mask as bits, [M][Ng/8] (bit e of byte
   // b = channel 8b + e > 0); post 4 = post 1 with the mask read from such bits (mbits, halo path only)
   unsigned char* mbits_out;
-  // synthesised input (halo dgrad with post 4 only): the dgrad's input gradient dY is never stored --
-  // it is the backward of the model's 1x1 head through the ReLU of the conv this dgrad belongs to:
-  // dY[pix][c] = bf16(bit c of syn_mb[pix] ? sum_k syn_dl[n][k][pix] * syn_w[k][c] : 0)
-  // (pw_small_bwd_kernel's dx, bit for bit); syn_dl fp32 planar [N][syn_k][H*W], syn_w fp32
-  // [syn_k][64], syn_mb the head input's ReLU bits [pix][8] (kEpiMask layout)
-  const float* syn_dl;
-  const float* syn_w;
-  const unsigned char* syn_mb;
-  int syn_k;
-  // input upsampled on the fly (halo forward, kEpiUp): x1 is the half-resolution source [N][H/2][W/2]
-  // (pixel stride ldc1b) of a bilinear x2 upsample, 1 = align_corners=True, 2 = False; the conv reads
-  // bf16(upsample(x1)) exactly as unetseg_upsample2x_fwd stores it
-  int up;
 };
 
 struct FastWgradArgs {
@@ -115,13 +102,6 @@ struct HaloWgradArgs {
   unsigned dy_bytes;
   int ldyb, Cout;
   float* ws;
-  // synthesised dY (Cout == 64, dy unused): as FastTNArgs::syn_*
-  const float* syn_dl;
-  const float* syn_w;
-  const unsigned char* syn_mb;
-  int syn_k;
-  // X upsampled on the fly from x1 = the half-resolution source (cin == c1 == 64): as FastTNArgs::up
-  int up;
 };
 
 // kernel-configuration codes reported by the unetseg_conv2d_*_config queries (include/unetseg_hip.h)

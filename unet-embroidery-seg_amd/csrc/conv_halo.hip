@@ -41,59 +41,8 @@ __device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, unsigned off,
 // not read back by a separate head pass.
 // kEpiMask: the ReLU mask of the stored output packed to bits, mbits_out[pixel][Ng/8] (bit e of byte b =
 // channel 8b + e > 0) -- the consumer's data gradient (post 4) reads 1/16 of what the activation costs.
-// kEpiSyn (data gradient with post 4 only): the input dY is synthesised from the head's logit
-// gradient, weights and the head input's ReLU bits (FastTNArgs::syn_*) instead of being DMA'd.
 constexpr int kEpiBias = 1, kEpiRelu = 2, kEpiStats = 4, kEpiAcc = 8, kEpiDyn = 16, kEpiHead1 = 32, kEpiHead2 = 64,
-              kEpiMask = 128, kEpiSyn = 256, kEpiUp = 512;
-
-// kEpiUp: the input tile is the bilinear x2 upsample of the half-resolution x1 (FastTNArgs::up),
-// computed per halo chunk from the four source pixels (up_src / up_blend, as unetseg_upsample2x_fwd)
-// and written to LDS by the waves: the full-resolution upsampled tensor is never stored.
-// Lane slot i of a stage = halo pixel idx >> 3, 16-B chunk lane & 7 (as the DMA slots); one slot's
-// four source chunks, loaded a tile ahead, and its blend weights:
-struct UpSlot {
-  uint4 v[4];
-  float lw, lh;
-};
-__device__ __forceinline__ void up_slot_load(UpSlot& u, const bf16* src, long ld, int nb, int hs, int ws, int H, int W,
-                                             int h, int w, bool ok, int align, int chunk) {
-  int h0, h1, w0, w1;
-  up_src(ok ? h : 0, hs, H, align, h0, h1, u.lh);
-  up_src(ok ? w : 0, ws, W, align, w0, w1, u.lw);
-  const bf16* r0 = src + (long)(nb * hs + h0) * ws * ld + chunk * 8;
-  const bf16* r1 = src + (long)(nb * hs + h1) * ws * ld + chunk * 8;
-  const uint4 z = uint4{0u, 0u, 0u, 0u};
-  u.v[0] = ok ? *reinterpret_cast<const uint4*>(r0 + (long)w0 * ld) : z;
-  u.v[1] = ok ? *reinterpret_cast<const uint4*>(r0 + (long)w1 * ld) : z;
-  u.v[2] = ok ? *reinterpret_cast<const uint4*>(r1 + (long)w0 * ld) : z;
-  u.v[3] = ok ? *reinterpret_cast<const uint4*>(r1 + (long)w1 * ld) : z;
-}
-__device__ __forceinline__ uint4 up_slot_chunk(const UpSlot& u) {
-  const bf16* a = reinterpret_cast<const bf16*>(&u.v[0]);
-  const bf16* b = reinterpret_cast<const bf16*>(&u.v[1]);
-  const bf16* c = reinterpret_cast<const bf16*>(&u.v[2]);
-  const bf16* d = reinterpret_cast<const bf16*>(&u.v[3]);
-  const float wl0 = 1.f - u.lw, hl0 = 1.f - u.lh;
-  bf16 o[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e)
-    o[e] = (bf16)up_blend((float)a[e], (float)b[e], (float)c[e], (float)d[e], wl0, u.lw, hl0, u.lh);
-  return *reinterpret_cast<uint4*>(o);
-}
-
-// One 16-B chunk (8 channels) of the head backward's input gradient, as pw_small_bwd_kernel<MASK>
-// stores it: bf16(mask ? g0 * w0 [+ g1 * w1] : 0) (explicit product / fma: the same float operations
-// in both kernels, so the synthesised operand equals the stored one bit for bit).
-__device__ __forceinline__ uint4 syn_chunk(float g0, float g1, int hk, const float (&w)[2][8], unsigned bits) {
-  bf16 o[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    float s = g0 * w[0][e];
-    if (hk == 2) s = fmaf(g1, w[1][e], s);
-    o[e] = ((bits >> e) & 1u) ? (bf16)s : (bf16)0.f;
-  }
-  return *reinterpret_cast<uint4*>(o);
-}
+              kEpiMask = 128;
 
 __device__ __forceinline__ void bstore32(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
   asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
@@ -110,11 +59,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   constexpr int HK = (EPI & kEpiHead2) ? 2 : (EPI & kEpiHead1) ? 1 : 0;  // fused head logits
   static_assert(HK == 0 || (!kDyn && POST == 0), "the fused head rides on a fixed bias + ReLU epilogue");
   constexpr bool kMask = (EPI & kEpiMask) != 0;
-  static_assert(!kMask || (!kDyn && POST == 0 && (EPI & kEpiRelu)), "mask bits of a ReLU output");
-  constexpr bool kSyn = (EPI & kEpiSyn) != 0;
-  static_assert(!kSyn || (POST == 4 && EPI == kEpiSyn), "synthesised input: plain post-4 data gradient");
-  constexpr bool kUp = (EPI & kEpiUp) != 0;
-  static_assert(!kUp || (POST == 0 && !kDyn), "upsampled input: a forward epilogue");
+  static_assert(!kMask || (!kDyn && POST == 0 && HK == 0 && (EPI & kEpiRelu)), "mask bits of a ReLU output");
   // POST 4: post 1 with the ReLU mask read from packed bits (a.mbits, the kEpiMask layout)
   // wave w owns output rows [w*TH/NW, (w+1)*TH/NW)
   constexpr int RPW = TH / NW;               // rows per wave
@@ -206,76 +151,6 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     }
   };
 
-  // synthesised input (kSyn): lane slot i of a stage = halo pixel idx >> 3, chunk lane & 7 (the DMA
-  // slots' pixels); the chunk's 8 head-weight columns stay in registers.  The next tile's logit
-  // gradients and mask bytes are loaded at the top of a tile, the chunks written after its taps.
-  const int sk = kSyn ? a.syn_k : 1;
-  float swr[2][8];
-  float sg[kSyn ? HI : 1][2];
-  unsigned smb[kSyn ? HI : 1];
-  if constexpr (kSyn) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) swr[k][e] = k < sk ? a.syn_w[k * 64 + (lane & 7) * 8 + e] : 0.f;
-  }
-  const long syn_hw = (long)a.H * a.W;
-  auto syn_load = [&](int t) {
-    const int sp = slot + t * G_per;
-    const int tw = sp % tiles_w, rest = sp / tiles_w;
-    const int th = rest % tiles_h, nb = rest / tiles_h;
-#pragma unroll
-    for (int i = 0; i < (kSyn ? HI : 0); ++i) {
-      const int idx = (i * NW + wid) * 64 + lane;
-      const int hp = idx >> 3, hr = hp / (HW_TW + 2), hcol = hp % (HW_TW + 2);
-      const int h = th * TH - 1 + hr, w = tw * HW_TW - 1 + hcol;
-      const bool ok = idx < HCH && h >= 0 && h < a.H && w >= 0 && w < a.W;
-      const long q = (long)h * a.W + w;
-      smb[i] = ok ? (unsigned)a.syn_mb[((long)nb * syn_hw + q) * 8 + (lane & 7)] : 0u;
-      sg[i][0] = ok ? a.syn_dl[(long)nb * sk * syn_hw + q] : 0.f;
-      sg[i][1] = (ok && sk == 2) ? a.syn_dl[((long)nb * sk + 1) * syn_hw + q] : 0.f;
-    }
-  };
-  auto syn_store = [&](int stage) {
-#pragma unroll
-    for (int i = 0; i < (kSyn ? HI : 0); ++i) {
-      const int idx = (i * NW + wid) * 64 + lane;
-      const int hp = idx >> 3;
-      // slot (hp, s) holds chunk s ^ (hp & 7) (swzh), so chunk lane & 7 goes to slot (lane & 7) ^ (hp & 7)
-      if (idx < HCH) hl[stage * HCH + hp * 8 + ((lane & 7) ^ (hp & 7))] = syn_chunk(sg[i][0], sg[i][1], sk, swr, smb[i]);
-    }
-  };
-
-  // upsampled input (kUp): the next tile's slots in two halves (registers): the first half's source
-  // chunks are loaded at the top of a tile and written after its first taps, the second half's
-  // loaded then and written after the last tap
-  constexpr int UPH = (HI + 1) / 2;
-  UpSlot us[kUp ? UPH : 1];
-  auto up_load = [&](int t, int half) {
-    const int sp = slot + t * G_per;
-    const int tw = sp % tiles_w, rest = sp / tiles_w;
-    const int th = rest % tiles_h, nb = rest / tiles_h;
-#pragma unroll
-    for (int u = 0; u < (kUp ? UPH : 0); ++u) {
-      const int i = half * UPH + u;
-      const int idx = (i * NW + wid) * 64 + lane;
-      const int hp = idx >> 3, hr = hp / (HW_TW + 2), hcol = hp % (HW_TW + 2);
-      const int h = th * TH - 1 + hr, w = tw * HW_TW - 1 + hcol;
-      const bool ok = i < HI && idx < HCH && h >= 0 && h < a.H && w >= 0 && w < a.W;
-      up_slot_load(us[u], reinterpret_cast<const bf16*>(a.x1), a.ldc1b >> 1, nb, a.H >> 1, a.W >> 1, a.H, a.W, h, w,
-                   ok, a.up == 1, lane & 7);
-    }
-  };
-  auto up_store = [&](int stage, int half) {
-#pragma unroll
-    for (int u = 0; u < (kUp ? UPH : 0); ++u) {
-      const int i = half * UPH + u;
-      const int idx = (i * NW + wid) * 64 + lane;
-      const int hp = idx >> 3;
-      if (i < HI && idx < HCH) hl[stage * HCH + hp * 8 + ((lane & 7) ^ (hp & 7))] = up_slot_chunk(us[u]);
-    }
-  };
-
   f32x4 acc[FC][FP];
   // data-gradient post-op (a.post): running per-lane sums of the masked gradient over all tiles of
   // this block, reduced once at the end into ppart[blockIdx.x][2][Ng]
@@ -284,19 +159,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   for (int c = 0; c < FC; ++c)
 #pragma unroll
     for (int e = 0; e < 4; ++e) pq0[c][e] = pq1[c][e] = 0.f;
-  if (my_tiles > 0) {
-    if constexpr (kSyn) {
-      syn_load(0);
-      syn_store(0);
-    } else if constexpr (kUp) {
-      up_load(0, 0);
-      up_store(0, 0);
-      up_load(0, 1);
-      up_store(0, 1);
-    } else {
-      issue_halo(0, 0);
-    }
-  }
+  if (my_tiles > 0) issue_halo(0, 0);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   // halo tap offsets (uniform): jt -> (dh, dw)
@@ -320,11 +183,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
 
   for (int t = 0; t < my_tiles; ++t) {
     const int stage = t & 1;
-    if (t + 1 < my_tiles) {
-      if constexpr (kSyn) syn_load(t + 1);
-      else if constexpr (kUp) up_load(t + 1, 0);
-      else issue_halo(t + 1, stage ^ 1);
-    }
+    if (t + 1 < my_tiles) issue_halo(t + 1, stage ^ 1);
     // post-op: this tile's aux values are loaded now, so their latency hides under the tap loop
     uint2 zr[FC][FP];
     uint2 zb[FP];  // POST 4: the 8 mask bytes (64 channels) of this lane's pixel
@@ -360,11 +219,6 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     const uint4* hs = hl + stage * HCH;
 #pragma unroll
     for (int jt = 0; jt < 9; ++jt) {
-      if constexpr (kUp)
-        if (jt == 4 && t + 1 < my_tiles) {
-          up_store(stage ^ 1, 0);
-          up_load(t + 1, 1);
-        }
       const int jr = jt / 3, js = jt - jr * 3;
       const int dh = dh0 + dhs * jr, dw = dw0 + dws * js;
 #pragma unroll
@@ -392,12 +246,6 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
             acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], pf[p], acc[c][p], 0, 0, 0);
       }
     }
-
-    // the next tile's synthesised input (stage ^ 1 was last read in tile t-1, before its barrier)
-    if constexpr (kSyn)
-      if (t + 1 < my_tiles) syn_store(stage ^ 1);
-    if constexpr (kUp)
-      if (t + 1 < my_tiles) up_store(stage ^ 1, 1);
 
     // ================= epilogue =================
     const int sp = slot + t * G_per;
@@ -843,11 +691,7 @@ __global__ __launch_bounds__(64 * NW) void stem_halo_kernel(const bf16* xp, unsi
 // NW = 8: two waves per SIMD -- wave w owns input channels 16 (w % 4) .. of the 9 taps for output
 // channels 32 (w / 4) .. 32 (w / 4) + 31 (the X fragments are read by both halves; the single wave per
 // SIMD of NW = 4 left the MFMA pipe idle while its own LDS reads were in flight).
-// SYN: dY is synthesised from the head's logit gradient (HaloWgradArgs::syn_*, Cout == 64) and
-// written into the stage's dY part by the waves instead of DMA'd (halo3_kernel's kEpiSyn).
-// UPX: X is the bilinear x2 upsample of the half-resolution x1 (HaloWgradArgs::up, cin == 64),
-// blended per halo chunk by the waves (halo3_kernel's kEpiUp) instead of DMA'd.
-template <int TH, int NW, bool SYN = false, bool UPX = false>
+template <int TH, int NW>
 __global__ __launch_bounds__(64 * NW) void halo3_wgrad_kernel(HaloWgradArgs a, int tiles_w, int tiles_h, int n_sp,
                                                               int G_per) {
   constexpr int TP = TH * HW_TW;              // output pixels per tile
@@ -893,69 +737,6 @@ __global__ __launch_bounds__(64 * NW) void halo3_wgrad_kernel(HaloWgradArgs a, i
     hoff[i] = (unsigned)(hr * a.W + hc) * ldxb + xcb + (unsigned)((pc ^ swz_tr8(hp)) * 16);
     hflag[i] = idx >= HCH ? 16u : (hr == 0 ? 1u : 0u) | (hr == TH + 1 ? 2u : 0u) | (hc == 0 ? 4u : 0u) | (hc == HW_TW + 1 ? 8u : 0u);
   }
-  // SYN: lane slot i of the dY part = tile pixel idx >> 3, chunk lane & 7 (output channels 8 (lane & 7) ..)
-  const int sk = SYN ? a.syn_k : 1;
-  float swr[2][8];
-  float sg[SYN ? DI : 1][2];
-  unsigned smb[SYN ? DI : 1];
-  if constexpr (SYN) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) swr[k][e] = k < sk ? a.syn_w[k * 64 + (lane & 7) * 8 + e] : 0.f;
-  }
-  const long syn_hw = (long)a.H * a.W;
-  auto syn_load = [&](int t) {
-    const int sp = slot + t * G_per;
-    const int tw = sp % tiles_w, rest = sp / tiles_w;
-    const int th = rest % tiles_h, nb = rest / tiles_h;
-#pragma unroll
-    for (int i = 0; i < (SYN ? DI : 0); ++i) {
-      const int px = ((i * NW + wid) * 64 + lane) >> 3;
-      const long q = (long)(th * TH + px / HW_TW) * a.W + tw * HW_TW + px % HW_TW;
-      smb[i] = (unsigned)a.syn_mb[((long)nb * syn_hw + q) * 8 + (lane & 7)];
-      sg[i][0] = a.syn_dl[(long)nb * sk * syn_hw + q];
-      sg[i][1] = sk == 2 ? a.syn_dl[((long)nb * sk + 1) * syn_hw + q] : 0.f;
-    }
-  };
-  auto syn_store = [&](int stage) {
-#pragma unroll
-    for (int i = 0; i < (SYN ? DI : 0); ++i) {
-      const int px = ((i * NW + wid) * 64 + lane) >> 3;
-      // the DMA layout: slot (px, s) holds chunk s ^ swz_tr8(px)
-      lds[stage * STG + px * 8 + ((lane & 7) ^ swz_tr8(px))] = syn_chunk(sg[i][0], sg[i][1], sk, swr, smb[i]);
-    }
-  };
-  // UPX: the next tile's X slots in UPN parts (registers; the accumulators leave room for two slots),
-  // as halo3_kernel's kEpiUp: part p is loaded before row p * TH / UPN of this tile (part 0 at its top)
-  // and written at the next part's start (the last part after the rows)
-  constexpr int UPN = 6, UPH = (HI + UPN - 1) / UPN;
-  UpSlot us[UPX ? UPH : 1];
-  auto up_load = [&](int t, int half) {
-    const int sp = slot + t * G_per;
-    const int tw = sp % tiles_w, rest = sp / tiles_w;
-    const int th = rest % tiles_h, nb = rest / tiles_h;
-#pragma unroll
-    for (int u = 0; u < (UPX ? UPH : 0); ++u) {
-      const int i = half * UPH + u;
-      const int idx = (i * NW + wid) * 64 + lane;
-      const int hp = idx >> 3, hr = hp / (HW_TW + 2), hcol = hp % (HW_TW + 2);
-      const int h = th * TH - 1 + hr, w = tw * HW_TW - 1 + hcol;
-      const bool ok = i < HI && idx < HCH && h >= 0 && h < a.H && w >= 0 && w < a.W;
-      up_slot_load(us[u], reinterpret_cast<const bf16*>(a.x1), a.ldc1b >> 1, nb, a.H >> 1, a.W >> 1, a.H, a.W, h, w,
-                   ok, a.up == 1, (ct * 64 >> 3) + (lane & 7));
-    }
-  };
-  auto up_store = [&](int stage, int half) {
-#pragma unroll
-    for (int u = 0; u < (UPX ? UPH : 0); ++u) {
-      const int i = half * UPH + u;
-      const int idx = (i * NW + wid) * 64 + lane;
-      const int hp = idx >> 3;
-      // the DMA layout: slot (hp, s) of the halo part holds chunk s ^ swz_tr8(hp)
-      if (i < HI && idx < HCH) lds[stage * STG + DCH + hp * 8 + ((lane & 7) ^ swz_tr8(hp))] = up_slot_chunk(us[u]);
-    }
-  };
   auto issue = [&](int t, int stage) {
     const int sp = slot + t * G_per;
     const int tw = sp % tiles_w, rest = sp / tiles_w;
@@ -963,14 +744,8 @@ __global__ __launch_bounds__(64 * NW) void halo3_wgrad_kernel(HaloWgradArgs a, i
     const int h0 = th * TH, w0 = tw * HW_TW;
     const unsigned base = __builtin_amdgcn_readfirstlane(lds_addr(lds + stage * STG));
     const unsigned tb = __builtin_amdgcn_readfirstlane((unsigned)((nb * a.H + h0) * a.W + w0) * (unsigned)a.ldyb);
-    if constexpr (SYN) syn_load(t);
-    else
 #pragma unroll
-      for (int i = 0; i < DI; ++i) dma16(rdy, base + (unsigned)((i * NW + wid) * 1024), tb + doff[i]);
-    if constexpr (UPX) {
-      up_load(t, 0);
-      return;
-    }
+    for (int i = 0; i < DI; ++i) dma16(rdy, base + (unsigned)((i * NW + wid) * 1024), tb + doff[i]);
     const unsigned hbase = base + DCH * 16;
     // halo origin (h0 - 1, w0 - 1): wraps below zero on the first row / column, whose lanes the
     // edge mask sends out of range
@@ -991,18 +766,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_wgrad_kernel(HaloWgradArgs a, i
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (my_tiles > 0) {
-    issue(0, 0);
-    if constexpr (SYN) syn_store(0);
-    if constexpr (UPX) {
-      up_store(0, 0);
-#pragma unroll
-      for (int ph = 1; ph < UPN; ++ph) {
-        up_load(0, ph);
-        up_store(0, ph);
-      }
-    }
-  }
+  if (my_tiles > 0) issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
   typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -1037,12 +801,6 @@ __global__ __launch_bounds__(64 * NW) void halo3_wgrad_kernel(HaloWgradArgs a, i
     const char* hbase = dbase + DCH * 16;
 #pragma unroll
     for (int rr = 0; rr < TH; ++rr) {
-      if constexpr (UPX)
-        if (rr * UPN / TH != (rr - 1) * UPN / TH && rr > 0 && t + 1 < my_tiles) {  // part ph starts here
-          const int ph = rr * UPN / TH;
-          up_store(stage ^ 1, ph - 1);
-          up_load(t + 1, ph);
-        }
       bf16x8 af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) af[i] = tr2(dbase + rr * HW_TW * 128, pa[i][0], pa[i][1]);
@@ -1058,11 +816,6 @@ __global__ __launch_bounds__(64 * NW) void halo3_wgrad_kernel(HaloWgradArgs a, i
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    // the next tile's synthesised dY (stage ^ 1 was last read in tile t-1, before its barrier)
-    if constexpr (SYN)
-      if (t + 1 < my_tiles) syn_store(stage ^ 1);
-    if constexpr (UPX)
-      if (t + 1 < my_tiles) up_store(stage ^ 1, UPN - 1);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   // slab[slot][cout][tap*cin + c]
@@ -1609,21 +1362,10 @@ int launch_halo3(const FastTNArgs& a, hipStream_t st) {
   static const bool dyn = getenv("UNETSEG_HALO_EPI_DYN") != nullptr;
   const int epi = (a.bias ? kEpiBias : 0) | (a.relu ? kEpiRelu : 0) | (a.stats ? kEpiStats : 0) |
                   (a.accumulate ? kEpiAcc : 0);
-  if (a.head_y) {  // fused head: bias + ReLU epilogue only (checked by the caller), optionally mask bits
+  if (a.head_y) {  // fused head: bias + ReLU epilogue only (checked by the caller)
     if (a.post || epi != (kEpiBias | kEpiRelu) || (a.head_k != 1 && a.head_k != 2)) return -1;
-    if (a.mbits_out)
-      return a.head_k == 2 ? launch_halo3_cfg<8, 8, 0, kEpiBias | kEpiRelu | kEpiHead2 | kEpiMask>(a, st)
-                           : launch_halo3_cfg<8, 8, 0, kEpiBias | kEpiRelu | kEpiHead1 | kEpiMask>(a, st);
     return a.head_k == 2 ? launch_halo3_cfg<8, 8, 0, kEpiBias | kEpiRelu | kEpiHead2>(a, st)
                          : launch_halo3_cfg<8, 8, 0, kEpiBias | kEpiRelu | kEpiHead1>(a, st);
-  }
-  if (a.syn_dl) {  // synthesised input: the post-4 data gradient only
-    if (a.post != 4 || epi != 0 || (a.syn_k != 1 && a.syn_k != 2) || !a.syn_w || !a.syn_mb) return -1;
-    return launch_halo3_cfg<8, 8, 4, kEpiSyn>(a, st);
-  }
-  if (a.up) {  // upsampled input: the decoder's 512^2 conv1 (bias + ReLU + mask bits) only
-    if (a.post || epi != (kEpiBias | kEpiRelu) || !a.mbits_out || a.H % 2 || a.W % 2) return -1;
-    return launch_halo3_cfg<8, 8, 0, kEpiBias | kEpiRelu | kEpiMask | kEpiUp>(a, st);
   }
   if (a.mbits_out) {  // ReLU mask bits: bias + ReLU epilogue only (checked by the caller)
     if (a.post || epi != (kEpiBias | kEpiRelu)) return -1;
@@ -1732,30 +1474,6 @@ int launch_halo3_wgrad(const HaloWgradArgs& a, int G_per, hipStream_t st) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_wgrad_kernel<TH, 4>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
-  }
-  if (a.up) {  // X upsampled on the fly: 64 input channels (from one source), dY stored
-    if (a.cin != 64 || a.c1 != 64 || a.x2 || a.syn_dl || a.H % 2 || a.W % 2) return -1;
-    static bool attr_u = false;
-    if (!attr_u) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_wgrad_kernel<TH, 8, false, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr_u = true;
-    }
-    hipLaunchKernelGGL((halo3_wgrad_kernel<TH, 8, false, true>), dim3(groups * G_per), dim3(512), lds, st, a,
-                       tiles_w, tiles_h, n_sp, G_per);
-    return 0;
-  }
-  if (a.syn_dl) {  // synthesised dY: the 64 -> 64 head-input conv only
-    if (a.Cout != 64 || (a.syn_k != 1 && a.syn_k != 2) || !a.syn_w || !a.syn_mb) return -1;
-    static bool attr_s = false;
-    if (!attr_s) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_wgrad_kernel<TH, 8, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr_s = true;
-    }
-    hipLaunchKernelGGL((halo3_wgrad_kernel<TH, 8, true>), dim3(groups * G_per), dim3(512), lds, st, a, tiles_w,
-                       tiles_h, n_sp, G_per);
-    return 0;
   }
   if (w4)
     hipLaunchKernelGGL((halo3_wgrad_kernel<TH, 4>), dim3(groups * G_per), dim3(256), lds, st, a, tiles_w, tiles_h,

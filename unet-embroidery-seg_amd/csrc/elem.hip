@@ -23,30 +23,45 @@ constexpr int VE = 16 / sizeof(T);
 // Per-channel reductions of row partials part[g][q][C] (G row tiles, q = 0 .. nq-1) -- the BN
 // finalizes of the forward statistics and of the fused data-gradient post-ops.  They sit on the
 // compute stream between a producer and its consumer, so they are latency kernels: one wave per
-// channel (NWV = 1, four channels per block, no barrier) when G <= 512, the four waves of a block
-// per channel above that; every lane issues all its loads (kFinRPL rows x nq) before it adds, and
-// the lanes' fp64 partials are combined in a fixed order (deterministic).
+// channel (NWV = 1, four channels per block, no barrier) when G <= 512, a block of NWV = 4 or 16
+// waves per channel above that; every lane issues all its loads (kFinRPL rows x nq) before it adds,
+// and the lanes' fp64 partials are combined in a fixed order (deterministic).
 // ------------------------------------------------------------------------------------------
 constexpr int kFinRPL = 8;  // rows per lane per round
 
-static inline int fin_waves(int G) { return G > 512 ? 4 : 1; }
-static inline unsigned fin_blocks(int C, int nwv) { return nwv == 4 ? (unsigned)C : (unsigned)ceil_div(C, 4); }
+static inline int fin_waves(int G) { return G > 2048 ? 16 : G > 512 ? 4 : 1; }
+static inline unsigned fin_blocks(int C, int nwv) { return nwv > 1 ? (unsigned)C : (unsigned)ceil_div(C, 4); }
+static inline unsigned fin_threads(int nwv) { return nwv > 1 ? 64u * nwv : 256u; }
+// launch KERNEL<nwv> for the row count G with the finalize geometry
+#define FIN_LAUNCH(KERNEL, C, G, stream, ...)                                                                  \
+  do {                                                                                                     \
+    const int nwv_ = fin_waves(G);                                                                         \
+    const dim3 grid_(fin_blocks(C, nwv_)), block_(fin_threads(nwv_));                                      \
+    if (nwv_ == 16) hipLaunchKernelGGL(KERNEL<16>, grid_, block_, 0, (hipStream_t)(stream), __VA_ARGS__);  \
+    else if (nwv_ == 4) hipLaunchKernelGGL(KERNEL<4>, grid_, block_, 0, (hipStream_t)(stream), __VA_ARGS__); \
+    else hipLaunchKernelGGL(KERNEL<1>, grid_, block_, 0, (hipStream_t)(stream), __VA_ARGS__);              \
+  } while (0)
 
-// sum over the channel's lanes (one wave, or the block's four waves through sc[NQ][4]); every lane
+// sum over the channel's lanes (one wave, or the block's NWV waves through sc[NQ][NWV]); every lane
 // gets lane 0's / the fixed-order total
 template <int NWV, int NQ>
 __device__ __forceinline__ void fin_group_sum(double (&v)[NQ], double* sc) {
 #pragma unroll
   for (int j = 0; j < NQ; ++j) v[j] = __shfl(wave_sum_d(v[j]), 0, 64);
-  if constexpr (NWV == 4) {
+  if constexpr (NWV > 1) {
     const int wid = threadIdx.x >> 6;
     __syncthreads();
     if ((threadIdx.x & 63) == 0)
 #pragma unroll
-      for (int j = 0; j < NQ; ++j) sc[j * 4 + wid] = v[j];
+      for (int j = 0; j < NQ; ++j) sc[j * NWV + wid] = v[j];
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < NQ; ++j) v[j] = (sc[j * 4 + 0] + sc[j * 4 + 1]) + (sc[j * 4 + 2] + sc[j * 4 + 3]);
+    for (int j = 0; j < NQ; ++j) {
+      double t = 0.0;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) t += sc[j * NWV + w];
+      v[j] = t;
+    }
   }
 }
 
@@ -80,12 +95,12 @@ __device__ __forceinline__ void fin_row_sums(const float* part, long ldrow, int 
 // nn.BatchNorm2d (momentum 0.1, unbiased running var) and emits scale/shift for the apply pass.
 // ------------------------------------------------------------------------------------------
 template <int NWV>
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* part, int C, int G, long M, int tile,
+__global__ __launch_bounds__(NWV > 4 ? 64 * NWV : 256) void bn_finalize_kernel(const float* part, int C, int G, long M, int tile,
                                                           const float* gamma, const float* beta, float* rmean,
                                                           float* rvar, long long* nbt, float momentum, float eps,
                                                           float* mean_out, float* invstd_out, float* scale,
                                                           float* shift) {
-  __shared__ double sc[4];
+  __shared__ double sc[NWV];
   constexpr int NL = 64 * NWV;
   const int c = NWV == 1 ? (int)blockIdx.x * 4 + (threadIdx.x >> 6) : (int)blockIdx.x;
   if (NWV == 1 && c >= C) return;  // whole waves: no barrier in the one-wave form
@@ -524,10 +539,10 @@ __global__ __launch_bounds__(256) void relu_bwd_bias_kernel(const T* dA, int ldd
 // The same coefficients from the row partials of a fused data-gradient post-op
 // (unetseg_conv2d_dgrad_post): part[g][2][C] = (sum dz, sum dz*xhat) per row tile.
 template <int NWV>
-__global__ __launch_bounds__(256) void bn_bwd_finalize_rows_kernel(const float* part, int C, int G, long M,
+__global__ __launch_bounds__(NWV > 4 ? 64 * NWV : 256) void bn_bwd_finalize_rows_kernel(const float* part, int C, int G, long M,
                                                                    const float* g1, const float* inv1, float* dg1,
                                                                    float* db1, float* coef) {
-  __shared__ double sc[2 * 4];
+  __shared__ double sc[2 * NWV];
   const int c = NWV == 1 ? (int)blockIdx.x * 4 + (threadIdx.x >> 6) : (int)blockIdx.x;
   if (NWV == 1 && c >= C) return;
   double t[2];
@@ -545,12 +560,12 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_rows_kernel(const float* 
 // The two-branch form for the residual post-op (unetseg_conv2d_dgrad_post_res): part[g][1+nbranch][C] =
 // (sum dz, sum dz*xhat1 [, sum dz*xhat2]) per row tile; coefficients as bn_bwd_finalize_kernel.
 template <int NWV>
-__global__ __launch_bounds__(256) void bn_bwd_finalize_rows_res_kernel(const float* part, int C, int G, long M,
+__global__ __launch_bounds__(NWV > 4 ? 64 * NWV : 256) void bn_bwd_finalize_rows_res_kernel(const float* part, int C, int G, long M,
                                                                        int nbranch, const float* g1,
                                                                        const float* inv1, float* dg1, float* db1,
                                                                        const float* g2, const float* inv2, float* dg2,
                                                                        float* db2, float* coef) {
-  __shared__ double sc[3 * 4];
+  __shared__ double sc[3 * NWV];
   const int c = NWV == 1 ? (int)blockIdx.x * 4 + (threadIdx.x >> 6) : (int)blockIdx.x;
   if (NWV == 1 && c >= C) return;
   const int nq = 1 + nbranch;
@@ -575,9 +590,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_rows_res_kernel(const flo
 
 // out[c] (+)= sum_g part[g][k][c] for part [G][2][C] (bias gradient from the fused ReLU post-op)
 template <int NWV>
-__global__ __launch_bounds__(256) void colsum_rows_kernel(const float* part, int C, int G, int k, float* out,
+__global__ __launch_bounds__(NWV > 4 ? 64 * NWV : 256) void colsum_rows_kernel(const float* part, int C, int G, int k, float* out,
                                                           int accumulate) {
-  __shared__ double sc[4];
+  __shared__ double sc[NWV];
   const int c = NWV == 1 ? (int)blockIdx.x * 4 + (threadIdx.x >> 6) : (int)blockIdx.x;
   if (NWV == 1 && c >= C) return;
   double t[1];
@@ -1223,7 +1238,7 @@ __global__ void pw_small_bwd_kernel(const float* dy, const T* x, int ldx, long M
     load_vec(x + p * ldx + c0, xv);
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      // explicit product then fma: the halo data gradient synthesises this value (syn_chunk)
+      // explicit product then fma (no contraction choice left to the compiler)
       float s = 0.f;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -1528,13 +1543,8 @@ UNETSEG_API int unetseg_bn_finalize(const float* part, int C, int G, long M, int
                                     float eps, float* mean, float* invstd, float* scale, float* shift, void* stream) {
   US_CHECK_ARG(part && gamma && beta && mean && invstd && scale && shift && M > 0, "bn_finalize: bad args");
   US_CHECK_ARG(C > 0 && G > 0 && tile > 0, "bn_finalize: bad sizes");
-  const int nwv = fin_waves(G);
-  if (nwv == 4)
-    hipLaunchKernelGGL(bn_finalize_kernel<4>, dim3(fin_blocks(C, 4)), dim3(256), 0, (hipStream_t)stream, part, C, G, M,
-                       tile, gamma, beta, rmean, rvar, nbt, momentum, eps, mean, invstd, scale, shift);
-  else
-    hipLaunchKernelGGL(bn_finalize_kernel<1>, dim3(fin_blocks(C, 1)), dim3(256), 0, (hipStream_t)stream, part, C, G, M,
-                       tile, gamma, beta, rmean, rvar, nbt, momentum, eps, mean, invstd, scale, shift);
+  FIN_LAUNCH(bn_finalize_kernel, C, G, stream, part, C, G, M, tile, gamma, beta, rmean, rvar, nbt, momentum, eps, mean,
+             invstd, scale, shift);
   US_LAUNCH_CHECK("bn_finalize");
   return 0;
 }
@@ -1717,12 +1727,7 @@ UNETSEG_API int unetseg_bn_bwd_finalize_rows(const float* part, int C, int G, lo
                                              const float* inv1, float* dg1, float* db1, float* coef, void* stream) {
   US_CHECK_ARG(part && g1 && inv1 && dg1 && db1 && coef && M > 0, "bn_bwd_finalize_rows: bad args");
   US_CHECK_ARG(C > 0 && G > 0, "bn_bwd_finalize_rows: bad sizes");
-  if (fin_waves(G) == 4)
-    hipLaunchKernelGGL(bn_bwd_finalize_rows_kernel<4>, dim3(fin_blocks(C, 4)), dim3(256), 0, (hipStream_t)stream, part,
-                       C, G, M, g1, inv1, dg1, db1, coef);
-  else
-    hipLaunchKernelGGL(bn_bwd_finalize_rows_kernel<1>, dim3(fin_blocks(C, 1)), dim3(256), 0, (hipStream_t)stream, part,
-                       C, G, M, g1, inv1, dg1, db1, coef);
+  FIN_LAUNCH(bn_bwd_finalize_rows_kernel, C, G, stream, part, C, G, M, g1, inv1, dg1, db1, coef);
   US_LAUNCH_CHECK("bn_bwd_finalize_rows");
   return 0;
 }
@@ -1733,24 +1738,15 @@ UNETSEG_API int unetseg_bn_bwd_finalize_rows_res(const float* part, int C, int G
   US_CHECK_ARG(part && g1 && inv1 && dg1 && db1 && coef && M > 0 && C > 0 && G > 0 && (nbranch == 1 || nbranch == 2),
                "bn_bwd_finalize_rows_res: bad args");
   US_CHECK_ARG(nbranch == 1 || (g2 && inv2 && dg2 && db2), "bn_bwd_finalize_rows_res: branch 2 needs its pointers");
-  if (fin_waves(G) == 4)
-    hipLaunchKernelGGL(bn_bwd_finalize_rows_res_kernel<4>, dim3(fin_blocks(C, 4)), dim3(256), 0, (hipStream_t)stream,
-                       part, C, G, M, nbranch, g1, inv1, dg1, db1, g2, inv2, dg2, db2, coef);
-  else
-    hipLaunchKernelGGL(bn_bwd_finalize_rows_res_kernel<1>, dim3(fin_blocks(C, 1)), dim3(256), 0, (hipStream_t)stream,
-                       part, C, G, M, nbranch, g1, inv1, dg1, db1, g2, inv2, dg2, db2, coef);
+  FIN_LAUNCH(bn_bwd_finalize_rows_res_kernel, C, G, stream, part, C, G, M, nbranch, g1, inv1, dg1, db1, g2, inv2, dg2,
+             db2, coef);
   US_LAUNCH_CHECK("bn_bwd_finalize_rows_res");
   return 0;
 }
 
 UNETSEG_API int unetseg_colsum_rows(const float* part, int C, int G, int k, float* out, int accumulate, void* stream) {
   US_CHECK_ARG(part && out && C > 0 && G >= 0 && (k == 0 || k == 1), "colsum_rows: bad args");
-  if (fin_waves(G) == 4)
-    hipLaunchKernelGGL(colsum_rows_kernel<4>, dim3(fin_blocks(C, 4)), dim3(256), 0, (hipStream_t)stream, part, C, G, k,
-                       out, accumulate);
-  else
-    hipLaunchKernelGGL(colsum_rows_kernel<1>, dim3(fin_blocks(C, 1)), dim3(256), 0, (hipStream_t)stream, part, C, G, k,
-                       out, accumulate);
+  FIN_LAUNCH(colsum_rows_kernel, C, G, stream, part, C, G, k, out, accumulate);
   US_LAUNCH_CHECK("colsum_rows");
   return 0;
 }
@@ -1962,9 +1958,7 @@ UNETSEG_API int unetseg_pw_small_bwd_relu(int dtype, const float* dy, const void
   CHECK_VEC(dtype, c, "pw_small_bwd_relu");
   US_CHECK_ARG(c / 8 <= 256 && 256 % (c / 8) == 0, "pw_small_bwd_relu: bad C");
   US_CHECK_ARG(k == 1 || k == 2, "pw_small_bwd_relu: k must be 1 or 2");
-  // dx == NULL: the masked gradient is not stored (the head input's producer conv synthesises it in
-  // its data / weight gradients, unetseg_conv2d_dgrad_post_syn / unetseg_conv2d_wgrad_syn)
-  US_CHECK_ARG(dy && x && w && part_w && part_b && part_d, "pw_small_bwd_relu: null pointer");
+  US_CHECK_ARG(dx != nullptr && part_d != nullptr, "pw_small_bwd_relu: dx and part_d required");
   const int G = unetseg_pw_small_tiles(M);
   hipStream_t st = (hipStream_t)stream;
   if (k == 1)

@@ -43,7 +43,8 @@ def run_resnet_decoder(ctx, m, feats, head=None):
         ops.tap_mark(ctx, name)
         u = run_unet_up(ctx, getattr(m, name), skip, u)
     ops.tap_mark(ctx, "up_conv")
-    u = ops.up_conv(ctx, u, m.up_conv[1]._pc, align_corners=True)  # up_conv[0..2]: upsample -> conv -> ReLU
+    u = ops.upsample2x(ctx, u, align_corners=True)
+    u, _ = ops.conv(ctx, u, m.up_conv[1]._pc, relu=True)
     u, _ = ops.conv(ctx, u, m.up_conv[3]._pc, relu=True, head=head)
     return u
 

@@ -43,16 +43,6 @@ def call_configs(desc, dt=DT_BF16):
     if d in ("dgrad", "dgrad_post1", "dgrad_post2", "dgrad_post3", "dgrad_post4"):
         tag = "dgrad" if d == "dgrad" else d
         return [f"{tag}:{c}" for c in _lib.dgrad_config(dt, K, N, Pq, Qq, K, cin, R, S, stride, pad, cin, H, W)]
-    if d == "fwd_up":  # the conv that blends its upsampled input (halo kernel only)
-        return ["fwd_up:halo3"]
-    if d == "wgrad_up":
-        kern, sp, red = _lib.wgrad_config(dt, C1, C1, 0, 0, N, H, W, K, K, R, S, stride, pad)
-        return [f"wgrad_up:{kern}", red]
-    if d == "dgrad_syn":  # the head producer's data gradient with its input synthesised (halo kernel only)
-        return ["dgrad_syn:halo3"]
-    if d == "wgrad_syn":
-        kern, sp, red = _lib.wgrad_config(dt, C1, ld1 or C1, 0, 0, N, H, W, K, K, R, S, stride, pad)
-        return [f"wgrad_syn:{kern}", red]
     if d == "dgrad_padk":
         Kp = -(-K // 64) * 64
         return [f"dgrad:{c}" for c in _lib.dgrad_config(dt, Kp, N, Pq, Qq, Kp, C1, 1, 1, 1, 0, C1, H, W)]

@@ -42,11 +42,6 @@ SIGNATURES = {
     "unetseg_upsample2x_bwd_tiles": (I, [I, I, I, I, I]),
     "unetseg_upsample2x_bwd_relu": (I, [I, P, I, I, I, I, I, I, P, I, P, I, P, I, P]),
     "unetseg_conv2d_fwd_head": (I, [I, P, I, I, I, I, P, P, P, I, I, P, P, P, P]),
-    "unetseg_conv2d_fwd_head_mask": (I, [I, P, I, I, I, I, P, P, P, I, I, P, P, P, P, P]),
-    "unetseg_conv2d_dgrad_post_syn": (I, [I, P, I, P, P, I, I, I, P, P, I, P, P, I, P]),
-    "unetseg_conv2d_wgrad_syn": (I, [I, P, I, I, I, I, P, I, P, P, P, SZ, P, I, P]),
-    "unetseg_conv2d_fwd_up_mask": (I, [I, P, I, I, I, I, I, P, P, P, I, P, P]),
-    "unetseg_conv2d_wgrad_up": (I, [I, P, I, I, I, I, I, P, I, I, P, SZ, P, I, P]),
     "unetseg_conv2d_fwd_mask": (I, [I, P, I, I, I, I, P, P, P, I, P, P]),
     "unetseg_conv2d_wgrad_bnrelu_in": (I, [I, P, I, I, I, I, I, P, I, I, P, P, P, SZ, P, I, I, P]),
     "unetseg_conv2d_fwd_affine": (I, [I, P, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P, P, I, P, I, P]),
@@ -131,8 +126,8 @@ SIGNATURES = {
 }
 
 #: functions returning a value rather than a status (no RuntimeError on non-zero)
-VALUE_FUNCS = {"conv2d_fwd_mask", "conv2d_fwd_up_mask", "reduce_tiles", "pw_small_tiles", "conv_tile_m", "abi_version", "conv2d_fwd_tile_m",
-               "conv2d_dgrad_post", "conv2d_dgrad_post_res", "conv2d_dgrad_post_syn", "stem_fwd_tile_m", "attn_bwd1_tiles", "pw_small_tile", "conv2d_fwd_config",
+VALUE_FUNCS = {"conv2d_fwd_mask", "reduce_tiles", "pw_small_tiles", "conv_tile_m", "abi_version", "conv2d_fwd_tile_m",
+               "conv2d_dgrad_post", "conv2d_dgrad_post_res", "stem_fwd_tile_m", "attn_bwd1_tiles", "pw_small_tile", "conv2d_fwd_config",
                "conv2d_dgrad_config", "conv2d_wgrad_config", "stem_config", "pw_head_tiles", "channel_stats_tiles",
                "augment_tables_len", "pack_tiles",
                "conv2d_fwd_bnrelu_in_config", "conv2d_fwd_head_ok", "upsample2x_bwd_tiles"}

@@ -37,7 +37,7 @@ class Node:
     ``lazy`` (a BNState): the node stands for relu(BN(data)) that was never stored -- ``data`` is the
     BN input and the consuming conv applies BN-ReLU on load (``bn(..., lazy=True)``)."""
 
-    __slots__ = ("data", "grad", "need_grad", "uses", "fuse", "fused", "lazy", "head", "mbits", "vgrad")
+    __slots__ = ("data", "grad", "need_grad", "uses", "fuse", "fused", "lazy", "head", "mbits")
 
     def __init__(self, data, need_grad=True):
         self.data = data
@@ -49,9 +49,6 @@ class Node:
         self.lazy = None
         self.head = None  # (head Conv2d, fp32 logits) computed by the producing conv's epilogue
         self.mbits = None  # packed ReLU mask of data (unetseg_conv2d_fwd_mask), read by post 4
-        # the gradient of data left unstored by the head backward (SYN_HEAD): (logit gradient fp32
-        # [N][k][H][W], head weight [k][64], mbits); the producer conv's gradients synthesise it
-        self.vgrad = None
 
     @property
     def shape(self):
@@ -73,10 +70,6 @@ FUSE_UP = os.environ.get("UNETSEG_NO_UP_FUSE", "0") != "1"
 #: a 64-channel halo conv + bias + ReLU stores its ReLU mask as bits for the consumer's data gradient
 #: (post 4) instead of that dgrad re-reading the activation (UNETSEG_NO_RELU_BITS=1 disables)
 RELU_BITS = os.environ.get("UNETSEG_NO_RELU_BITS", "0") != "1"
-#: the fused head's producer conv also stores its output's ReLU bits, the head backward then stores no
-#: input gradient, and that conv's data / weight gradients synthesise it from the logit gradient
-#: (unetseg_conv2d_dgrad_post_syn / unetseg_conv2d_wgrad_syn; UNETSEG_NO_HEAD_SYN=1 disables)
-SYN_HEAD = os.environ.get("UNETSEG_NO_HEAD_SYN", "0") != "1"
 
 
 _WORKSPACES = {}
@@ -428,15 +421,9 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                                lib.conv2d_fwd_head_ok(ctx.dt, ldp(X1), N, H, W, ldp(y), head.weight.shape[0])):
         Kh = head.weight.shape[0]
         logits = torch.empty((N, Kh, Pq, Qq), dtype=torch.float32, device=ctx.device)
-        if SYN_HEAD and FUSE and RELU_BITS and ctx.training and ctx.tape is not None and ldp(y) % 8 == 0:
-            mbits = torch.empty(M * 8, dtype=torch.uint8, device=ctx.device)
-            with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
-                lib.conv2d_fwd_head_mask(ctx.dt, P(X1), ldp(X1), N, H, W, P(pc.wk), P(b), P(y), ldp(y), Kh,
-                                         P(head.weight), P(head.bias), P(logits), P(mbits), ctx.stream)
-        else:
-            with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
-                lib.conv2d_fwd_head(ctx.dt, P(X1), ldp(X1), N, H, W, P(pc.wk), P(b), P(y), ldp(y), Kh,
-                                    P(head.weight), P(head.bias), P(logits), ctx.stream)
+        with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
+            lib.conv2d_fwd_head(ctx.dt, P(X1), ldp(X1), N, H, W, P(pc.wk), P(b), P(y), ldp(y), Kh, P(head.weight),
+                                P(head.bias), P(logits), ctx.stream)
         head = (head, logits)
     else:
         head = None
@@ -463,15 +450,9 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
 
     def bwd():
         dA = out.grad
-        vg, out.vgrad = out.vgrad, None
-        if dA is None and vg is None:
+        if dA is None:
             return
         dev = ctx.device
-        syn = None  # (logit gradient, head weight, head mbits, k, dgrad rows or 0) when dY is synthesised
-        if vg is not None:
-            syn = _syn_plan(ctx, vg, x1, x2, pc, N, H, W, C1, Pq, Qq, X1)
-            if syn is None:
-                dA = _materialize_vgrad(ctx, out, vg)
         if relu and out.fused is not None:
             # the consumer's dgrad stored the masked gradient and the bias partials
             part, rows = out.fused
@@ -508,8 +489,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                 lib.stream_wait(side.cuda_stream, ctx.stream)
                 # dY, the inputs and the input prologue's BN coefficients may be freed (compute-stream
                 # order) before the wgrad has run on the side stream, which lags the compute stream
-                for t in ((dY, X1, X2) + ((lazy.sc, lazy.sh) if lazy is not None else ()) +
-                          ((syn[0], syn[2]) if syn is not None else ())):
+                for t in (dY, X1, X2) + ((lazy.sc, lazy.sh) if lazy is not None else ()):
                     if t is not None:
                         t.record_stream(side)
                 ws = workspace(ws_bytes, dev, 1)
@@ -525,10 +505,6 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                     lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), 0, 0, 0, N, H, W, P(dY), Kp, Kp, 1, 1, 1, 0, P(ws),
                                      ws.numel(), P(dwp), pc.C, 0, wst)
                     lib.add(DT_F32, P(dwp), pc.C, P(pc.conv.weight.grad), pc.C, K, pc.C, wst)
-            elif syn is not None:
-                with _probe("wgrad", flops, 1, ("wgrad_syn",) + desc, stream=side):
-                    lib.conv2d_wgrad_syn(ctx.dt, P(X1), ldp(X1), N, H, W, P(syn[0]), syn[3], P(syn[1]), P(syn[2]),
-                                         P(ws), ws.numel(), P(pc.conv.weight.grad), 1, wst)
             elif lazy is not None:
                 with _probe("wgrad", flops, 1, ("wgrad_bnrelu_in",) + desc, stream=side):
                     lib.conv2d_wgrad_bnrelu_in(ctx.dt, P(X1), C1, ldp(X1), N, H, W, P(dY), ldp(dY), K, P(lazy.sc),
@@ -552,18 +528,6 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                 with _probe("igemm_tn", flops, 1, ("dgrad_padk",) + desc):
                     lib.conv2d_dgrad(ctx.dt, P(dY), Kp, N, Pq, Qq, P(wtp), Kp, C1, 1, 1, 1, 0, P(g), ldp(g), H, W, acc,
                                      ctx.stream)
-        elif syn is not None:
-            if x1.need_grad:
-                rows = syn[4]
-                g = ctx.empty(N, H, W, C1)
-                part1 = ctx.f32(rows, 2, C1)
-                with _probe("igemm_tn", flops, 1, ("dgrad_syn",) + desc):
-                    rc = lib.conv2d_dgrad_post_syn(ctx.dt, P(syn[0]), syn[3], P(syn[1]), P(syn[2]), N, Pq, Qq,
-                                                   P(pc.wt), P(g), C1, P(x1.mbits), P(part1), rows, ctx.stream)
-                if rc != 0:
-                    raise RuntimeError(f"unetseg_conv2d_dgrad_post_syn failed ({rc}): {lib_last_error()}")
-                x1.grad = g
-                x1.fused = (part1, rows)
         elif x2 is None:
             if x1.need_grad and not _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc, last_grad):
                 g, acc = gbuf(ctx, x1)
@@ -591,40 +555,6 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
 
     ctx.push(bwd)
     return out, st
-
-
-def _syn_plan(ctx, vg, x1, x2, pc, N, H, W, C1, Pq, Qq, X1):
-    """whether this conv's backward can synthesise its (never stored) output gradient vg: the head's
-    producer (3x3, 64 -> 64, bf16 halo path) whose input is a ReLU output with mask bits consumed only
-    here; -> (dl, head weight, head mbits, k, dgrad rows) or None"""
-    dl, hw, hmb, k = vg
-    if not (ctx.dt == DT_BF16 and x2 is None and pc.K == 64 and C1 == 64 and (pc.R, pc.S) == (3, 3) and
-            pc.conv.stride in (1, (1, 1)) and pc.conv.padding in (1, (1, 1)) and ldp(X1) % 8 == 0 and
-            X1.stride(-1) == 1):
-        return None
-    rows = 0
-    if x1.need_grad:
-        if not (x1.fuse is not None and x1.fuse[0] == 1 and x1.mbits is not None and x1.grad is None and
-                x1.uses == 1):
-            return None
-        rows = lib.conv2d_dgrad_post_syn(ctx.dt, 0, k, 0, 0, N, Pq, Qq, 0, 0, C1, 0, 0, 0, ctx.stream)
-        if rows <= 0:
-            return None
-    return dl, hw, hmb, k, rows
-
-
-def _materialize_vgrad(ctx, node, vg):
-    """the stored form of a synthesised gradient (pw_small_bwd_relu's dx; its partials are discarded:
-    the head backward already delivered them)"""
-    dl, hw, hmb, k = vg
-    X = node.data
-    N, H, W, C = X.shape
-    M = N * H * W
-    G = lib.pw_small_tiles(M)
-    dx = ctx.empty(N, H, W, C)
-    lib.pw_small_bwd_relu(ctx.dt, P(dl), P(X), ldp(X), M, H * W, C, k, P(hw), P(dx), ldp(dx), P(ctx.f32(k, C, G)),
-                          P(ctx.f32(k, G)), P(ctx.f32(G, 2, C)), ctx.stream)
-    return dx
 
 
 #: eval-mode BatchNorm folded into the preceding conv (UNETSEG_NO_BN_FOLD=1: separate BN pass)
@@ -1035,82 +965,6 @@ def _upsample_bwd(ctx, x, gout, align_corners):
     lib.upsample2x_bwd(ctx.dt, P(gout), ldp(gout), N, H, W, C, int(align_corners), P(g), ldp(g), acc, ctx.stream)
 
 
-#: the decoder's last upsample blended inside its consumer conv (unetseg_conv2d_fwd_up_mask /
-#: unetseg_conv2d_wgrad_up): the 512^2 upsampled tensor is never stored (UNETSEG_NO_UP_CONV=1 disables)
-UP_CONV = os.environ.get("UNETSEG_NO_UP_CONV", "0") != "1"
-
-
-def up_conv(ctx, x, pc, align_corners):
-    """relu(conv(upsample2x(x))) (+ bias): model/unet_resnet.py:90-97 up_conv[0..2].  On the halo path
-    (bf16, 64 -> 64, 3x3) the conv blends its input tiles from x itself and stores its output's ReLU
-    bits for the next conv's data gradient; otherwise the upsample is stored and ops.conv runs."""
-    X = x.data
-    N, Hs, Ws, C1 = X.shape
-    H, W = 2 * Hs, 2 * Ws
-    b = pc.conv.bias
-    if not (UP_CONV and RELU_BITS and FUSE and ctx.dt == DT_BF16 and pc.K == 64 and C1 == 64 and b is not None and
-            (pc.R, pc.S) == (3, 3) and pc.conv.stride in (1, (1, 1)) and pc.conv.padding in (1, (1, 1)) and
-            X.stride(-1) == 1 and lib.conv2d_fwd_up_mask(ctx.dt, 0, ldp(X), N, H, W, int(align_corners), 0, 0, 0,
-                                                         64, 0, 0) == 1):
-        u = upsample2x(ctx, x, align_corners)
-        return conv(ctx, u, pc, relu=True)[0]
-    use(x)
-    K = 64
-    M = N * H * W
-    y = ctx.empty(N, H, W, K)
-    mbits = torch.empty(M * 8, dtype=torch.uint8, device=ctx.device)
-    flops = 2.0 * M * K * C1 * 9
-    desc = (N, H, W, C1, 0, K, 3, 3, 1, 1, C1, 0)  # the conv on the (virtual) upsampled input
-    with _probe("igemm_tn", flops, 1, ("fwd_up",) + desc):
-        lib.conv2d_fwd_up_mask(ctx.dt, P(X), ldp(X), N, H, W, int(align_corners), P(pc.wk), P(b), P(y), K, P(mbits),
-                               ctx.stream)
-    out = Node(y)
-    out.mbits = mbits
-    out.fuse = (1, y, None)
-    if TAP is not None and ctx.tape is not None:
-        vnode = Node(None)  # the upsampled input: never stored (lazy)
-        _tap(ctx, "resize", vnode, [x], size=(H, W), align_corners=bool(align_corners), lazy=True,
-             dtype=ctx.tdtype)
-        _tap(ctx, "conv", out, [vnode, None], conv=pc.conv, relu=True)
-
-    def bwd():
-        dA = out.grad
-        if dA is None:
-            return
-        if out.fused is not None:  # the consumer's dgrad stored the masked gradient and the bias partials
-            part, rows = out.fused
-            dY = dA
-            lib.colsum_rows(P(part), K, rows, 0, P(b.grad), 1, ctx.stream)
-        else:
-            Gr = lib.reduce_tiles(ctx.dt, M, K, None, None)
-            part = ctx.f32(K, Gr)
-            dY = ctx.empty(N, H, W, K)
-            lib.relu_bwd_bias(ctx.dt, P(dA), ldp(dA), P(y), ldp(y), P(dY), K, M, K, P(part), Gr, ctx.stream)
-            lib.colsum_finalize(P(part), K, Gr, P(b.grad), 1, ctx.stream)
-        ws_bytes = lib.conv2d_wgrad_workspace(ctx.dt, N, H, W, K, C1, 3, 3)
-        side = ctx.side
-        if side is not None:
-            lib.stream_wait(side.cuda_stream, ctx.stream)
-            for t in (dY, X):
-                t.record_stream(side)
-            ws, wst = workspace(ws_bytes, ctx.device, 1), side.cuda_stream
-        else:
-            ws, wst = workspace(ws_bytes, ctx.device), ctx.stream
-        with _probe("wgrad", flops, 1, ("wgrad_up",) + desc, stream=side):
-            lib.conv2d_wgrad_up(ctx.dt, P(X), ldp(X), N, H, W, int(align_corners), P(dY), ldp(dY), K, P(ws),
-                                ws.numel(), P(pc.conv.weight.grad), 1, wst)
-        if x.need_grad:
-            gu = ctx.empty(N, H, W, C1)
-            with _probe("igemm_tn", flops, 1, ("dgrad",) + desc):
-                lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, H, W, P(pc.wt), K, C1, 3, 3, 1, 1, P(gu), C1, H, W, 0,
-                                 ctx.stream)
-            _upsample_bwd(ctx, x, gu, align_corners)
-        ctx.param_done(pc.conv.weight, b)
-
-    ctx.push(bwd)
-    return out
-
-
 def resize_bilinear(ctx, x, oh, ow, align_corners):
     """F.interpolate(x, size=(oh, ow), mode="bilinear") for sizes that are not an exact x2
     (model/unet_attention.py:31-33,52-53, model/unet_dualdense.py:57-58)"""
@@ -1211,18 +1065,11 @@ def pw_head(ctx, x, conv_mod):
                 and x.grad is None and x.uses == 1 and ctx.dt == DT_BF16):
             # x is a ReLU output consumed only here: its backward mask and the producer conv's
             # bias-gradient partials ride along (conv() reads them back from x.fused)
+            dx = ctx.empty(N, H, W, C)
             part = ctx.f32(G, 2, C)
-            if SYN_HEAD and x.mbits is not None and x.head is not None and x.head[0] is conv_mod:
-                # the producer conv stored x's ReLU bits: dx is not stored, that conv's gradients
-                # synthesise it from dy (ops.conv, _syn_plan)
-                lib.pw_small_bwd_relu(ctx.dt, P(dy), P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), 0, 0,
-                                      P(pw), P(pb), P(part), ctx.stream)
-                x.vgrad = (dy, conv_mod.weight, x.mbits, K)
-            else:
-                dx = ctx.empty(N, H, W, C)
-                lib.pw_small_bwd_relu(ctx.dt, P(dy), P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(dx),
-                                      ldp(dx), P(pw), P(pb), P(part), ctx.stream)
-                x.grad = dx
+            lib.pw_small_bwd_relu(ctx.dt, P(dy), P(X), ldp(X), M, H * W, C, K, P(conv_mod.weight), P(dx), ldp(dx),
+                                  P(pw), P(pb), P(part), ctx.stream)
+            x.grad = dx
             x.fused = (part, G)
         else:
             dx, acc = (gbuf(ctx, x) if x.need_grad else (None, 0))
