@@ -166,7 +166,8 @@ def last_error() -> str:
 
 
 class _Caller:
-    """lib.<name>(...) raises RuntimeError on a non-zero status."""
+    """lib.<name>(...) raises RuntimeError on a non-zero status.  The bound callable is cached on the
+    instance after the first lookup (the op layer makes ~500 calls per training step)."""
 
     def __getattr__(self, item):
         fn = getattr(load(), "unetseg_" + item)
@@ -176,7 +177,9 @@ class _Caller:
                 if rc != 0:
                     raise RuntimeError(f"unetseg_{item} failed ({rc}): {last_error()}")
                 return rc
+            self.__dict__[item] = call
             return call
+        self.__dict__[item] = fn
         return fn
 
 
