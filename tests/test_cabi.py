@@ -90,3 +90,31 @@ def test_argument_errors_reported_without_device():
     assert b"cpad" in raw.unetseg_last_error()
     with pytest.raises(RuntimeError, match="cpad"):
         lib.lib.pack_input(0, None, 1, 3, 4, 4, 2, None, None)
+
+
+def test_fastcall_binding_matches_ctypes():
+    """The CPython fast-call binding (unetseg_hip/gen_fastcall.py) covers every int / float / pointer
+    entry point, returns what the ctypes call returns and raises the same status errors."""
+    from unetseg_hip import lib
+
+    if not os.path.exists(lib.LIB_PATH):
+        pytest.skip("libunetseg_hip.so not built")
+    raw = lib.load()
+    fast = lib._fast()
+    if fast is None:
+        pytest.skip("fast-call binding not built (make -C unet-embroidery-seg_amd/csrc)")
+    from unetseg_hip.gen_fastcall import supported
+    names = [n[len("unetseg_"):] for n, _, _ in supported()]
+    assert len(names) >= 90 and all(hasattr(fast, n) for n in names)
+    # value-returning queries agree with ctypes
+    for args in ((1, 1 << 20, 64, None, None), (0, 4096, 2048, None, None)):
+        assert fast.reduce_tiles(*args) == raw.unetseg_reduce_tiles(*args)
+    assert fast.conv2d_wgrad_workspace(1, 16, 128, 128, 64, 64, 3, 3) == \
+        raw.unetseg_conv2d_wgrad_workspace(1, 16, 128, 128, 64, 64, 3, 3)
+    assert fast.abi_version() == 1
+    # status errors: same exception type and message as the ctypes wrapper
+    with pytest.raises(RuntimeError, match="unetseg_pack_input failed .*cpad"):
+        fast.pack_input(0, None, 1, 3, 4, 4, 2, None, None)
+    with pytest.raises(TypeError):
+        fast.pack_input(0, None)
+    assert lib.lib.pack_input is fast.pack_input  # the op layer's lib.<name> resolves to the binding

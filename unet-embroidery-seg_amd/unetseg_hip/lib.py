@@ -165,12 +165,39 @@ def last_error() -> str:
     return load().unetseg_last_error().decode("utf-8", "replace")
 
 
+_FAST = None
+
+
+def _fast():
+    """the CPython fast-call binding (gen_fastcall.py, built next to the library by the csrc Makefile):
+    the same entry points without ctypes' per-call conversion cost; None when absent, when the
+    library comes from UNETSEG_LIB_PATH (A/B builds: the binding links the in-tree library) or with
+    UNETSEG_NO_FASTCALL=1"""
+    global _FAST
+    if _FAST is None:
+        _FAST = False
+        if os.environ.get("UNETSEG_LIB_PATH") is None and os.environ.get("UNETSEG_NO_FASTCALL", "0") != "1":
+            try:
+                from . import _unetseg_fast
+                _FAST = _unetseg_fast
+            except ImportError:
+                pass
+    return _FAST or None
+
+
 class _Caller:
     """lib.<name>(...) raises RuntimeError on a non-zero status.  The bound callable is cached on the
-    instance after the first lookup (the op layer makes ~500 calls per training step)."""
+    instance after the first lookup (the op layer makes ~500 calls per training step); entry points the
+    fast-call binding covers use it (same arguments, same status errors)."""
 
     def __getattr__(self, item):
-        fn = getattr(load(), "unetseg_" + item)
+        lib_ = load()
+        fast = _fast()
+        if fast is not None and hasattr(fast, item):
+            fn = getattr(fast, item)
+            self.__dict__[item] = fn
+            return fn
+        fn = getattr(lib_, "unetseg_" + item)
         if SIGNATURES["unetseg_" + item][0] is I and item not in VALUE_FUNCS:
             def call(*args):
                 rc = fn(*args)

@@ -30,6 +30,20 @@ def ldp(t):
     return 0 if t is None else t.stride(-2)
 
 
+_QMEMO = {}
+
+
+def _q(name, *args):
+    """a host-only shape query of the C ABI (tile counts, partial rows, workspace sizes), memoised: its
+    result depends on the integer arguments only, so callers pass 0 for every pointer and the stream"""
+    # the one dispatch switch the library reads per call (tests flip it): part of the key
+    key = (name, os.environ.get("UNETSEG_TN_NO_HALO_RING")) + args
+    v = _QMEMO.get(key)
+    if v is None:
+        v = _QMEMO[key] = getattr(lib, name)(*args)
+    return v
+
+
 class Node:
     """An activation.  ``uses`` counts the ops that consumed it; ``fuse`` describes the ReLU that
     produced it, so that a sole consumer conv can apply that op's backward mask and first reduction
@@ -403,7 +417,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
     st = None
     stats = stats and ctx.training  # eval-mode BN normalises with the running statistics
     if stats:
-        tile = lib.conv2d_fwd_tile_m(ctx.dt, C1, ldp(X1), C2, ldp(X2), N, H, W, K, R, S, stride, pad)
+        tile = _q("conv2d_fwd_tile_m", ctx.dt, C1, ldp(X1), C2, ldp(X2), N, H, W, K, R, S, stride, pad)
         st = (ctx.f32(math.ceil(M / tile), 2, K), tile)  # [row tiles][sum, M2][K]
     b = pc.conv.bias
     flops = 2.0 * M * K * pc.C * R * S  # algorithmic (unpadded Cin)
@@ -418,7 +432,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
     elif head is not None and (FUSE_HEAD and x2 is None and relu and st is None and b is not None and
                                head.bias is not None and K == 64 and
                                C1 == 64 and (R, S, stride, pad) == (3, 3, 1, 1) and
-                               lib.conv2d_fwd_head_ok(ctx.dt, ldp(X1), N, H, W, ldp(y), head.weight.shape[0])):
+                               _q("conv2d_fwd_head_ok", ctx.dt, ldp(X1), N, H, W, ldp(y), head.weight.shape[0])):
         Kh = head.weight.shape[0]
         logits = torch.empty((N, Kh, Pq, Qq), dtype=torch.float32, device=ctx.device)
         with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
@@ -429,7 +443,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
         head = None
         if (RELU_BITS and FUSE and relu and b is not None and x2 is None and st is None and ctx.training and
                 ctx.tape is not None and K == 64 and C1 == 64 and (R, S, stride, pad) == (3, 3, 1, 1) and
-                lib.conv2d_fwd_mask(ctx.dt, 0, ldp(X1), N, H, W, 0, 0, 0, ldp(y), 0, 0) == 1):
+                _q("conv2d_fwd_mask", ctx.dt, 0, ldp(X1), N, H, W, 0, 0, 0, ldp(y), 0, 0) == 1):
             mbits = torch.empty(M * 8, dtype=torch.uint8, device=ctx.device)
             with _probe("igemm_tn", flops, 1, ("fwd",) + desc):
                 rc = lib.conv2d_fwd_mask(ctx.dt, P(X1), ldp(X1), N, H, W, P(pc.wk), P(b), P(y), ldp(y), P(mbits),
@@ -460,7 +474,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
             if b is not None:
                 lib.colsum_rows(P(part), K, rows, 0, P(b.grad), 1, ctx.stream)
         elif relu:
-            Gr = lib.reduce_tiles(ctx.dt, M, K, None, None)
+            Gr = _q("reduce_tiles", ctx.dt, M, K, None, None)
             part = ctx.f32(K, Gr)
             dY = ctx.empty(N, Pq, Qq, K)
             lib.relu_bwd_bias(ctx.dt, P(dA), ldp(dA), P(y), ldp(y), P(dY), K, M, K, P(part), Gr, ctx.stream)
@@ -483,7 +497,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
         def launch_wgrad(serial=False):
             # weight gradient: on the side stream when overlapping (it only needs dY and the inputs,
             # and nothing in the data-gradient chain reads its output)
-            ws_bytes = lib.conv2d_wgrad_workspace(ctx.dt, N, Pq, Qq, Kp, cin, R, S)
+            ws_bytes = _q("conv2d_wgrad_workspace", ctx.dt, N, Pq, Qq, Kp, cin, R, S)
             side = None if serial else ctx.side
             if side is not None:
                 lib.stream_wait(side.cuda_stream, ctx.stream)
@@ -614,8 +628,8 @@ def _dgrad_fused_res(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc, last_gra
     _, y3, s1, mbits, y2, s2 = x1.fuse
     K = pc.K
     g = x1.grad
-    rows = lib.conv2d_dgrad_post_res(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, 0, ldp(g), P(y3), ldp(y3),
-                                     0, 0, 0, 0, 0, 0, 0, 0, 0, ctx.stream)
+    rows = _q("conv2d_dgrad_post_res", ctx.dt, 0, ldp(dY), N, Pq, Qq, 0, K, C1, 0, ldp(g), 0, ldp(y3),
+              0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
     if rows <= 0:
         return False
     nq = 3 if y2 is not None else 2
@@ -642,14 +656,15 @@ def _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc, last_grad=Fa
     stride, pad = pc.conv.stride, pc.conv.padding
     args = [ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, R, S, stride, pad]
     coeffs = [P(st.sc), P(st.sh), P(st.mean), P(st.inv)] if kind == 2 else [0, 0, 0, 0]
+    qargs = (ctx.dt, 0, ldp(dY), N, Pq, Qq, 0, K, C1, R, S, stride, pad, 0, C1, H, W)
     rows = -1
     if kind == 1 and x1.mbits is not None:
         # the producer stored its ReLU mask as bits: post 4 reads them instead of the activation
-        rows = lib.conv2d_dgrad_post(*args, 0, C1, H, W, 4, P(x1.mbits), 0, *coeffs, 0, 0, ctx.stream)
+        rows = _q("conv2d_dgrad_post", *qargs, 4, 0, 0, 0, 0, 0, 0, 0, 0, 0)
         if rows > 0:
             kind, aux = 4, x1.mbits
     if rows <= 0:
-        rows = lib.conv2d_dgrad_post(*args, 0, C1, H, W, kind, P(aux), ldp(aux), *coeffs, 0, 0, ctx.stream)
+        rows = _q("conv2d_dgrad_post", *qargs, kind, 0, ldp(aux), 0, 0, 0, 0, 0, 0, 0)
     if rows <= 0:
         return False
     g = ctx.empty(N, H, W, C1)
@@ -735,14 +750,15 @@ def _bn_coeffs(ctx, bn, st, M, tile=None):
         st, tile = st
     C = bn.weight.shape[0]
     s = BNState()
-    s.sc, s.sh = ctx.f32(C), ctx.f32(C)
     if ctx.training:
-        s.mean, s.inv = ctx.f32(C), ctx.f32(C)
+        # one allocation for the four coefficient vectors (the host cost of a step is per allocation)
+        s.sc, s.sh, s.mean, s.inv = ctx.f32(4, C).unbind(0)
         G = st.shape[0]
         lib.bn_finalize(P(st), C, G, M, tile, P(bn.weight), P(bn.bias), P(bn.running_mean), P(bn.running_var),
                         P(bn.num_batches_tracked), bn.momentum, bn.eps, P(s.mean), P(s.inv), P(s.sc), P(s.sh),
                         ctx.stream)
     else:
+        s.sc, s.sh = ctx.f32(2, C).unbind(0)
         s.mean = s.inv = None
         lib.bn_eval_coeffs(C, P(bn.weight), P(bn.bias), P(bn.running_mean), P(bn.running_var), bn.eps, P(s.sc),
                            P(s.sh), ctx.stream)
@@ -857,7 +873,7 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None, lazy=False):
             lib.bn_bwd_apply(ctx.dt, P(dA), ldp(dA), 0, C, 0, 0, P(Y), ldp(Y), P(s1.mean), P(s1.inv),
                              P(dy1), ldp(dy1), 0, 0, 0, 0, 0, 0, P(coef), 0, 0, 0, M, C, ctx.stream)
             return
-        Gr = lib.reduce_tiles(ctx.dt, M, C, None, None)
+        Gr = _q("reduce_tiles", ctx.dt, M, C, None, None)
         part = ctx.f32(3, C, Gr)
         y2 = res_bn[0] if res_bn is not None else None
         Y2 = y2.data if y2 is not None else None
@@ -953,7 +969,7 @@ def _upsample_bwd(ctx, x, gout, align_corners):
             and x.grad is None and x.uses == 1):
         # x is a ReLU output consumed only here (unetUp conv2 -> next block's upsample): its
         # backward mask and the producer conv's bias-gradient partials ride along
-        rows = lib.upsample2x_bwd_tiles(ctx.dt, N, H, W, C)
+        rows = _q("upsample2x_bwd_tiles", ctx.dt, N, H, W, C)
         g = ctx.empty(N, H, W, C)
         part = ctx.f32(rows, 2, C)
         lib.upsample2x_bwd_relu(ctx.dt, P(gout), ldp(gout), N, H, W, C, int(align_corners), P(X), ldp(X), P(g),
@@ -1059,7 +1075,7 @@ def pw_head(ctx, x, conv_mod):
             lib.colsum_finalize(P(pb), K, G, P(conv_mod.bias.grad), 1, ctx.stream)
             ctx.param_done(conv_mod.weight, conv_mod.bias)
             return
-        G = lib.pw_small_tiles(M)
+        G = _q("pw_small_tiles", M)
         pw, pb = ctx.f32(K, C, G), ctx.f32(K, G)
         if (FUSE and x.need_grad and x.fuse is not None and x.fuse[0] == 1 and x.fuse[1] is X
                 and x.grad is None and x.uses == 1 and ctx.dt == DT_BF16):
