@@ -755,39 +755,65 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
       iv3[1][e] = (ok && two) ? a.pinv2[nc + e] : 0.f;
     }
   }
+  // the write-out's global reads (the old gradient; post 3: y3 / y_ds and the mask byte) of GRP rows
+  // are issued together before their stores: the stores may alias them as far as the compiler knows,
+  // so loads left inside the row loop would each wait out a full memory round trip (vmcnt also counts
+  // the preceding stores) -- eight serial HBM latencies per tile in these short-K layers.  Post 3 in
+  // groups of four rows (its 13 registers per row beside the partials and coefficients would spill).
+  constexpr int NIT = WTM / RPI;
+  constexpr int GRP = (POST == 3 && NIT > 4) ? 4 : NIT;
+  static_assert(NIT % GRP == 0, "row groups");
 #pragma unroll
-  for (int i = 0; i < WTM / RPI; ++i) {
-    const int r = i * RPI + rsub;
-    if (r >= cnt || nc >= a.Ng) continue;
-    const long opx = out_pix(row0 + r);
-    bf16* ptr = (bf16*)a.y + opx * a.ldy + nc;
-    uint4 v = *reinterpret_cast<const uint4*>(tl + r * LROW + ck * 16);
-    if constexpr (POST == 3) {
-      const uint4 old = *reinterpret_cast<const uint4*>(ptr);
-      const uint4 z = *reinterpret_cast<const uint4*>((const bf16*)a.aux + opx * a.ld_aux + nc);
-      const uint4 z2 = two ? *reinterpret_cast<const uint4*>((const bf16*)a.aux2 + opx * a.ld_aux2 + nc) : uint4{0u, 0u, 0u, 0u};
-      const unsigned mk = a.mbits[opx * (a.Ng >> 3) + (nc >> 3)];
-      const bf16* ob = reinterpret_cast<const bf16*>(&old);
-      const bf16* zb = reinterpret_cast<const bf16*>(&z);
-      const bf16* z2b = reinterpret_cast<const bf16*>(&z2);
-      bf16* nv = reinterpret_cast<bf16*>(&v);
+  for (int g0 = 0; g0 < NIT; g0 += GRP) {
+    uint4 oldv[GRP], zv[POST == 3 ? GRP : 1], z2v[POST == 3 ? GRP : 1];
+    unsigned mkv[POST == 3 ? GRP : 1];
+    if (POST == 3 || a.accumulate) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const bf16 sm = (bf16)((float)nv[e] + (float)ob[e]);  // == the accumulating store
-        const float d = ((mk >> e) & 1u) ? (float)sm : 0.f;
-        nv[e] = (bf16)d;
-        q3[0][e] += d;
-        q3[1][e] = fmaf(d, ((float)zb[e] - mu3[0][e]) * iv3[0][e], q3[1][e]);
-        if (two) q3[2][e] = fmaf(d, ((float)z2b[e] - mu3[1][e]) * iv3[1][e], q3[2][e]);
+      for (int j = 0; j < GRP; ++j) {
+        const int r = (g0 + j) * RPI + rsub;
+        const bool ok = r < cnt && nc < a.Ng;
+        const long opx = ok ? out_pix(row0 + r) : 0;
+        oldv[j] = ok ? *reinterpret_cast<const uint4*>((const bf16*)a.y + opx * a.ldy + nc) : uint4{0u, 0u, 0u, 0u};
+        if constexpr (POST == 3) {
+          zv[j] = ok ? *reinterpret_cast<const uint4*>((const bf16*)a.aux + opx * a.ld_aux + nc) : uint4{0u, 0u, 0u, 0u};
+          z2v[j] = ok && two ? *reinterpret_cast<const uint4*>((const bf16*)a.aux2 + opx * a.ld_aux2 + nc)
+                             : uint4{0u, 0u, 0u, 0u};
+          mkv[j] = ok ? (unsigned)a.mbits[opx * (a.Ng >> 3) + (nc >> 3)] : 0u;
+        }
       }
-    } else if (a.accumulate) {  // dx += dgrad (two bf16 tensors summed in fp32, like autograd's accumulation)
-      const uint4 old = *reinterpret_cast<const uint4*>(ptr);
-      const bf16* ob = reinterpret_cast<const bf16*>(&old);
-      bf16* nv = reinterpret_cast<bf16*>(&v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) nv[e] = (bf16)((float)nv[e] + (float)ob[e]);
     }
-    *reinterpret_cast<uint4*>(ptr) = v;
+#pragma unroll
+    for (int j = 0; j < GRP; ++j) {
+      const int r = (g0 + j) * RPI + rsub;
+      if (r >= cnt || nc >= a.Ng) continue;
+      const long opx = out_pix(row0 + r);
+      bf16* ptr = (bf16*)a.y + opx * a.ldy + nc;
+      uint4 v = *reinterpret_cast<const uint4*>(tl + r * LROW + ck * 16);
+      if constexpr (POST == 3) {
+        const uint4 old = oldv[j], z = zv[j], z2 = z2v[j];
+        const unsigned mk = mkv[j];
+        const bf16* ob = reinterpret_cast<const bf16*>(&old);
+        const bf16* zb = reinterpret_cast<const bf16*>(&z);
+        const bf16* z2b = reinterpret_cast<const bf16*>(&z2);
+        bf16* nv = reinterpret_cast<bf16*>(&v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bf16 sm = (bf16)((float)nv[e] + (float)ob[e]);  // == the accumulating store
+          const float d = ((mk >> e) & 1u) ? (float)sm : 0.f;
+          nv[e] = (bf16)d;
+          q3[0][e] += d;
+          q3[1][e] = fmaf(d, ((float)zb[e] - mu3[0][e]) * iv3[0][e], q3[1][e]);
+          if (two) q3[2][e] = fmaf(d, ((float)z2b[e] - mu3[1][e]) * iv3[1][e], q3[2][e]);
+        }
+      } else if (a.accumulate) {  // dx += dgrad (two bf16 tensors summed in fp32, like autograd's accumulation)
+        const uint4 old = oldv[j];
+        const bf16* ob = reinterpret_cast<const bf16*>(&old);
+        bf16* nv = reinterpret_cast<bf16*>(&v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) nv[e] = (bf16)((float)nv[e] + (float)ob[e]);
+      }
+      *reinterpret_cast<uint4*>(ptr) = v;
+    }
   }
   if constexpr (POST == 3) {
     // sum over the lanes of this chunk column (same ck), then one lane per chunk writes the wave's
