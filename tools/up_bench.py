@@ -35,6 +35,9 @@ for (H, C) in [(256, 64), (128, 128), (64, 256), (32, 512)]:
     dx = torch.empty_like(x)
     tb = timeit(lambda: lib.upsample2x_bwd_relu(DT_BF16, y.data_ptr(), C, N, H, H, C, 1, x.data_ptr(), C,
                                                 dx.data_ptr(), C, part.data_ptr(), rows, st))
+    out = torch.zeros(C, device=DEV)
+    tc = timeit(lambda: lib.colsum_rows(part.data_ptr(), C, rows, 0, out.data_ptr(), 1, st))
     fb = (x.numel() + y.numel()) * 2
     bb = (y.numel() + 2 * x.numel()) * 2
-    print(f"H={H:4d} C={C:4d}  fwd {tf:7.1f} us {fb / tf / 1e3:5.2f} GB/s   bwd_relu {tb:7.1f} us {bb / tb / 1e3:5.2f} GB/s")
+    print(f"H={H:4d} C={C:4d}  fwd {tf:7.1f} us {fb / tf / 1e3:5.2f} GB/s   bwd_relu {tb:7.1f} us {bb / tb / 1e3:5.2f} GB/s"
+          f"   colsum_rows (G={rows}) {tc:6.1f} us")

@@ -23,13 +23,15 @@ constexpr int VE = 16 / sizeof(T);
 // Per-channel reductions of row partials part[g][q][C] (G row tiles, q = 0 .. nq-1) -- the BN
 // finalizes of the forward statistics and of the fused data-gradient post-ops.  They sit on the
 // compute stream between a producer and its consumer, so they are latency kernels: one wave per
-// channel (NWV = 1, four channels per block, no barrier) when G <= 512, a block of NWV = 4 or 16
-// waves per channel above that; every lane issues all its loads (kFinRPL rows x nq) before it adds,
-// and the lanes' fp64 partials are combined in a fixed order (deterministic).
+// channel (NWV = 1, four channels per block, no barrier) when G <= 512, a block of NWV = 4 waves per
+// channel above that; every lane issues all its loads (kFinRPL rows x nq) before it adds, and the
+// lanes' fp64 partials are combined in a fixed order (deterministic).  Never 1024-thread blocks: beside
+// the weight-gradient stream's persistent kernels such a block found no CU until they drained (a
+// 12 us colsum took 235 us in the bench trace); 256-thread blocks ran at their isolated speed.
 // ------------------------------------------------------------------------------------------
 constexpr int kFinRPL = 8;  // rows per lane per round
 
-static inline int fin_waves(int G) { return G > 2048 ? 16 : G > 512 ? 4 : 1; }
+static inline int fin_waves(int G) { return G > 512 ? 4 : 1; }
 static inline unsigned fin_blocks(int C, int nwv) { return nwv > 1 ? (unsigned)C : (unsigned)ceil_div(C, 4); }
 static inline unsigned fin_threads(int nwv) { return nwv > 1 ? 64u * nwv : 256u; }
 // launch KERNEL<nwv> for the row count G with the finalize geometry
@@ -37,8 +39,7 @@ static inline unsigned fin_threads(int nwv) { return nwv > 1 ? 64u * nwv : 256u;
   do {                                                                                                     \
     const int nwv_ = fin_waves(G);                                                                         \
     const dim3 grid_(fin_blocks(C, nwv_)), block_(fin_threads(nwv_));                                      \
-    if (nwv_ == 16) hipLaunchKernelGGL(KERNEL<16>, grid_, block_, 0, (hipStream_t)(stream), __VA_ARGS__);  \
-    else if (nwv_ == 4) hipLaunchKernelGGL(KERNEL<4>, grid_, block_, 0, (hipStream_t)(stream), __VA_ARGS__); \
+    if (nwv_ == 4) hipLaunchKernelGGL(KERNEL<4>, grid_, block_, 0, (hipStream_t)(stream), __VA_ARGS__); \
     else hipLaunchKernelGGL(KERNEL<1>, grid_, block_, 0, (hipStream_t)(stream), __VA_ARGS__);              \
   } while (0)
 
