@@ -49,9 +49,11 @@ class Node:
     produced it, so that a sole consumer conv can apply that op's backward mask and first reduction
     in its data-gradient epilogue (``fused`` then holds the partials for the producer's backward).
     ``lazy`` (a BNState): the node stands for relu(BN(data)) that was never stored -- ``data`` is the
-    BN input and the consuming conv applies BN-ReLU on load (``bn(..., lazy=True)``)."""
+    BN input and the consuming conv applies BN-ReLU on load (``bn(..., lazy=True)``).  ``kpad`` (Kp > K):
+    the gradient buffer is allocated as the first K channels of a zeroed Kp-channel tensor (``gpad``),
+    which the producing conv's padded-K backward reads as it is (see conv)."""
 
-    __slots__ = ("data", "grad", "need_grad", "uses", "fuse", "fused", "lazy", "head", "mbits")
+    __slots__ = ("data", "grad", "need_grad", "uses", "fuse", "fused", "lazy", "head", "mbits", "kpad", "gpad")
 
     def __init__(self, data, need_grad=True):
         self.data = data
@@ -63,6 +65,8 @@ class Node:
         self.lazy = None
         self.head = None  # (head Conv2d, fp32 logits) computed by the producing conv's epilogue
         self.mbits = None  # packed ReLU mask of data (unetseg_conv2d_fwd_mask), read by post 4
+        self.kpad = 0
+        self.gpad = None
 
     @property
     def shape(self):
@@ -277,7 +281,12 @@ def flush_point(ctx, where):
 def gbuf(ctx, node):
     """gradient buffer of node: (tensor, accumulate flag)"""
     if node.grad is None:
-        node.grad = ctx.empty(*node.data.shape)
+        if node.kpad:
+            shape = node.data.shape
+            node.gpad = torch.zeros(*shape[:-1], node.kpad, dtype=ctx.tdtype, device=ctx.device)
+            node.grad = node.gpad[..., :shape[-1]]
+        else:
+            node.grad = ctx.empty(*node.data.shape)
         return node.grad, 0
     return node.grad, 1
 
@@ -456,6 +465,8 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                                pad, P(b), int(relu), P(y), ldp(y), P(st[0] if st else None), ctx.stream)
     out = Node(y)
     out.head = head
+    if PAD_K and ctx.dt == DT_BF16 and R == 1 and S == 1 and K % 64 != 0 and K % 8 == 0 and x2 is None and stride == 1:
+        out.kpad = -(-K // 64) * 64
     if mbits is not None:
         out.mbits = mbits
     if relu:
@@ -485,13 +496,18 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
             dY = dA
         # 1x1 convs with a narrow output (the attention gates' theta/phi, K = inter = 32): both
         # gradient GEMMs reduce over or produce K, below the fast tiles' 64-channel granule, so dY
-        # is zero-padded to Kp channels once and the padded rows of dW / columns of W^T are zero
+        # is zero-padded to Kp channels and the padded rows of dW / columns of W^T are zero.  The
+        # consumer's backward wrote dY into the zeroed padded buffer (out.kpad, gbuf); a gradient
+        # adopted from elsewhere is copied into one
         Kp = K
-        if PAD_K and ctx.dt == DT_BF16 and R == 1 and S == 1 and K % 64 != 0 and K % 8 == 0 and x2 is None and stride == 1:
-            Kp = -(-K // 64) * 64
-            dYp = torch.zeros(N, Pq, Qq, Kp, dtype=ctx.tdtype, device=dev)
-            lib.add(ctx.dt, P(dY), ldp(dY), P(dYp), Kp, M, K, ctx.stream)
-            dY = dYp
+        if out.kpad:
+            Kp = out.kpad
+            if out.gpad is not None and dY is out.grad:
+                dY = out.gpad
+            else:
+                dYp = torch.zeros(N, Pq, Qq, Kp, dtype=ctx.tdtype, device=dev)
+                lib.add(ctx.dt, P(dY), ldp(dY), P(dYp), Kp, M, K, ctx.stream)
+                dY = dYp
         cin = C1 + C2
 
         def launch_wgrad(serial=False):
