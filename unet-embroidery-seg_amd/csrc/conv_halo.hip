@@ -48,7 +48,30 @@ __device__ __forceinline__ void bstore32(__amdgpu_buffer_rsrc_t r, unsigned off,
   asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
 }
 
-template <int TH, int NW, int POST, int EPI>
+// wait for half h of the HS pipeline and join the block: the vector-memory operations issued after
+// half h's DMA may stay in flight -- the next two halves (D instructions each) and the aux loads (NA)
+// / output stores (NS) issued in between (exact for the first three halves, whose predecessors are
+// fewer).  A count below the true one only waits longer.
+template <int D, int NA, int NS>
+__device__ __forceinline__ void hs_wait(int h) {
+  if (h == 0)
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * D) : "memory");
+  else if (h == 1)
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * D + NA) : "memory");
+  else if (h == 2)
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * D + NA + NS) : "memory");
+  else if (h & 1)
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * D + 2 * NA + NS) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * D + NA + 2 * NS) : "memory");
+}
+
+// HS: the input arrives as 32-channel half tiles through FOUR half stages (the same 85 KiB as two
+// whole-tile stages): a half tile's DMA is issued three half-steps before it is consumed, so 64 KiB
+// stay in flight per CU instead of the 0-43 KiB of the double-buffered whole tiles, whose wait at
+// every tile end left the waves parked (the 512^2 layers ran at ~2.7 TB/s).  Half-stage rows are
+// 64 B (4 chunks, chunk ^ (bit 2 of the pixel) << 1: conflict-free 16-pixel reads from any start).
+template <int TH, int NW, int POST, int EPI, bool HS = false>
 __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_w, int tiles_h, int n_sp, int G_per,
                                                         unsigned y_bytes) {
   constexpr bool kDyn = (EPI & kEpiDyn) != 0;
@@ -151,6 +174,49 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     }
   };
 
+  // ---- half-stage geometry (HS): 4 chunks per halo pixel, HI2 DMA instructions per wave (the last
+  // one only for the waves whose slots exist: waves 0..5 issue HI2, the rest HI2 - 1) ----
+  constexpr int HCH2 = HP * 4;
+  constexpr int HI2 = (HCH2 + 64 * NW - 1) / (64 * NW);
+  constexpr int LASTW = (HCH2 - (HI2 - 1) * 64 * NW + 63) / 64;  // waves with slots in the last instruction
+  static_assert(!HS || (HCH2 % 64 != 0 || true), "");
+  unsigned hoff2[HS ? HI2 : 1], hflag2[HS ? HI2 : 1];
+  if constexpr (HS) {
+#pragma unroll
+    for (int i = 0; i < HI2; ++i) {
+      const int idx = (i * NW + wid) * 64 + lane;
+      const int hp = idx >> 2, q = idx & 3;
+      const int hr = hp / (HW_TW + 2), hc = hp % (HW_TW + 2);
+      hoff2[i] = (unsigned)(hr * a.W + hc) * (unsigned)a.ldc1b + (unsigned)((q ^ (((hp >> 2) & 1) << 1)) * 16);
+      hflag2[i] = idx >= HCH2 ? 16u : (hr == 0 ? 1u : 0u) | (hr == TH + 1 ? 2u : 0u) | (hc == 0 ? 4u : 0u) | (hc == HW_TW + 1 ? 8u : 0u);
+    }
+  }
+  const bool last_dma = wid < LASTW;  // this wave issues the last half-stage instruction
+  // half h = 2 t + kk (input channels 32 kk .. 32 kk + 31 of tile t) into half stage `stage`; halves
+  // past this block's tiles load nothing (out of range) but are issued, so every wave's count is fixed
+  auto issue_half = [&](int h, int stage) {
+    const int t = h >> 1;
+    const bool live = t < my_tiles;
+    const int sp = live ? slot + t * G_per : slot;
+    const int tw = sp % tiles_w, rest = sp / tiles_w;
+    const int th = rest % tiles_h, nb = rest / tiles_h;
+    const int h0 = th * TH, w0 = tw * HW_TW;
+    const unsigned base = __builtin_amdgcn_readfirstlane(lds_addr(hl + stage * HCH2));
+    const unsigned hb = __builtin_amdgcn_readfirstlane((unsigned)((nb * a.H + h0 - 1) * a.W + w0 - 1) * (unsigned)a.ldc1b +
+                                                       (unsigned)(h & 1) * 64u);
+    const unsigned kill = __builtin_amdgcn_readfirstlane(16u | (h0 == 0 ? 1u : 0u) | (h0 + TH >= a.H ? 2u : 0u) |
+                                                         (w0 == 0 ? 4u : 0u) | (w0 + HW_TW >= a.W ? 8u : 0u));
+#pragma unroll
+    for (int i = 0; i < HI2; ++i) {
+      const unsigned off = (!live || (hflag2[i] & kill)) ? kOOB : hb + hoff2[i];
+      if (i < HI2 - 1) {
+        dma16(rx, base + (unsigned)((i * NW + wid) * 1024), off);
+      } else if (last_dma) {
+        if (hflag2[i] != 16u) dma16(rx, base + (unsigned)((i * NW + wid) * 1024), off);
+      }
+    }
+  };
+
   f32x4 acc[FC][FP];
   // data-gradient post-op (a.post): running per-lane sums of the masked gradient over all tiles of
   // this block, reduced once at the end into ppart[blockIdx.x][2][Ng]
@@ -159,8 +225,20 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   for (int c = 0; c < FC; ++c)
 #pragma unroll
     for (int e = 0; e < 4; ++e) pq0[c][e] = pq1[c][e] = 0.f;
-  if (my_tiles > 0) issue_halo(0, 0);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  constexpr int NA_ = POST == 4 ? FP : POST ? FP * FC : 0;                   // aux loads per tile
+  constexpr int NS_ = FP * FC + FP * HK + (kMask ? FP : 0);                   // output stores per tile
+  auto half_wait = [&](int h) {
+    if (last_dma) hs_wait<HI2, NA_, NS_>(h);
+    else hs_wait<HI2 - 1, NA_, NS_>(h);
+  };
+  if constexpr (HS) {
+    issue_half(0, 0);
+    issue_half(1, 1);
+    issue_half(2, 2);
+  } else {
+    if (my_tiles > 0) issue_halo(0, 0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
 
   // halo tap offsets (uniform): jt -> (dh, dw)
   const int dh0 = a.dh0, dhs = a.dhs, dw0 = a.dw0, dws = a.dws;
@@ -183,7 +261,12 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
 
   for (int t = 0; t < my_tiles; ++t) {
     const int stage = t & 1;
-    if (t + 1 < my_tiles) issue_halo(t + 1, stage ^ 1);
+    if constexpr (HS) {
+      half_wait(2 * t);
+      issue_half(2 * t + 3, (2 * t + 3) & 3);
+    } else {
+      if (t + 1 < my_tiles) issue_halo(t + 1, stage ^ 1);
+    }
     // post-op: this tile's aux values are loaded now, so their latency hides under the tap loop
     uint2 zr[FC][FP];
     uint2 zb[FP];  // POST 4: the 8 mask bytes (64 channels) of this lane's pixel
@@ -216,34 +299,72 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     for (int c = 0; c < FC; ++c)
 #pragma unroll
       for (int p = 0; p < FP; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const uint4* hs = hl + stage * HCH;
-#pragma unroll
-    for (int jt = 0; jt < 9; ++jt) {
-      const int jr = jt / 3, js = jt - jr * 3;
-      const int dh = dh0 + dhs * jr, dw = dw0 + dws * js;
+    if constexpr (HS) {
+      // half kk = input channels 32 kk .. 32 kk + 31: all nine taps, then the next half
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
+        if (kk == 1) {
+          half_wait(2 * t + 1);
+          issue_half(2 * t + 4, (2 * t + 4) & 3);
+        }
+        const uint4* hs2 = hl + ((2 * t + kk) & 3) * HCH2;
         const int ch = kk * 4 + kg;
-        bf16x8 wf[FC], pf[FP];
 #pragma unroll
-        for (int c = 0; c < FC; ++c) {
-          const int row = jt * 64 + c * 16 + j16;
-          uint4 v = wl[row * 8 + swz8(row, ch)];
-          wf[c] = *reinterpret_cast<bf16x8*>(&v);
+        for (int jt = 0; jt < 9; ++jt) {
+          const int jr = jt / 3, js = jt - jr * 3;
+          const int dh = dh0 + dhs * jr, dw = dw0 + dws * js;
+          bf16x8 wf[FC], pf[FP];
+#pragma unroll
+          for (int c = 0; c < FC; ++c) {
+            const int row = jt * 64 + c * 16 + j16;
+            uint4 v = wl[row * 8 + swz8(row, ch)];
+            wf[c] = *reinterpret_cast<bf16x8*>(&v);
+          }
+#pragma unroll
+          for (int p = 0; p < FP; ++p) {
+            const int r = wid * RPW + p / (HW_TW / 16);
+            const int col = (p % (HW_TW / 16)) * 16 + j16;
+            const int hp = (r + 1 + dh) * (HW_TW + 2) + col + 1 + dw;
+            uint4 v = hs2[hp * 4 + (kg ^ (((hp >> 2) & 1) << 1))];
+            pf[p] = *reinterpret_cast<bf16x8*>(&v);
+          }
+#pragma unroll
+          for (int c = 0; c < FC; ++c)
+#pragma unroll
+            for (int p = 0; p < FP; ++p)
+              acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], pf[p], acc[c][p], 0, 0, 0);
         }
+      }
+    } else {
+      const uint4* hs = hl + stage * HCH;
 #pragma unroll
-        for (int p = 0; p < FP; ++p) {
-          const int r = wid * RPW + p / (HW_TW / 16);
-          const int col = (p % (HW_TW / 16)) * 16 + j16;
-          const int hp = (r + 1 + dh) * (HW_TW + 2) + col + 1 + dw;
-          uint4 v = hs[hp * 8 + swzh(hp, ch)];
-          pf[p] = *reinterpret_cast<bf16x8*>(&v);
+      for (int jt = 0; jt < 9; ++jt) {
+        const int jr = jt / 3, js = jt - jr * 3;
+        const int dh = dh0 + dhs * jr, dw = dw0 + dws * js;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int ch = kk * 4 + kg;
+          bf16x8 wf[FC], pf[FP];
+#pragma unroll
+          for (int c = 0; c < FC; ++c) {
+            const int row = jt * 64 + c * 16 + j16;
+            uint4 v = wl[row * 8 + swz8(row, ch)];
+            wf[c] = *reinterpret_cast<bf16x8*>(&v);
+          }
+#pragma unroll
+          for (int p = 0; p < FP; ++p) {
+            const int r = wid * RPW + p / (HW_TW / 16);
+            const int col = (p % (HW_TW / 16)) * 16 + j16;
+            const int hp = (r + 1 + dh) * (HW_TW + 2) + col + 1 + dw;
+            uint4 v = hs[hp * 8 + swzh(hp, ch)];
+            pf[p] = *reinterpret_cast<bf16x8*>(&v);
+          }
+#pragma unroll
+          for (int c = 0; c < FC; ++c)
+#pragma unroll
+            for (int p = 0; p < FP; ++p)
+              acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], pf[p], acc[c][p], 0, 0, 0);
         }
-#pragma unroll
-        for (int c = 0; c < FC; ++c)
-#pragma unroll
-          for (int p = 0; p < FP; ++p)
-            acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], pf[p], acc[c][p], 0, 0, 0);
       }
     }
 
@@ -415,10 +536,13 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
 #pragma unroll
       for (int p = 0; p < FP; ++p) bstore64(rmb, kg == 0 ? mko[p] : kOOB, uint2{mkx[p], mky[p]});
     // next halo landed (all but this tile's stores retired) and every wave is done with both the
-    // current stage (WAR for the DMA after next) and `red`
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(FP * FC + FP * HK + (kMask ? FP : 0)) : "memory");
+    // current stage (WAR for the DMA after next) and `red` (HS: the next half's wait does both)
+    if constexpr (!HS)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(FP * FC + FP * HK + (kMask ? FP : 0)) : "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // HS: the past-the-end halves are still landing in the stages of other waves
+  if constexpr (HS) asm volatile("s_barrier" ::: "memory");
   if (POST) {
     // lanes -> waves -> block: ppart[blockIdx.x][2][Ng] for this block's 64 output channels (the
     // halo stages are free now: every wave has passed the last tile's barrier)
@@ -1270,8 +1394,8 @@ bool halo3_ok(const FastTNArgs& a) {
   return true;
 }
 
-template <int TH, int NW, int POST, int EPI>
-static int launch_halo3_cfg(const FastTNArgs& a, hipStream_t st) {
+template <int TH, int NW, int POST, int EPI, bool HS>
+static int launch_halo3_hs(const FastTNArgs& a, hipStream_t st) {
   const int tiles_w = a.wc / HW_TW, tiles_h = a.hc / TH;
   const int n_img = a.M / (a.hc * a.wc);
   const int n_sp = n_img * tiles_h * tiles_w;
@@ -1283,14 +1407,24 @@ static int launch_halo3_cfg(const FastTNArgs& a, hipStream_t st) {
   const size_t lds = halo_lds_bytes<TH, NW>(HK);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_kernel<TH, NW, POST, EPI>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo3_kernel<TH, NW, POST, EPI, HS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const unsigned y_bytes = (unsigned)((long)a.M * a.ldy * 2);
-  hipLaunchKernelGGL((halo3_kernel<TH, NW, POST, EPI>), dim3(ntn * G_per), dim3(64 * NW), lds, st, a, tiles_w, tiles_h, n_sp,
-                     G_per, y_bytes);
+  hipLaunchKernelGGL((halo3_kernel<TH, NW, POST, EPI, HS>), dim3(ntn * G_per), dim3(64 * NW), lds, st, a, tiles_w, tiles_h,
+                     n_sp, G_per, y_bytes);
   return 0;
+}
+
+// the half-stage pipeline (HS) for the 8-wave kernels (UNETSEG_HALO_HS=0: the whole-tile double buffer)
+template <int TH, int NW, int POST, int EPI>
+static int launch_halo3_cfg(const FastTNArgs& a, hipStream_t st) {
+  static const bool hs = !getenv("UNETSEG_HALO_HS") || atoi(getenv("UNETSEG_HALO_HS")) != 0;
+  if constexpr (NW == 8) {
+    if (hs) return launch_halo3_hs<TH, NW, POST, EPI, true>(a, st);
+  }
+  return launch_halo3_hs<TH, NW, POST, EPI, false>(a, st);
 }
 
 // blocks (= post-op partial rows) of a launch_halo3 call
