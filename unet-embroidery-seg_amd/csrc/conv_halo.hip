@@ -1582,10 +1582,12 @@ int halo3_wgrad_splits(const HaloWgradArgs& a) {
   // seconds per (8 x 32)-pixel tile of one block (the makespan model; UNETSEG_HALO_WG_TILE_US overrides)
   static const double tile_s = (getenv("UNETSEG_HALO_WG_TILE_US") ? atof(getenv("UNETSEG_HALO_WG_TILE_US")) : 1.0) * 1e-6;
   // with several (cout, cin) groups, the blocks of one slot in different groups walk the same spatial
-  // tiles in step; G a multiple of 8 puts them on one XCD (block b runs on XCD b % 8), so a tile's dY
-  // (read by every cin group) or X halo (every cout group) comes from that XCD's L2 after the first
-  // read instead of from HBM (UNETSEG_HALO_WG_XCD=0: any G)
-  static const bool xcd = !getenv("UNETSEG_HALO_WG_XCD") || atoi(getenv("UNETSEG_HALO_WG_XCD")) != 0;
+  // tiles in step; G a multiple of 8 would put them on one XCD (block b runs on XCD b % 8), so a tile's
+  // dY or X halo came from that XCD's L2 after the first read -- but it forces G >= 8 and with it
+  // G slabs of split-K partials (the 32^2 concat conv: 453 MB written and re-read by the reduce).  Any
+  // G measured better in the step (round 4, three interleaved repeats: C2 979.8 vs 976.2 img/s, C4
+  // 423.5 vs 418.8, C5 783.6 vs 765.9, allocator peak 8.11 vs 8.39 GiB); UNETSEG_HALO_WG_XCD=1 restores it
+  static const bool xcd = getenv("UNETSEG_HALO_WG_XCD") && atoi(getenv("UNETSEG_HALO_WG_XCD")) != 0;
   const int step = (xcd && groups > 1) ? 8 : 1;
   for (int g = step; g <= maxg && g <= n_sp; g += step) {
     if (slab * g > 768.0 * (1 << 20)) break;  // workspace cap
