@@ -420,12 +420,15 @@ def main():
                 continue
             m2, _, run2, _, _ = build_step(name, batch, args.size, loss_name, dev, rank, world, args)
             torch.cuda.reset_peak_memory_stats(dev)
-            w2, med2, _, _, _ = timed(run2, args.steps, args.warmup, world, dev)
+            # at least 30 timed steps: a B=8 step is ~10 ms, and over 10 steps one host hiccup of a few
+            # ms moved the C5 line by 10-20 % between otherwise identical runs
+            k2 = max(args.steps, 30)
+            w2, med2, _, _, _ = timed(run2, k2, args.warmup, world, dev)
             peak2 = torch.cuda.max_memory_allocated(dev) / 2 ** 30
-            ips = batch * world * args.steps / w2
+            ips = batch * world * k2 / w2
             configs[tag] = {"workload": f"{name} {args.size}x{args.size}, per-GPU batch {batch}, "
                                         f"{loss_name}{' + ce' if name == 'multitask_unet' else ''} + Adam",
-                            "value": round(ips, 2), "unit": "images/s", "ms_per_step": round(1000.0 * w2 / args.steps, 3),
+                            "value": round(ips, 2), "unit": "images/s", "steps": k2, "ms_per_step": round(1000.0 * w2 / k2, 3),
                             "median_gpu_ms_per_step": round(med2, 3), "peak_alloc_gib": round(peak2, 2),
                             "step_mfma_frac": round(ips / world * GFLOP_PER_IMG[name] / 1e3 / PEAK_BF16_TFLOPS, 4)}
             del m2, run2
