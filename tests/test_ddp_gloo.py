@@ -121,3 +121,41 @@ def test_grad_buckets_average_matches_oracle_shards(reduce_dtype):
             scale = torch.maximum(torch.from_numpy(res[0][1][n]).abs(), torch.from_numpy(res[1][1][n]).abs())
             assert ((got0 - want).abs() <= 8 * 2.0 ** -9 * scale + 1e-30).all(), n
         torch.testing.assert_close(got1, got0, rtol=0, atol=0)
+
+
+def _soft_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from unetseg_hip import losses
+        if rank == 1:  # only rank 1's loss saw a soft seg target
+            losses._poison(torch.tensor(True), torch.zeros(3))
+        raised = []
+        for _ in range(2):  # the second epoch is clean on both ranks
+            try:
+                losses.raise_if_soft_targets("cpu")
+                raised.append(False)
+            except ValueError:
+                raised.append(True)
+        out_q.put((rank, raised))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_soft_target_flag_raises_on_every_rank():
+    """a soft label seen by one rank makes EVERY rank raise at the epoch check (the flag is
+    all-reduced with MAX), instead of the clean ranks blocking in the next collective; the flag is
+    cleared afterwards"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_soft_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res == {0: [True, False], 1: [True, False]}, res

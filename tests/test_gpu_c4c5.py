@@ -312,11 +312,11 @@ def test_attention_unet_train_step_512_b8_bf16():
     EMU_FRAC of amp-vs-f32 (max and mean); HIP-vs-f32 no worse than 1.5x amp-vs-f32; loss within 2x
     amp's deviation + 1e-3 relative; gradients: median relative L2 over tensors no worse than 1.5x
     amp's, and every tensor of >= 64 elements that bf16 storage moves by < 5 % held individually (1.5x
-    amp + 1e-3).  Single-value tensors (the gates' psi conv bias and BN affine) are left to the
-    teacher-forced per-block check (tests/test_gpu_teacher.py, every parameter at 1e-3 relative L2):
-    end to end, their error is one draw of the chaotic bf16 rounding noise, not an average -- with the
-    halo3 half-tile pipeline's accumulation order, up2's psi BN weight moved 0.055 against amp's
-    0.031 while every tensor of the step passed the teacher-forced bounds."""
+    amp + 1e-3).  Single-value tensors (the gates' psi conv bias and BN affine) are held at 3x amp +
+    1e-2: end to end, their error is one draw of the chaotic bf16 rounding noise, not an average --
+    with the halo3 half-tile pipeline's accumulation order, up2's psi BN weight moved 0.055 against
+    amp's 0.031 while every tensor of the step passed the teacher-forced per-block check
+    (tests/test_gpu_teacher.py), which holds them tightly."""
     from oracle import ref_cpu
     from oracle.weights import make_torch_state
     from unetseg_hip.losses import binary_segmentation_loss
@@ -359,15 +359,22 @@ def test_attention_unet_train_step_512_b8_bf16():
     assert e_f32[0] <= 1.5 * e_amp[0] and e_f32[1] <= 1.5 * e_amp[1], (e_f32, e_amp)
     assert abs(hip_loss - f32[0]) <= 2 * abs(runs["amp"][0] - f32[0]) + 1e-3 * abs(f32[0])
     assert gh[len(gh) // 2] <= 1.5 * ga[len(ga) // 2], (gh[len(gh) // 2], ga[len(ga) // 2])
-    well = 0
+    well = small = 0
     for k, v in f32[2].items():
         ra = _rel_l2(runs["amp"][2][k], v)
-        if v.double().norm().item() > 0 and ra < 0.05 and v.numel() >= 64:
+        if v.double().norm().item() == 0:
+            continue
+        rh = _rel_l2(hip_grads[k], v)
+        if v.numel() < 64:
+            # the gates' psi conv bias / psi BN affine: one draw of the bf16 rounding noise each, so a
+            # looser bound than the large tensors' -- but a regression in a gate scalar still fails here
+            small += 1
+            assert rh <= 3.0 * ra + 1e-2, (k, rh, ra)
+        elif ra < 0.05:
             well += 1
-            rh = _rel_l2(hip_grads[k], v)
             assert rh <= 1.5 * ra + 1e-3, (k, rh, ra)
-    print(f"well-conditioned gradient tensors checked individually: {well}")
-    assert well >= 10
+    print(f"gradient tensors checked individually: {well} well-conditioned, {small} single-value gate scalars")
+    assert well >= 10 and small >= 8
 
 
 def test_unet_plain_128_b2_golden(golden_dir):

@@ -170,16 +170,28 @@ _FAST = None
 
 def _fast():
     """the CPython fast-call binding (gen_fastcall.py, built next to the library by the csrc Makefile):
-    the same entry points without ctypes' per-call conversion cost; None when absent, when the
-    library comes from UNETSEG_LIB_PATH (A/B builds: the binding links the in-tree library) or with
-    UNETSEG_NO_FASTCALL=1"""
+    the same entry points without ctypes' per-call conversion cost; None when absent or with
+    UNETSEG_NO_FASTCALL=1.  With UNETSEG_LIB_PATH (A/B builds) the binding is taken from that library's
+    directory (``make OUT=<dir>/libunetseg_hip.so`` builds both there; its rpath links the library beside
+    it), so an A/B arm runs at the production host cost -- or not at all when that directory has none."""
     global _FAST
     if _FAST is None:
         _FAST = False
-        if os.environ.get("UNETSEG_LIB_PATH") is None and os.environ.get("UNETSEG_NO_FASTCALL", "0") != "1":
+        if os.environ.get("UNETSEG_NO_FASTCALL", "0") != "1":
             try:
-                from . import _unetseg_fast
-                _FAST = _unetseg_fast
+                if os.environ.get("UNETSEG_LIB_PATH") is None:
+                    from . import _unetseg_fast
+                    _FAST = _unetseg_fast
+                else:
+                    import glob
+                    import importlib.util
+                    cand = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(LIB_PATH)),
+                                                         "_unetseg_fast*.so")))
+                    if cand and os.path.basename(LIB_PATH) == "libunetseg_hip.so":
+                        spec = importlib.util.spec_from_file_location("_unetseg_fast", cand[0])
+                        mod = importlib.util.module_from_spec(spec)
+                        spec.loader.exec_module(mod)
+                        _FAST = mod
             except ImportError:
                 pass
     return _FAST or None

@@ -61,14 +61,31 @@ def raise_if_soft_targets(device=None):
     (one host read; the loss itself was NaN-poisoned on the device).  The reference's
     BCEWithLogitsLoss would train on such soft labels (model/unet_multitask.py:131); the fused
     0/1 kernels cannot, so the data error is reported instead of training on NaN silently.  The
-    multitask train / eval loops call this once per epoch / evaluation."""
-    devs = [torch.device(device)] if device is not None else list(_SOFT_SEEN)
+    multitask train / eval loops call this once per epoch / evaluation.  Under data parallelism the
+    flag is all-reduced (MAX) first, so every rank raises together instead of the others blocking in
+    the next collective (every rank must call this, as the loops do)."""
+    import torch.distributed as dist
+
+    dp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    if device is not None:
+        devs = [torch.device(device)]
+    elif dp:  # exactly one collective per call on every rank: this rank's device
+        devs = [torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")]
+    else:
+        devs = list(_SOFT_SEEN)
     for d in devs:
         if d.type == "cuda" and d.index is None:
             d = torch.device("cuda", torch.cuda.current_device())
         flag = _SOFT_SEEN.get(d)
-        if flag is not None and bool(flag.item()):
-            flag.zero_()
+        seen = flag is not None and bool(flag.item())
+        if dp:
+            on_dev = dist.get_backend() == "nccl"
+            t = torch.tensor([int(seen)], dtype=torch.int32, device=d if on_dev else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            seen = bool(t.item())
+        if seen:
+            if flag is not None:
+                flag.zero_()
             raise ValueError("MultiTaskLoss: seg targets must be 0 or 1 (the fused BCE kernel takes binary "
                              "labels; a soft / out-of-range target was seen and the loss was set to NaN)")
 

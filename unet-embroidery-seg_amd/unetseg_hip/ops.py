@@ -32,12 +32,17 @@ def ldp(t):
 
 _QMEMO = {}
 
+#: dispatch switches the library reads on every call (not once per process): tests flip them
+#: in-process, so each is part of the query memo's key (conv.hip / conv_fast.hip / elem.hip getenv)
+_CALL_SWITCHES = ("UNETSEG_TN_NO_HALO_RING", "UNETSEG_TN_CFG", "UNETSEG_TN_CFG_NO23", "UNETSEG_NO_FAST",
+                  "UNETSEG_RED_TARGET", "UNETSEG_MAXPOOL_GENERIC")
+_ENV = os.environ
+
 
 def _q(name, *args):
     """a host-only shape query of the C ABI (tile counts, partial rows, workspace sizes), memoised: its
     result depends on the integer arguments only, so callers pass 0 for every pointer and the stream"""
-    # the one dispatch switch the library reads per call (tests flip it): part of the key
-    key = (name, os.environ.get("UNETSEG_TN_NO_HALO_RING")) + args
+    key = (name, tuple(map(_ENV.get, _CALL_SWITCHES))) + args
     v = _QMEMO.get(key)
     if v is None:
         v = _QMEMO[key] = getattr(lib, name)(*args)
