@@ -13,7 +13,9 @@ oracle (oracle/ref_cpu.py, fp32, the reference's op sequence) on the host on a b
 `configs` times BASELINE.json's other GPU configurations the same way in the same process (C4
 attention_unet B=8 at N=1, C5 multitask_unet B=8 BCE + CE at every N); `card` records the GPU's
 clocks / power in the middle of the timed region and its own bf16 GEMM and HBM copy rates, so a slow
-box can be told from a code change.  `median_gpu_ms_per_step` is the median of per-step HIP-event
+box can be told from a code change; every configuration also records its card state during its own
+timed steps and `host_enqueue_ms` (the host's cost of enqueueing one step with the GPU parked, after
+the timed region, N=1), so a host-bound rate can be told from a slow GPU.  `median_gpu_ms_per_step` is the median of per-step HIP-event
 times over the K timed steps.
 """
 from __future__ import annotations
@@ -231,6 +233,37 @@ def card_probe(dev):
     return res
 
 
+def _spin_rate(dev):
+    """torch.cuda._sleep cycles per millisecond on this card (one short calibrated spin)"""
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    torch.cuda._sleep(20_000_000)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    return 20_000_000 / max(e0.elapsed_time(e1), 1e-3)
+
+
+def host_enqueue_ms(run, dev, gpu_ms, steps=3):
+    """host cost of one step: the GPU is first parked on a spin kernel long enough to cover the
+    enqueue, so the launch queue never throttles the host; the wall time of enqueueing `steps` steps
+    (the Python op layer and the C-ABI calls of fwd + loss + bwd + Adam), per step.  A step whose
+    host cost approaches its GPU time is host-bound: its rate then depends on the box's CPU, not the
+    kernels.  Also the host's 1-minute load average, to tell a busy host from a code change."""
+    rate = _spin_rate(dev)
+    torch.cuda._sleep(int(rate * (steps * max(gpu_ms, 5.0) * 2.5 + 100.0)))
+    t0 = time.perf_counter()
+    for i in range(steps):
+        run(i)
+    host = (time.perf_counter() - t0) / steps * 1e3
+    torch.cuda.synchronize(dev)
+    try:
+        load = round(os.getloadavg()[0], 2)
+    except OSError:
+        load = None
+    return round(host, 3), load
+
+
 def build_step(model_name, batch, size, loss_name, dev, rank, world, args):
     """(model, step fn) of one configuration: synthetic batches resident in HBM, fused Adam with the
     per-bucket overlapped update, the RCCL bucket all-reduce when world > 1"""
@@ -362,6 +395,7 @@ def main():
     wall, median_ms, gpu_ms, loss, card_mid = timed(run, args.steps, args.warmup, world, dev,
                                                     sample=lambda: card_state(dev))
     peak_gib = torch.cuda.max_memory_allocated(dev) / 2 ** 30  # caching-allocator peak over warmup + timed steps
+    host_ms, host_load = host_enqueue_ms(run, dev, median_ms) if world == 1 else (None, None)
     ms_per_step = 1000.0 * wall / args.steps
     imgs_per_s = args.batch * world * args.steps / wall
     final_loss = float(loss.item())
@@ -423,13 +457,16 @@ def main():
             # at least 30 timed steps: a B=8 step is ~10 ms, and over 10 steps one host hiccup of a few
             # ms moved the C5 line by 10-20 % between otherwise identical runs
             k2 = max(args.steps, 30)
-            w2, med2, _, _, _ = timed(run2, k2, args.warmup, world, dev)
+            w2, med2, _, _, card2 = timed(run2, k2, args.warmup, world, dev,
+                                          sample=(lambda: card_state(dev)) if rank == 0 else None)
             peak2 = torch.cuda.max_memory_allocated(dev) / 2 ** 30
             ips = batch * world * k2 / w2
+            host2 = host_enqueue_ms(run2, dev, med2) if world == 1 else (None, None)
             configs[tag] = {"workload": f"{name} {args.size}x{args.size}, per-GPU batch {batch}, "
                                         f"{loss_name}{' + ce' if name == 'multitask_unet' else ''} + Adam",
                             "value": round(ips, 2), "unit": "images/s", "steps": k2, "ms_per_step": round(1000.0 * w2 / k2, 3),
                             "median_gpu_ms_per_step": round(med2, 3), "peak_alloc_gib": round(peak2, 2),
+                            "host_enqueue_ms": host2[0], "host_loadavg": host2[1], "card_during": card2,
                             "step_mfma_frac": round(ips / world * GFLOP_PER_IMG[name] / 1e3 / PEAK_BF16_TFLOPS, 4)}
             del m2, run2
             gc.collect()
@@ -460,6 +497,7 @@ def main():
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 3),
             "median_gpu_ms_per_step": round(median_ms, 3), "final_loss": round(final_loss, 5),
             "peak_alloc_gib": round(peak_gib, 2),
+            "host_enqueue_ms": host_ms, "host_loadavg": host_load,
             "hip_graph": use_graph, "overlap_adam": overlap, "params_in_sync": in_sync,
             "grad_reduce_dtype": ("bf16" if args.ddp_bf16 else "fp32") if world > 1 else None,
             "configs": configs, "card": card,

@@ -578,3 +578,48 @@ def test_bench_configs_covered(model_name, batch):
     stem = {"stem_fwd:tn128x64", "stem_fwd:stem_halo", "stem_wgrad:wgrad_ring64x256"}  # test_stem_bench_size
     missing = sorted(used - covered_keys() - stem)
     assert not missing, f"{model_name} B={batch}: configurations without a parity case: {missing}"
+
+
+@pytest.mark.parametrize("direction", ["fwd_relu", "fwd_stats", "post1", "dgrad"])
+def test_halo3_hs_repeat_bit_identical(direction):
+    """the halo3 half-tile pipeline's waits are hand-counted vmcnt values (conv_halo.hip
+    hs_wait); a count too high would let a tap read a half stage before its DMA landed -- a silent LDS
+    race.  The same 512^2 launch, three times in one process (and at 128^2 with several tiles per
+    block), must give bit-identical outputs."""
+    from unetseg_hip.lib import DT_BF16, lib
+    for shape in ((4, 512, 512, 64, 0, 64, 3, 1), (5, 128, 128, 64, 0, 64, 3, 1)):
+        N, H, W, C1, C2, K, R, s = shape
+        op = _Op(shape, RNG + 77)
+        wk, wt = op.packed()
+        st = _st()
+        x1, _ = op.x_parts()
+        dyh = _nhwc(op.dy)
+        z = _bf(torch.randn(N, H, W, C1, generator=op.gen, device=DEV))
+        aux = torch.relu(z)
+        outs = []
+        for _ in range(3):
+            if direction.startswith("fwd"):
+                y = torch.empty(N, H, W, K, dtype=torch.bfloat16, device=DEV)
+                stats = direction == "fwd_stats"
+                tile = lib.conv2d_fwd_tile_m(DT_BF16, C1, C1, 0, 0, N, H, W, K, R, R, s, 1)
+                stt = torch.empty(-(-N * H * W // tile), 2, K, dtype=torch.float32, device=DEV) if stats else None
+                lib.conv2d_fwd(DT_BF16, _P(x1), C1, C1, 0, 0, 0, N, H, W, _P(wk), K, R, R, s, 1,
+                               0 if stats else _P(op.bias), int(not stats), _P(y), K, _P(stt), st)
+                outs.append((y,) + ((stt,) if stats else ()))
+            elif direction == "dgrad":
+                dx = torch.empty(N, H, W, C1, dtype=torch.bfloat16, device=DEV)
+                lib.conv2d_dgrad(DT_BF16, _P(dyh), K, N, H, W, _P(wt), K, C1, R, R, s, 1, _P(dx), C1, H, W, 0, st)
+                outs.append((dx,))
+            else:
+                args = [DT_BF16, _P(dyh), K, N, H, W, _P(wt), K, C1, R, R, s, 1]
+                rows = lib.conv2d_dgrad_post(*args, 0, C1, H, W, 1, _P(aux), C1, 0, 0, 0, 0, 0, 0, st)
+                assert rows > 0
+                dx = torch.empty(N, H, W, C1, dtype=torch.bfloat16, device=DEV)
+                part = torch.empty(rows, 2, C1, dtype=torch.float32, device=DEV)
+                lib.conv2d_dgrad_post(*args, _P(dx), C1, H, W, 1, _P(aux), C1, 0, 0, 0, 0, _P(part), rows, st)
+                outs.append((dx, part))
+        torch.cuda.synchronize()
+        for o in outs[1:]:
+            for a_, b_ in zip(outs[0], o):
+                assert torch.equal(a_.view(torch.int16) if a_.dtype == torch.bfloat16 else a_,
+                                   b_.view(torch.int16) if b_.dtype == torch.bfloat16 else b_), (direction, shape)

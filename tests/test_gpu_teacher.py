@@ -11,7 +11,8 @@ teacher_tap.py), so no error is amplified across blocks.  Held per tensor:
 
 * every parameter gradient (fp32): relative L2 <= PARAM_REL against the float64 rebuild with bf16
   rounding where the path stores a gradient (``emu``), or <= NOISE_K x the distance between that
-  rebuild run in float32 and in float64 where fp32 accumulation is ill-conditioned;
+  rebuild run in float32 and in float64 where fp32 accumulation is ill-conditioned; the analytically
+  zero psi conv bias gradients absolutely, at <= ZERO_K x that rebuild's absolute deviation;
 * every block input's gradient contribution (bf16-stored): relative L2 <= INPUT_REL;
 * every op's forward output against float64 on the stored inputs: relative L2 <= FWD_REL (bf16
   rounding of the stored output is ~1.1e-3 rms);
@@ -38,8 +39,15 @@ DEV = "cuda"
 PARAM_REL = 1e-3
 #: ... or NOISE_K x the float32 rebuild's own distance from the float64 one, where fp32 accumulation
 #: itself is ill-conditioned (per-channel sums with heavy cancellation: a BN bias whose incoming
-#: gradient is nearly mean-free, the psi conv bias in front of a train-mode BN, whose exact gradient is 0)
-NOISE_K = 16.0
+#: gradient is nearly mean-free).  Round 4 measured every such tensor at <= 1.33x its noise floor
+#: (C5 layer1.0.downsample.0.weight), so 3x leaves room for the draw of the noise and no more.
+NOISE_K = 3.0
+#: conv biases in front of a train-mode BN (the attention gates' psi conv, model/unet_attention.py:24-25):
+#: the exact gradient is 0 (BN removes the mean), so a relative bound is vacuous (the float64 value is
+#: ~1e-17).  Held absolutely: |hip - float64| <= ZERO_K x |float32 rebuild - float64|, the size of one
+#: fp32 accumulation of the same summands (round 4: <= 0.95x).
+ZERO_K = 4.0
+ZERO_GRAD = ("attn.psi.0.bias",)
 INPUT_REL = 1e-2
 FWD_REL = 5e-3
 LOSS_REL = 1e-4
@@ -200,13 +208,25 @@ def _run(tag):
                 bad += [(sname, f"fwd:{kind}", rel) for rel, kind in fr if not rel <= FWD_REL]
             del r
         torch.cuda.empty_cache()
+    worst_ratio = (0.0, None)
     for sname, seg in report["segments"].items():
         e = seg["emu"]
+        e["zero_abs"] = {}
         for n, rel in e["params"].items():
-            allow = max(PARAM_REL, NOISE_K * e["noise"][n])
+            if n.endswith(ZERO_GRAD):
+                # analytically zero: the absolute error against the fp32 rebuild's absolute deviation
+                # (both relative to the same float64 norm, so the ratio of the two rels is that of the absolutes)
+                allow = ZERO_K * e["noise"][n]
+                e["zero_abs"][n] = {"ratio": rel / max(e["noise"][n], 1e-300), "allow_ratio": ZERO_K}
+            else:
+                allow = max(PARAM_REL, NOISE_K * e["noise"][n])
+                if rel > PARAM_REL:
+                    worst_ratio = max(worst_ratio, (rel / max(e["noise"][n], 1e-300), n))
             if not rel <= allow:
                 bad.append((sname, n, rel, allow))
-        e["allowance_max"] = max(max(PARAM_REL, NOISE_K * v) for v in e["noise"].values()) if e["noise"] else None
+        e["allowance_max"] = max(max(PARAM_REL, NOISE_K * v) for k, v in e["noise"].items()
+                                 if not k.endswith(ZERO_GRAD)) if e["noise"] else None
+    report["worst_noise_ratio"] = {"ratio": worst_ratio[0], "param": worst_ratio[1], "noise_k": NOISE_K}
     t_check = time.time() - t1
     report["seconds"] = {"step": round(t_step, 1), "check": round(t_check, 1)}
     n_params = sum(s["emu"]["n_params"] for s in report["segments"].values())

@@ -225,8 +225,15 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   for (int c = 0; c < FC; ++c)
 #pragma unroll
     for (int e = 0; e < 4; ++e) pq0[c][e] = pq1[c][e] = 0.f;
-  constexpr int NA_ = POST == 4 ? FP : POST ? FP * FC : 0;                   // aux loads per tile
-  constexpr int NS_ = FP * FC + FP * HK + (kMask ? FP : 0);                   // output stores per tile
+  // per-wave vector-memory operations of one tile's epilogue, counted from the loops that issue them
+  // (each issues its full count on every wave: inactive lanes go out of range, nothing is skipped):
+  //   aux loads (post op): POST 4 one 8-B mask load per 16-pixel group, POST 1/2 one per (group, channel
+  //   group); stores: FP x FC outputs, FP x HK head logits, FP mask words
+  constexpr int NA_ = POST == 4 ? FP : POST ? FP * FC : 0;
+  constexpr int NS_ = FP * FC + FP * HK + (kMask ? FP : 0);
+  // (operations issued beyond these -- the accumulate epilogue's old-value loads -- only make a wait
+  // wait longer; a count above the true one would not wait for the DMA)
+  static_assert(!HS || 2 * HI2 + 2 * NA_ + 2 * NS_ <= 63, "hs_wait counts must fit vmcnt's 6 bits");
   auto half_wait = [&](int h) {
     if (last_dma) hs_wait<HI2, NA_, NS_>(h);
     else hs_wait<HI2 - 1, NA_, NS_>(h);

@@ -9,8 +9,11 @@ The reference is single-process (train.py:98); this is the build's DP path (SURV
     stream, fenced against the compute stream by torch.distributed);
   * BatchNorm uses per-GPU batch statistics and rank-local running stats (DDP without SyncBN);
   * on a GPU each bucket's collective runs on a dedicated COMM stream (``comm_stream``) that first
-    waits for the compute stream (BN / bias gradients) and the weight-gradient stream (conv weight
-    gradients) -- so it follows every writer -- and the bucket's optimizer actions run on that comm
+    waits for the compute stream (BN / bias gradients) and for the bucket's OWN last weight-gradient
+    launch (an event recorded on the weight-gradient stream right after the last of the bucket's conv
+    weight gradients, ``param_done(..., stream=side)``; not that stream's tail when the bucket
+    completes, which may hold later buckets' gradients) -- so it follows every writer -- and the
+    bucket's optimizer actions run on that comm
     stream right behind the collective.  The weight-gradient stream never waits on RCCL: the next
     buckets' weight gradients keep running while a bucket is on the wire (three streams: compute,
     weight gradients, comm; the compute stream joins the comm stream once, at the end of backward);
@@ -76,6 +79,8 @@ class GradBuckets:
         # params in arena order
         order = sorted(model._param_list, key=lambda p: model._slices[id(p)][0])
         self.buckets = []  # [start, end, remaining]
+        self._side_ev = []  # per bucket: event after its last weight-gradient launch (reused every step)
+        self._side_rec = []  # per bucket: that event was recorded in this backward
         self.owner = {}
         start, count = None, 0
         for p in order:
@@ -89,6 +94,7 @@ class GradBuckets:
                 start, count = None, 0
         if start is not None:
             self.buckets.append([start, flat.numel(), count])
+        self._side_ev = [None] * len(self.buckets)
         self._pending = []
         self._left = None
         self._issued = None
@@ -123,6 +129,7 @@ class GradBuckets:
     def _reset(self):
         self._left = [b[2] for b in self.buckets]
         self._issued = [False] * len(self.buckets)
+        self._side_rec = [False] * len(self.buckets)
         self._pending = []
 
     def _reduce(self, i, view):
@@ -144,8 +151,10 @@ class GradBuckets:
             # writer of the bucket: BN / bias gradients (compute stream), weight gradients (side stream)
             comm = comm_stream(view.device)
             comm.wait_stream(torch.cuda.current_stream(view.device))
-            if side is not None:
-                comm.wait_stream(side)
+            if self._side_rec[i]:
+                # the bucket's last weight-gradient launch (every side-stream writer reports its stream:
+                # a bucket without one has no writer there)
+                comm.wait_event(self._side_ev[i])
             with torch.cuda.stream(comm):
                 w, buf = self._reduce(i, view)
                 w.wait()  # RCCL: the comm stream waits for the collective; gloo: the host waits
@@ -172,12 +181,19 @@ class GradBuckets:
                     act(i, s, e, side)
         self._issued[i] = True
 
-    def _on_grad(self, p):
+    def _on_grad(self, p, stream=None):
+        """p's gradient is final; stream: the weight-gradient stream when its last launch wrote it"""
         if self._left is None:
             self._reset()
         i = self.owner.get(id(p))
         if i is None:  # a stand-in tensor (e.g. a re-laid-out weight), not a model parameter
             return
+        if stream is not None and self.allreduce:
+            ev = self._side_ev[i]
+            if ev is None:
+                ev = self._side_ev[i] = torch.cuda.Event()
+            ev.record(stream)  # re-recorded by later side-written params of the bucket (stream order)
+            self._side_rec[i] = True
         self._left[i] -= 1
         if self._left[i] == 0 and not self._issued[i]:
             self._issue(i)

@@ -227,15 +227,18 @@ class Ctx:
         while self.deferred:
             self.deferred.pop(0)()
 
-    def param_done(self, *params):
+    def param_done(self, *params, stream=None):
         """report parameters whose gradient is final AND that no later compute-stream kernel of this
         backward reads (nor its packed image): a bucket's all-reduce / optimizer update may run on the
         side stream right after (stand-in tensors that are not model parameters, e.g. a re-laid-out
-        weight, are ignored by the hook)"""
+        weight, are ignored by the hook).  stream: the weight-gradient stream when the gradients were
+        written there and that stream's last launch is their writer (the bucket fences on an event
+        recorded now, not on whatever the stream holds when the bucket completes); None = the
+        compute stream"""
         if self.grad_hook is not None:
             for p in params:
                 if p is not None:
-                    self.grad_hook(p)
+                    self.grad_hook(p, stream)
 
 
 #: weight gradients of 3x3 convs whose output has >= this many pixels per image are held back in
@@ -516,8 +519,8 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
         cin = C1 + C2
 
         def launch_wgrad(serial=False):
-            # weight gradient: on the side stream when overlapping (it only needs dY and the inputs,
-            # and nothing in the data-gradient chain reads its output)
+            """weight gradient: on the side stream when overlapping (it only needs dY and the inputs,
+            and nothing in the data-gradient chain reads its output); returns that stream or None"""
             ws_bytes = _q("conv2d_wgrad_workspace", ctx.dt, N, Pq, Qq, Kp, cin, R, S)
             side = None if serial else ctx.side
             if side is not None:
@@ -548,12 +551,14 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                 with _probe("wgrad", flops, 1, ("wgrad",) + desc, stream=side):
                     lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), P(X2), C2, ldp(X2), N, H, W, P(dY), ldp(dY), K, R, S,
                                      stride, pad, P(ws), ws.numel(), P(pc.conv.weight.grad), pc.C, 1, wst)
+            return side
 
         deferred = defer_wgrad(ctx, N, Pq, Qq, R, S, x2)
         serial = not deferred and ((bool(WG_SERIAL_HW) and Pq * Qq >= WG_SERIAL_HW and R * S > 1) or
                                    layer in WG_SERIAL_LAYERS)
+        wstream = None
         if not deferred and not serial:
-            launch_wgrad()
+            wstream = launch_wgrad()
         # data gradient (reads the packed weight pc.wt: the parameter is reported done after it)
         if Kp != K:
             if x1.need_grad:
@@ -582,11 +587,14 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
             launch_wgrad(serial=True)  # after the data gradient, on the compute stream
         if deferred:
             def late():
-                launch_wgrad()
-                ctx.param_done(pc.conv.weight, b)
+                ctx.param_done(pc.conv.weight, stream=launch_wgrad())
+                ctx.param_done(b)
             ctx.deferred.append(late)
         else:
-            ctx.param_done(pc.conv.weight, b)
+            # the side stream's last launch is still this wgrad (only the data gradient, on the compute
+            # stream, was enqueued since)
+            ctx.param_done(pc.conv.weight, stream=wstream)
+            ctx.param_done(b)
 
     ctx.push(bwd)
     return out, st
@@ -753,7 +761,7 @@ def stem_conv(ctx, x, conv_mod):
             wst = ctx.stream
         with _probe("wgrad", flops, 1, ("stem_wgrad",) + desc, stream=side):
             lib.stem_wgrad(P(xp), N, H, W, P(dY), ldp(dY), K, P(ws), ws.numel(), P(conv_mod.weight.grad), C, 1, wst)
-        ctx.param_done(conv_mod.weight)
+        ctx.param_done(conv_mod.weight, stream=side)
 
     ctx.push(bwd)
     return out, st
