@@ -244,6 +244,31 @@ def _spin_rate(dev):
     return 20_000_000 / max(e0.elapsed_time(e1), 1e-3)
 
 
+def compulsory_bytes(desc):
+    """HBM bytes one conv call cannot avoid (bf16): each operand read once, the result written once,
+    the weights once; post-op data gradients add their aux reads (post 1/2: the producer's activation,
+    post 3: y3 (+ y_ds) + the old gradient + the mask byte, post 4: the mask bits).  The probe's
+    descriptor: (kind, N, H, W, C1, C2, K, R, S, stride, pad, ld1, ld2)."""
+    kind, N, H, W, C1, C2, K, R, S, stride, pad = desc[:11]
+    cin = C1 + C2
+    P = (H + 2 * pad - R) // stride + 1
+    Q = (W + 2 * pad - S) // stride + 1
+    mi, mo = N * H * W, N * P * Q
+    w = 2 * K * cin * R * S
+    if kind.startswith("stem"):
+        return N * H * (W + 8) * 16 + w + 2 * mo * K
+    if kind.startswith("fwd"):
+        return 2 * mi * cin + w + 2 * mo * K
+    b = 2 * mo * K + w + 2 * mi * cin  # dgrad: dY, W^T, dX
+    if kind.startswith(("dgrad_post1", "dgrad_post2")):
+        b += 2 * mi * cin
+    elif kind.startswith("dgrad_post3"):
+        b += 2 * mi * cin * 2 + mi * cin // 8
+    elif kind.startswith("dgrad_post4"):
+        b += mi * cin // 8
+    return b
+
+
 def host_enqueue_ms(run, dev, gpu_ms, steps=3):
     """host cost of one step: the GPU is first parked on a spin kernel long enough to cover the
     enqueue, so the launch queue never throttles the host; the wall time of enqueueing `steps` steps
@@ -415,11 +440,14 @@ def main():
                 for kind, flops, nl, e0, e1, desc in ops.PROBE:
                     us = e0.elapsed_time(e1) * 1e3
                     f.write(f"{kind:9s} {us:9.1f} us {flops / max(us, 1e-3) / 1e6:8.1f} TF/s  {desc}\n")
-        for kind, flops, nl, e0, e1, _ in ops.PROBE:
+        comp = {}
+        for kind, flops, nl, e0, e1, desc in ops.PROBE:
             d = kinds.setdefault(kind, [0.0, 0.0, 0])
             d[0] += flops
             d[1] += e0.elapsed_time(e1) * 1e-3
             d[2] += nl
+            if desc is not None:
+                comp[kind] = comp.get(kind, 0) + compulsory_bytes(desc)
         ops.PROBE = None
         dom = max(kinds, key=lambda k: kinds[k][1])
         fl, sec, n = kinds[dom]
@@ -429,6 +457,8 @@ def main():
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": tr[0] if tr else None,
                 "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": tr[1] if tr else None,
+                "compulsory_bytes_per_launch": round(comp.get(dom, 0) / n) if n else None,
+                "traffic_over_compulsory": round(tr[0] / (comp[dom] / n), 3) if (tr and comp.get(dom) and n) else None,
                 "mfma_busy": mb[0] if mb else None, "mfma_busy_source": mb[1] if mb else None,
                 "launches_per_step": n, "avg_launch_us": round(1e6 * sec / n, 2),
                 "algorithmic_gflop_per_step": round(fl / 1e9, 1),

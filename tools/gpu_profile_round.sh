@@ -1,7 +1,9 @@
 # Round artifacts on one MI355X: bench line, rocprofv3 kernel stats, PMC HBM traffic (two passes),
 # PMC MFMA utilisation (one pass), conv kernel-configuration table.
-#   bash tools/gpu_profile_round.sh <round tag, e.g. r02> [model] [batch] [loss]
-# Outputs under gpurun_out/<tag>_*; copy the summaries into profiles/ afterwards.
+#   COMMIT=<sha> bash tools/gpu_profile_round.sh <round tag, e.g. r02> [model] [batch] [loss]
+# Outputs under gpurun_out/<tag>_*; copy the summaries into profiles/ afterwards.  COMMIT (the tree's
+# git sha, substituted on the host before the call: the GPU box gets no .git) is written into every
+# summary.
 set -o pipefail
 TAG=${1:-r02}
 MODEL=${2:-unet_resnet50}
@@ -20,5 +22,29 @@ python tools/pmc_traffic.py gpurun_out/${TAG}_pmcF gpurun_out/${TAG}_pmcW gpurun
 python tools/pmc_mfma.py gpurun_out/${TAG}_pmcM gpurun_out/${TAG}_mfma.json "$WL" > /dev/null
 python tools/prof_summary.py gpurun_out/${TAG}_prof 8 40 > gpurun_out/${TAG}_kernel_stats_summary.txt
 python tools/trace_streams.py gpurun_out/${TAG}_prof 4 > gpurun_out/${TAG}_streams.txt
+python tools/trace_gaps.py gpurun_out/${TAG}_prof 2 > gpurun_out/${TAG}_gaps.txt
 timeout -k 10 240 python tools/bench_conv_configs.py --model $MODEL --batch $BATCH --out gpurun_out/${TAG}_conv_configs.txt > /dev/null 2>&1 || echo "config table failed"
+python - "$TAG" "${COMMIT:-unknown}" <<'PYEOF'
+import json, sys
+tag, commit = sys.argv[1:3]
+for f in ("kernel_stats_summary.txt", "streams.txt", "gaps.txt", "conv_configs.txt"):
+    p = f"gpurun_out/{tag}_{f}"
+    try:
+        body = open(p).read()
+    except OSError:
+        continue
+    open(p, "w").write(f"# commit {commit}\n" + body)
+for f in ("traffic.json", "mfma.json"):
+    p = f"gpurun_out/{tag}_{f}"
+    try:
+        d = json.load(open(p))
+    except (OSError, ValueError):
+        continue
+    d["commit"] = commit
+    json.dump(d, open(p, "w"), indent=1)
+p = f"gpurun_out/{tag}_bench.json"
+lines = open(p).read().strip().splitlines()
+d = json.loads(lines[-1]); d["commit"] = commit
+open(p, "w").write(json.dumps(d) + "\n")
+PYEOF
 tail -1 gpurun_out/${TAG}_bench.json | cut -c1-300

@@ -22,7 +22,7 @@ def main():
     rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
     ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"], r["Kernel_Name"]) for r in rows)
     # a step starts at the stem input pack (Adam runs once per gradient bucket with --overlap-adam)
-    mark = [i for i, k in enumerate(ks) if "pack_input_stem" in k[3]]
+    mark = [i for i, k in enumerate(ks) if "pack_input" in k[3]]  # the step's first kernel: the input pack (stem or plain)
     lo, hi = mark[-steps], len(ks)
     sel = ks[lo:hi]
     main_stream = ks[mark[-1]][2]

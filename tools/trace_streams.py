@@ -2,7 +2,7 @@
 
     python tools/trace_streams.py <dir with run_kernel_trace.csv> [steps]
 
-Takes the last `steps` training steps (split at the stem's input pack), and prints per stream: summed
+Takes the last `steps` training steps (split at the input pack: pack_input_stem or pack_input), and prints per stream: summed
 kernel time, union-of-intervals wall, and the top kernels by time on each stream; plus the idle
 gaps of the compute stream (time where no kernel of that stream runs).
 """
@@ -20,7 +20,7 @@ def main():
     ks.sort()
     # a step starts at the stem input pack (Adam runs once per gradient bucket with --overlap-adam);
     # the last step is closed by the final kernel of the trace
-    mark = [i for i, k in enumerate(ks) if "pack_input_stem" in k[3]]
+    mark = [i for i, k in enumerate(ks) if "pack_input" in k[3]]  # the step's first kernel: the input pack (stem or plain)
     if len(mark) < steps:
         print("not enough steps", len(mark))
         return
