@@ -4,7 +4,10 @@
     (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
 
 A step = zero_grad + forward + Lovasz-hinge loss + backward (+ RCCL gradient all-reduce when N>1) +
-fused Adam on one synthetic batch already resident in HBM.  Adam and the re-pack of the conv weights
+fused Adam on one synthetic batch already resident in HBM.  After one eager step and one recording
+step (--plan 1, default) the steps are replays of the recorded launch sequence (unetseg_hip/plan.py):
+every kernel of the step runs every time, on the same streams; only the Python that chose them is not
+re-run (tests/test_gpu_plan.py: bit-identical to eager steps).  Adam and the re-pack of the conv weights
 run per gradient bucket on the weight-gradient stream while backward continues (--overlap-adam 1,
 FusedAdam(overlap=True)); every parameter is updated inside each timed step.  Rank 0 prints ONE JSON line.
 `roofline` covers the dominant kernel (igemm_tn: conv fwd + dgrad), measured with HIP events around
@@ -61,6 +64,9 @@ def parse():
     ap.add_argument("--extra-configs", type=int, default=1,
                     help="also time C4 (attention_unet B=8, N=1 only) and C5 (multitask_unet B=8) after the headline")
     ap.add_argument("--card-probe", type=int, default=1, help="bf16 GEMM + HBM copy rate of this card (rank 0)")
+    ap.add_argument("--plan", type=int, default=1,
+                    help="replay a recorded step plan (unetseg_hip/plan.py: the eager step's launches re-issued "
+                         "from the host, every kernel every step) after one eager and one recording step")
     ap.add_argument("--ddp-bf16", type=int, default=0,
                     help="N>1: all-reduce bf16 copies of the gradient buckets (half the bytes; opt-in)")
     return ap.parse_args()
@@ -319,7 +325,9 @@ def build_step(model_name, batch, size, loss_name, dev, rank, world, args):
         data.append((x.to(dev), y.to(dev), c.to(dev)))
 
     def step(i):
-        x, y, c = data[i % nbatches]
+        return step_on(*data[i % nbatches])
+
+    def step_on(x, y, c):
         opt.zero_grad()
         with torch.autocast("cuda", dtype=torch.bfloat16):
             if multitask:  # seg BCE/Lovasz + 1.0 * CE (train.py:213-219 defaults)
@@ -332,6 +340,24 @@ def build_step(model_name, batch, size, loss_name, dev, rank, world, args):
         return loss
 
     run = step
+    if args.plan and not use_graph:
+        from unetseg_hip.plan import StepPlan
+        state = {"plan": None, "eager": 0}
+
+        def run(i):
+            p = state["plan"]
+            if p is not None:
+                x, y, c = data[i % nbatches]
+                return p.replay(x=x, y=y, c=c)
+            if state["eager"] < 1:  # one eager step first: weights pre-packed, memos and workspaces warm
+                state["eager"] += 1
+                return step(i)
+            x, y, c = data[i % nbatches]
+            p = StepPlan({"x": x, "y": y, "c": c})
+            loss = p.record(lambda: step_on(x, y, c))  # the recording is a real step
+            state["plan"] = p
+            return loss
+        run.state = state
     if use_graph:
         # one captured step per resident batch; every replay is a full fwd + loss + bwd + Adam step
         # (Adam's lr and step count are device-resident, so replays advance the optimizer state)
@@ -416,6 +442,7 @@ def main():
 
     model, step, run, use_graph, overlap = build_step(args.model, args.batch, args.size, args.loss, dev, rank, world,
                                                       args)
+    plan_state = getattr(run, "state", None)
     torch.cuda.reset_peak_memory_stats(dev)
     wall, median_ms, gpu_ms, loss, card_mid = timed(run, args.steps, args.warmup, world, dev,
                                                     sample=lambda: card_state(dev))
@@ -465,6 +492,7 @@ def main():
                 "kernels": {k: {"tflops": round(v[0] / v[1] / 1e12, 2), "ms_per_step": round(1e3 * v[1], 3),
                                 "launches": v[2]} for k, v in kinds.items()}}
 
+    plan_stats = plan_state["plan"].stats() if plan_state and plan_state["plan"] is not None else None
     # data-parallel consistency: after identical averaged updates every rank holds the same weights
     in_sync = None
     if world > 1:
@@ -473,7 +501,7 @@ def main():
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         in_sync = bool(float(hi.item()) == float(lo.item()))
-    del model, step, run
+    del model, step, run, plan_state
     gc.collect()  # the model and its gradient buckets reference each other
     torch.cuda.empty_cache()
 
@@ -483,6 +511,7 @@ def main():
             if world > 1 and not dp:
                 continue
             m2, _, run2, _, _ = build_step(name, batch, args.size, loss_name, dev, rank, world, args)
+            ps2 = getattr(run2, "state", None)
             torch.cuda.reset_peak_memory_stats(dev)
             # at least 30 timed steps: a B=8 step is ~10 ms, and over 10 steps one host hiccup of a few
             # ms moved the C5 line by 10-20 % between otherwise identical runs
@@ -497,8 +526,9 @@ def main():
                             "value": round(ips, 2), "unit": "images/s", "steps": k2, "ms_per_step": round(1000.0 * w2 / k2, 3),
                             "median_gpu_ms_per_step": round(med2, 3), "peak_alloc_gib": round(peak2, 2),
                             "host_enqueue_ms": host2[0], "host_loadavg": host2[1], "card_during": card2,
+                            "step_plan": ps2["plan"].stats() if ps2 and ps2["plan"] is not None else None,
                             "step_mfma_frac": round(ips / world * GFLOP_PER_IMG[name] / 1e3 / PEAK_BF16_TFLOPS, 4)}
-            del m2, run2
+            del m2, run2, ps2
             gc.collect()
             torch.cuda.empty_cache()
 
@@ -529,6 +559,7 @@ def main():
             "peak_alloc_gib": round(peak_gib, 2),
             "host_enqueue_ms": host_ms, "host_loadavg": host_load,
             "hip_graph": use_graph, "overlap_adam": overlap, "params_in_sync": in_sync,
+            "step_plan": plan_stats,
             "grad_reduce_dtype": ("bf16" if args.ddp_bf16 else "fp32") if world > 1 else None,
             "configs": configs, "card": card,
         }

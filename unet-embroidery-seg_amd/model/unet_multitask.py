@@ -5,6 +5,7 @@ import torch
 import torch.nn as nn
 
 from unetseg_hip import losses, ops
+from unetseg_hip.plan import Dyn
 from unetseg_hip.nn import AdaptiveAvgPool2d, Conv2d, Dropout, Flatten, HipModel, Linear, ReLU, Seq, Upsample
 
 from .resnet_backbone import resnet50, run_resnet
@@ -38,15 +39,19 @@ class MultiTaskUNet(HipModel):
         self._drop_step = 0
         self._finalize()
 
+    def _next_drop_seed(self):
+        self._drop_step += 1
+        return 0x5EED0000 + self._drop_step
+
     def _run(self, ctx, x):
         if self.num_seg_classes > 2:
             raise NotImplementedError("HIP seg head supports num_seg_classes <= 2")
         self._pack_weights(ctx, ctx.tape is not None)
         feats = run_resnet(ctx, self.encoder, x)
-        self._drop_step += 1
         ops.tap_mark(ctx, "cls_head")
-        cls, cls_holder, _ = ops.cls_head(ctx, feats[4], self.cls_head, self.dropout_mask,
-                                          seed=0x5EED0000 + self._drop_step)
+        # the dropout seed advances every step (a step plan re-evaluates it per replay)
+        seed = Dyn(self._next_drop_seed(), self._next_drop_seed)
+        cls, cls_holder, _ = ops.cls_head(ctx, feats[4], self.cls_head, self.dropout_mask, seed=seed)
         u = run_resnet_decoder(ctx, self, feats, head=self.seg_head)
         seg, seg_holder = ops.pw_head(ctx, u, self.seg_head)
         ops.tap_mark(ctx, "end")

@@ -6,6 +6,7 @@ import torch
 from .lib import lib
 from . import ops
 from .ops import P
+from .plan import py
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -78,6 +79,10 @@ class FusedAdam(torch.optim.Optimizer):
         if self._applied:
             self.model._mark_prepacked()
 
+    def _commit_step(self):
+        self._applied = False
+        self._step += 1
+
     def zero_grad(self, set_to_none: bool = True):  # keep the grads as arena views
         m = self.model
         m._attach_grads()
@@ -85,15 +90,14 @@ class FusedAdam(torch.optim.Optimizer):
         if ops.OVERLAP and g.is_cuda and not torch.cuda.is_current_stream_capturing():
             # nothing writes the arena before backward: clear it on the weight-gradient stream, idle
             # during the forward, instead of in front of the forward on the compute stream; the
-            # backward (and any step / grad read before it) waits for this event
+            # backward (and any step / grad read before it) waits for the side stream (which holds
+            # nothing after the clear until then).  C-ABI stream waits: a step plan logs them
             cur = torch.cuda.current_stream(g.device)
             side = ops.side_stream(g.device)
-            side.wait_stream(cur)
+            lib.stream_wait(side.cuda_stream, cur.cuda_stream)
             with torch.cuda.stream(side):
                 g.zero_()
-            ev = torch.cuda.Event()
-            ev.record(side)
-            m._grad_zero_event = ev
+            m._grad_zero_side = side
         else:
             g.zero_()
 
@@ -105,8 +109,7 @@ class FusedAdam(torch.optim.Optimizer):
         if self._applied:
             if grad_scale is not None:
                 raise ValueError("FusedAdam(overlap=True) cannot take a grad scale (the update ran in backward)")
-            self._applied = False
-            self._step += 1
+            py(self._commit_step)  # host state: a step plan advances the count every replay
             return loss
         m._prepacked = None  # the weights change below: the next forward packs them
         flat, grad = m._flat, m._flat_grad

@@ -39,6 +39,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops
+from .plan import py
 
 
 def _nullctx():
@@ -95,6 +96,7 @@ class GradBuckets:
         if start is not None:
             self.buckets.append([start, flat.numel(), count])
         self._side_ev = [None] * len(self.buckets)
+        self._side_rec = [False] * len(self.buckets)  # the bucket has a writer on the side stream (static)
         self._pending = []
         self._left = None
         self._issued = None
@@ -129,7 +131,6 @@ class GradBuckets:
     def _reset(self):
         self._left = [b[2] for b in self.buckets]
         self._issued = [False] * len(self.buckets)
-        self._side_rec = [False] * len(self.buckets)
         self._pending = []
 
     def _reduce(self, i, view):
@@ -192,14 +193,14 @@ class GradBuckets:
             ev = self._side_ev[i]
             if ev is None:
                 ev = self._side_ev[i] = torch.cuda.Event()
-            ev.record(stream)  # re-recorded by later side-written params of the bucket (stream order)
+            py(ev.record, stream)  # re-recorded by later side-written params of the bucket (stream order)
             self._side_rec[i] = True
         self._left[i] -= 1
         if self._left[i] == 0 and not self._issued[i]:
-            self._issue(i)
+            py(self._issue, i)  # a step plan replays the issue (the update reads Adam's step count then)
 
     def _finish(self):
-        if self._left is None:
+        if self._issued is None:  # (not `_left`: a replayed step issues buckets without _on_grad)
             self._reset()
         for i in range(len(self.buckets)):
             if not self._issued[i]:
@@ -215,6 +216,7 @@ class GradBuckets:
             act()
         self._left = None
         self._pending = []
+        self._issued = [False] * len(self.buckets)  # (a replayed step issues without _on_grad's reset)
 
 
 def init_from_env(backend: str = "nccl"):

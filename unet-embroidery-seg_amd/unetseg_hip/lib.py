@@ -197,6 +197,10 @@ def _fast():
     return _FAST or None
 
 
+#: set by plan.StepPlan.record: wraps every callable handed out (logging), none cached meanwhile
+_WRAP = None
+
+
 class _Caller:
     """lib.<name>(...) raises RuntimeError on a non-zero status.  The bound callable is cached on the
     instance after the first lookup (the op layer makes ~500 calls per training step); entry points the
@@ -207,17 +211,18 @@ class _Caller:
         fast = _fast()
         if fast is not None and hasattr(fast, item):
             fn = getattr(fast, item)
-            self.__dict__[item] = fn
-            return fn
-        fn = getattr(lib_, "unetseg_" + item)
-        if SIGNATURES["unetseg_" + item][0] is I and item not in VALUE_FUNCS:
-            def call(*args):
-                rc = fn(*args)
-                if rc != 0:
-                    raise RuntimeError(f"unetseg_{item} failed ({rc}): {last_error()}")
-                return rc
-            self.__dict__[item] = call
-            return call
+        else:
+            raw = getattr(lib_, "unetseg_" + item)
+            if SIGNATURES["unetseg_" + item][0] is I and item not in VALUE_FUNCS:
+                def fn(*args, _raw=raw):
+                    rc = _raw(*args)
+                    if rc != 0:
+                        raise RuntimeError(f"unetseg_{item} failed ({rc}): {last_error()}")
+                    return rc
+            else:
+                fn = raw
+        if _WRAP is not None:
+            return _WRAP(item, fn)
         self.__dict__[item] = fn
         return fn
 

@@ -191,10 +191,11 @@ class HipModel(nn.Module):
 
     def _wait_grad_zero(self):
         """the compute stream waits for a gradient-arena clear enqueued on the side stream (FusedAdam.zero_grad)"""
-        ev = getattr(self, "_grad_zero_event", None)
-        if ev is not None:
-            torch.cuda.current_stream(self._flat_grad.device).wait_event(ev)
-            self._grad_zero_event = None
+        side = getattr(self, "_grad_zero_side", None)
+        if side is not None:
+            from .lib import lib
+            lib.stream_wait(torch.cuda.current_stream(self._flat_grad.device).cuda_stream, side.cuda_stream)
+            self._grad_zero_side = None
 
     def _repoint(self):
         for p in self._param_list:

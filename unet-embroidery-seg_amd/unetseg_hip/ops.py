@@ -214,7 +214,8 @@ class Ctx:
             self.flush_deferred()
             if self.finish_hook is not None:
                 # the last buckets' collectives / optimizer updates, enqueued before the join below
-                self.finish_hook()
+                from .plan import py
+                py(self.finish_hook)
         finally:
             if ON_JOIN is not None:
                 ON_JOIN(self)
