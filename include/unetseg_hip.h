@@ -48,9 +48,9 @@ int unetseg_pack_conv_weight(int dtype, const float* w, int K, int C, int R, int
 typedef struct UnetsegPackDesc {
   const float* w;  /* fp32 [K][C][R][S] */
   void* wk;        /* dtype [K][R][S][Cpad] */
-  void* wt;        /* dtype [C][R][S][K] or NULL */
+  void* wt;        /* dtype [C][R][S][Kld] or NULL (columns K..Kld-1 untouched: a zeroed padded image) */
   long long start; /* first tile of this conv (ascending, desc[0].start == 0; unetseg_pack_tiles tiles) */
-  int K, C, R, S, Cpad, pad_;
+  int K, C, R, S, Cpad, Kld; /* Kld: wt row length, 0 = K (the 64-padded dgrad image of a narrow 1x1 conv) */
 } UnetsegPackDesc;
 /* blocks unetseg_pack_conv_weights spends on one conv: desc[i+1].start = desc[i].start + this */
 int unetseg_pack_tiles(int K, int Cpad, int taps);

@@ -435,15 +435,16 @@ def test_adam_matches_torch():
 @pytest.mark.parametrize("dtname", ["fp32", "bf16"])
 def test_pack_conv_weights_batched(dtname):
     """unetseg_pack_conv_weights (one launch for every conv) == torch permutes of the fp32 weights:
-    wk [K][R][S][Cpad] (zero channels C..Cpad-1) and wt [C][R][S][K]; ragged K/C tiles, tap chunks
-    of a 7x7, K not a multiple of 8 (scalar store path), bit-exact conversion."""
+    wk [K][R][S][Cpad] (zero channels C..Cpad-1) and wt [C][R][S][K] (bf16 narrow 1x1 convs: rows padded
+    to 64 with zero columns, the padded-K dgrad's operand); ragged K/C tiles, tap chunks of a 7x7, K not a
+    multiple of 8 (scalar store path), bit-exact conversion."""
     ops, DT_BF16, DT_F32 = _ops()
     dt = DT_BF16 if dtname == "bf16" else DT_F32
     tdt = torch.bfloat16 if dtname == "bf16" else torch.float32
     g = torch.Generator().manual_seed(7)
     shapes = [(64, 64, 3, 3, None, True), (64, 3, 7, 7, 8, False), (40, 24, 3, 3, None, True),
               (512, 2048, 1, 1, None, True), (36, 20, 3, 3, None, True), (96, 136, 1, 1, None, True),
-              (128, 192, 3, 3, None, True)]
+              (128, 192, 3, 3, None, True), (32, 64, 1, 1, None, True)]
     convs, pcs, need_t = [], [], []
     for K, C, R, S, cpad, nt in shapes:
         conv = torch.nn.Conv2d(C, K, (R, S), bias=False)
@@ -462,7 +463,11 @@ def test_pack_conv_weights_batched(dtname):
         ref_k[..., :C] = w.permute(0, 2, 3, 1)
         assert torch.equal(pc.wk.cpu(), ref_k.to(tdt)), (K, C, R, S)
         if nt:
-            assert torch.equal(pc.wt.cpu(), w.permute(1, 2, 3, 0).contiguous().to(tdt)), (K, C, R, S)
+            # narrow 1x1 convs in bf16 (PAD_K): wt rows are 64-padded, the pad columns zero (PackedConv.kld)
+            wt = pc.wt.cpu()
+            assert wt.shape[-1] == pc.kld and (pc.kld == K or (dtname == "bf16" and R == S == 1 and pc.kld % 64 == 0))
+            assert torch.equal(wt[..., :K], w.permute(1, 2, 3, 0).contiguous().to(tdt)), (K, C, R, S)
+            assert not wt[..., K:].any(), (K, C, R, S)
 
 
 

@@ -128,8 +128,8 @@ __device__ __forceinline__ float up_blend(float a, float b, float c, float d, fl
 struct UnetsegPackDesc {
   const float* w;   // fp32 [K][C][R][S]
   void* wk;         // dtype [K][R][S][Cpad]
-  void* wt;         // dtype [C][R][S][K] or NULL
+  void* wt;         // dtype [C][R][S][Kld] or NULL
   long long start;  // first tile of this conv in the batch (unetseg_pack_tiles tiles per conv)
-  int K, C, R, S, Cpad, pad_;
+  int K, C, R, S, Cpad, Kld;  // Kld: wt row length (0 = K; > K: the zeroed 64-padded image, see the header)
 };
 

@@ -712,9 +712,10 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const Unetseg
       if (k < d.K && c < d.Cpad) wk[((long)k * taps + tap) * d.Cpad + c] = (T)tile[kl][cl * taps + tap];
     }
   }
-  if (d.wt) {  // wt[c][tap][k], k fastest, 8 output channels per store
+  if (d.wt) {  // wt[c][tap][k], k fastest, 8 output channels per store; rows of Kld (>= K) elements
     T* wt = reinterpret_cast<T*>(d.wt);
-    if (d.K % 8 == 0) {
+    const int ldk = d.Kld > 0 ? d.Kld : d.K;
+    if (d.K % 8 == 0 && ldk % 8 == 0) {
       constexpr int K8 = kPackK / 8;
       for (int i = t; i < K8 * taps * CT; i += 256) {
         const int k8 = i % K8, rest = i / K8;
@@ -724,7 +725,7 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const Unetseg
         T o[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = (T)tile[k8 * 8 + e][cl * taps + tap];
-        T* dst = wt + ((long)c * taps + tap) * d.K + k;
+        T* dst = wt + ((long)c * taps + tap) * ldk + k;
         if (sizeof(T) == 2) {
           *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(o);
         } else {
@@ -737,7 +738,7 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const Unetseg
         const int kl = i % kPackK, rest = i / kPackK;
         const int tap = rest % taps, cl = rest / taps;
         const int k = k0 + kl, c = c0 + cl;
-        if (k < d.K && c < d.C) wt[((long)c * taps + tap) * d.K + k] = (T)tile[kl][cl * taps + tap];
+        if (k < d.K && c < d.C) wt[((long)c * taps + tap) * ldk + k] = (T)tile[kl][cl * taps + tap];
       }
     }
   }

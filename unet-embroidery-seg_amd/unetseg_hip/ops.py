@@ -315,7 +315,11 @@ def give_grad(ctx, node, g):
 # weights
 # ------------------------------------------------------------------------------------------------
 class PackedConv:
-    """bf16/fp32 GEMM images of one conv weight: wk [K][R][S][Cpad] (fwd), wt [C][R][S][K] (dgrad)"""
+    """bf16/fp32 GEMM images of one conv weight: wk [K][R][S][Cpad] (fwd), wt [C][R][S][Kld] (dgrad).
+    Kld = K, except for the narrow 1x1 convs whose gradients run through a 64-channel zero-padded dY
+    (PAD_K, bf16): their wt rows are Kp = 64-rounded wide with zero columns K..Kp, which is the B
+    operand that padded data gradient reads -- packed in place by the batched pack (UnetsegPackDesc
+    Kld), no per-step padded copy."""
 
     def __init__(self, conv, cpad=None):
         self.conv = conv
@@ -324,6 +328,7 @@ class PackedConv:
         self.cpad = cpad or C
         self.wk = self.wt = None
         self.dt = None
+        self.kld = K
 
     def ensure(self, ctx, need_t):
         """allocate the packed images for ctx's dtype/device (no launch)"""
@@ -332,20 +337,27 @@ class PackedConv:
             self.wk = ctx.empty(K, R, S, self.cpad)
             self.wt = None
             self.dt = ctx.dt
+            padk = PAD_K and ctx.dt == DT_BF16 and R == 1 and S == 1 and K % 64 != 0 and K % 8 == 0
+            self.kld = -(-K // 64) * 64 if padk else K
         if need_t and self.wt is None:
-            # [Cpad][R][S][K]: the padded input channels' rows stay zero (the pack writes C rows), so a
-            # data gradient over all Cpad channels of a padded input is well defined
-            self.wt = torch.zeros((self.cpad, R, S, K), dtype=ctx.tdtype, device=ctx.device)
+            # [Cpad][R][S][Kld]: the padded input channels' rows (and padded K columns) stay zero (the pack
+            # writes C rows x K columns), so a data gradient over all Cpad channels is well defined
+            self.wt = torch.zeros((self.cpad, R, S, self.kld), dtype=ctx.tdtype, device=ctx.device)
 
     def pack(self, ctx, need_t):
         K, C, R, S = self.K, self.C, self.R, self.S
         self.ensure(ctx, need_t)
+        if need_t and self.kld != K:  # the single-conv pack writes K-wide rows: stage, then widen
+            tmp = torch.empty((self.cpad, R, S, K), dtype=ctx.tdtype, device=ctx.device)
+            lib.pack_conv_weight(ctx.dt, P(self.conv.weight), K, C, R, S, self.cpad, P(self.wk), P(tmp), ctx.stream)
+            lib.add(ctx.dt, P(tmp), K, P(self.wt), self.kld, self.cpad * R * S, K, ctx.stream)
+            return
         lib.pack_conv_weight(ctx.dt, P(self.conv.weight), K, C, R, S, self.cpad, P(self.wk),
                              P(self.wt) if need_t else 0, ctx.stream)
 
 
 _PACK_DESC = np.dtype([("w", "<u8"), ("wk", "<u8"), ("wt", "<u8"), ("start", "<i8"), ("K", "<i4"), ("C", "<i4"),
-                       ("R", "<i4"), ("S", "<i4"), ("Cpad", "<i4"), ("pad_", "<i4")])  # UnetsegPackDesc
+                       ("R", "<i4"), ("S", "<i4"), ("Cpad", "<i4"), ("Kld", "<i4")])  # UnetsegPackDesc
 
 
 class PackTable:
@@ -368,7 +380,7 @@ class PackTable:
             start = 0
             for i, (pc, nt) in enumerate(zip(pcs, need_t)):
                 d[i] = (pc.conv.weight.data_ptr(), pc.wk.data_ptr(), pc.wt.data_ptr() if nt else 0, start,
-                        pc.K, pc.C, pc.R, pc.S, pc.cpad, 0)
+                        pc.K, pc.C, pc.R, pc.S, pc.cpad, pc.kld)
                 start += lib.pack_tiles(pc.K, pc.cpad, pc.R * pc.S)
             self.desc = torch.from_numpy(d.view(np.uint8).copy()).to(ctx.device)
             self.total = start
@@ -563,12 +575,11 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
         # data gradient (reads the packed weight pc.wt: the parameter is reported done after it)
         if Kp != K:
             if x1.need_grad:
-                wtp = torch.zeros(C1, Kp, dtype=ctx.tdtype, device=dev)
-                lib.add(ctx.dt, P(pc.wt), K, P(wtp), Kp, C1, K, ctx.stream)
+                assert pc.kld == Kp, "the padded-K data gradient reads the Kp-wide packed wt (PackedConv.kld)"
                 g, acc = gbuf(ctx, x1)
                 with _probe("igemm_tn", flops, 1, ("dgrad_padk",) + desc):
-                    lib.conv2d_dgrad(ctx.dt, P(dY), Kp, N, Pq, Qq, P(wtp), Kp, C1, 1, 1, 1, 0, P(g), ldp(g), H, W, acc,
-                                     ctx.stream)
+                    lib.conv2d_dgrad(ctx.dt, P(dY), Kp, N, Pq, Qq, P(pc.wt), Kp, C1, 1, 1, 1, 0, P(g), ldp(g), H, W,
+                                     acc, ctx.stream)
         elif x2 is None:
             if x1.need_grad and not _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc, last_grad):
                 g, acc = gbuf(ctx, x1)

@@ -10,10 +10,9 @@ A HIP graph removes the host cost but runs the weight-gradient stream's branches
 * ``record(fn)`` runs ``fn`` (one complete eager step: zero_grad, forward, loss, backward with the
   per-bucket Adam + weight re-pack on the side stream, optimizer step) once with
     - every C-ABI call logged with its arguments (``lib`` hands out logging wrappers),
-    - a TorchDispatchMode that keeps every tensor the step allocates alive (so no buffer is ever
-      reused: each recorded pointer stays valid and private to its role -- the caching allocator's
-      cross-stream reuse decisions depend on GPU progress at the time and cannot be replayed) and logs
-      the few torch kernels of the step (the autograd seed, small fills) as replayable calls,
+    - a private memory pool for every allocation of the step (see Memory below) and a
+      TorchDispatchMode that logs the few torch kernels of the step (the autograd seed, small fills)
+      as replayable calls,
     - the host-side actions that carry per-step state logged as Python calls (``py``): the gradient
       buckets' optimizer updates (Adam's step count is read when they run), the optimizer's step
       commit, the DDP collectives;
@@ -23,8 +22,12 @@ A HIP graph removes the host cost but runs the weight-gradient stream's branches
   dropout seed) are re-evaluated.  Every kernel of the step runs every replay; only the Python that
   decided which kernels to launch is skipped.
 
-Memory: with no reuse the plan holds every buffer of one step (unet_resnet50 B=16: ~20 GB against
-8 GB with reuse) -- on a 288 GB MI355X that is the better trade.  Correctness gate:
+Memory: the recording allocates from a private pool (torch.cuda.MemPool) that the plan owns for its
+life, so every recorded pointer stays valid and nothing outside the plan is ever placed there.
+Inside the pool the caching allocator reuses freed buffers in stream order, as in the eager step
+(deterministic, hence replayable; and a buffer rewritten while still in the 256 MB Infinity Cache
+saves the write-back of its old contents); only buffers handed to another stream (record_stream) are
+held for the plan's life, because their reuse would depend on GPU progress.  Correctness gate:
 tests/test_gpu_plan.py (replayed steps bit-identical to eager steps, every parameter, moment and
 BN statistic).
 """
@@ -95,15 +98,15 @@ class _Mode(TorchDispatchMode):
         plan = self.plan
         if threading.get_ident() != plan.thread:
             raise RuntimeError(f"StepPlan: {func} ran on another thread during the recording")
-        outs = out if isinstance(out, (tuple, list)) else (out,)
-        for t in outs:
-            if isinstance(t, torch.Tensor):
-                plan.keep.append(t)
-        if plan.suspended:
-            return out
         name = func._schema.name
         if name == "aten::record_stream":
-            return out  # no buffer is ever reused while the plan lives
+            # a buffer another stream reads: the allocator would reuse it only once that stream's event
+            # has completed -- a decision that depends on GPU progress at recording time.  Held for the
+            # plan's life instead, so it is never reused.
+            plan.keep.append(args[0])
+            return out
+        if plan.suspended:
+            return out
         if name in _NO_KERNEL or name.startswith("profiler::"):
             return out
         sch = func._schema
@@ -164,8 +167,9 @@ class StepPlan:
         _libmod._WRAP = _wrap
         RECORDING = self
         self.thread = threading.get_ident()
+        self.pool = torch.cuda.MemPool()
         try:
-            with torch.autograd.set_multithreading_enabled(False), _Mode(self):
+            with torch.autograd.set_multithreading_enabled(False), torch.cuda.use_mem_pool(self.pool), _Mode(self):
                 self.result = fn()
         finally:
             RECORDING = None
@@ -230,18 +234,9 @@ class StepPlan:
         return self.result
 
     def stats(self):
+        try:
+            pool = sum(seg["total_size"] for seg in self.pool.snapshot())
+        except Exception:  # noqa: BLE001 - diagnostics only
+            pool = 0
         return {"c_calls": self.n_c, "py_calls": self.n_py, "torch_ops": self.n_torch,
-                "torch_op_names": sorted(set(self.torch_names)),
-                "kept_gib": round(sum(t.untyped_storage().nbytes() for t in _unique_storages(self.keep)) / 2 ** 30, 2)}
-
-
-def _unique_storages(ts):
-    seen = set()
-    for t in ts:
-        if not t.is_cuda:
-            continue
-        s = t.untyped_storage()
-        k = s.data_ptr()
-        if k not in seen:
-            seen.add(k)
-            yield t
+                "torch_op_names": sorted(set(self.torch_names)), "pool_gib": round(pool / 2 ** 30, 2)}
