@@ -45,6 +45,12 @@ def _need_gpu():
 #              fwd_all (bias + ReLU + stats: every runtime epilogue flag of a TN tile) |
 #              dgrad (plain, then accumulated onto a random gradient) | post1 | post2 | wgrad
 CASES = {
+    # the first 3x3 conv of unet_plain / attention_unet on the 8-channel packed image (conv_first.hip):
+    # random values in all 8 channels (the kernel is exact for any 8-channel input), stats / bias + ReLU,
+    # attention_unet's C4 shape
+    "first3x3_stats": ("fwd_stats", (2, 64, 96, 8, 0, 64, 3, 1), ["fwd:first3x3"]),
+    "first3x3_relu": ("fwd_relu", (3, 32, 32, 8, 0, 64, 3, 1), ["fwd:first3x3"]),
+    "first3x3_bench": ("fwd_stats", (8, 512, 512, 8, 0, 64, 3, 1), ["fwd:first3x3"]),
     # ---- forward ----
     "fwd_halo3_relu": ("fwd_relu", (2, 64, 256, 64, 0, 64, 3, 1), ["fwd:halo3"]),           # up_conv @512^2 (rows)
     "fwd_halo3_stats": ("fwd_stats", (2, 128, 128, 64, 0, 64, 3, 1), ["fwd:halo3"]),        # layer1 conv2

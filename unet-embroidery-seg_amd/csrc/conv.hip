@@ -818,8 +818,14 @@ static IgemmArgs fwd_args(const void* x1, int c1, int ldc1, const void* x2, int 
   return a;
 }
 
+static bool first_ok(int dtype, const IgemmArgs& a, int ldy) {
+  return a.x2 == nullptr && a.c2 == 0 && a.nr == a.ns && a.dh0 == a.dw0 &&
+         first3x3_ok(dtype, a.c1, a.ldc1, a.c2, a.N, a.H, a.W, a.Ng, a.nr, a.ns, a.istride, -a.dh0, ldy);
+}
+
 static int fwd_tile_m(int dtype, const IgemmArgs& a) {
   FastTNArgs f;
+  if (first_ok(dtype, a, a.Ng)) return first3x3_tile_m();
   if (dtype == DT_BF16 && fast_tn_args(a, f)) return tn_fast_tile_m(f);
   return kBM;
 }
@@ -849,6 +855,13 @@ UNETSEG_API int unetseg_conv2d_fwd_config(int dtype, int c1, int ldc1, int c2, i
   IgemmArgs a = fwd_args(kSomePtr, c1, ldc1, c2 ? kSomePtr : nullptr, c2, ldc2, n, h, w, kSomePtr, cout, r, s, stride,
                          pad);
   a.ldy = cout;
+  if (c2 == 0) {
+    a.x2 = nullptr;
+    if (first_ok(dtype, a, cout)) {
+      if (taps_out) *taps_out = 0;
+      return kCfgFirst3x3;
+    }
+  }
   return tn_query(dtype, a, taps_out);
 }
 
@@ -872,6 +885,11 @@ UNETSEG_API int unetseg_conv2d_fwd(int dtype, const void* x1, int c1, int ldc1, 
   a.y = y; a.ldy = ldy; a.accumulate = 0; a.bias = bias; a.relu = relu;
   a.stats = stats; a.stats_ld = ceil_div(a.M, fwd_tile_m(dtype, a));
   hipStream_t st = (hipStream_t)stream;
+  if (first_ok(dtype, a, ldy)) {
+    launch_first3x3(x1, ldc1, wk, bias, relu, y, ldy, stats, n, h, w, st);
+    US_LAUNCH_CHECK("first3x3");
+    return 0;
+  }
   return dtype == DT_BF16 ? launch_tn<bf16>(a, st) : launch_tn<float>(a, st);
 }
 

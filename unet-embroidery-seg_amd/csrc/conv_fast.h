@@ -108,7 +108,7 @@ struct HaloWgradArgs {
 // 1..14: TN tile configurations of tn_config (conv_fast.hip); 17 / 18: stride-2 dgrad parity classes
 // merged into one launch on 128x128 / 64x128 register-staged tiles (launch_tn_multi); 19 / 20: short K
 // (2-4 steps) on one LDS stage, 128x128 / 128x64
-enum { kCfgHalo = 0, kCfgMulti128 = 17, kCfgMulti64 = 18, kCfgStemHalo = 30, kCfgGeneric = 100 };
+enum { kCfgHalo = 0, kCfgMulti128 = 17, kCfgMulti64 = 18, kCfgStemHalo = 30, kCfgFirst3x3 = 31, kCfgGeneric = 100 };
 enum { kWgHalo = 0, kWgFastRow64x256 = 1, kWgFastRow128 = 2, kWgFast64x256 = 3, kWgFast128 = 4, kWgGeneric = 5,
        kWgRing64x256 = 6, kWgRing128 = 7 };
 
@@ -141,3 +141,11 @@ bool wgrad_ring_ok(const FastWgradArgs& a);  // launch_wgrad_fast takes the LDS-
 int launch_wgrad_ring(const FastWgradArgs& a, int splits, hipStream_t st);  // conv_wgrad_ring.hip
 int wgrad_fast_splits(int Cout, int Ng, long Kpix);
 int launch_wgrad_fast(FastWgradArgs a, int splits, hipStream_t st);
+
+// the plain / attention U-Nets' first 3x3 conv on the packed image (conv_first.hip): 3 -> 64 channels,
+// one K = 32 MFMA step per pixel fragment; BN partials per 8 x 32 tile (first3x3_tile_m() pixels)
+bool first3x3_ok(int dtype, int c1, int ldc1, int c2, int n, int h, int w, int cout, int r, int s, int stride, int pad,
+                 int ldy);
+int first3x3_tile_m();
+int launch_first3x3(const void* x, int ldx, const void* wk, const float* bias, int relu, void* y, int ldy, float* stats,
+                    int n, int h, int w, hipStream_t st);
