@@ -260,8 +260,11 @@ WG_FLUSH = os.environ.get("UNETSEG_WG_FLUSH", "layer4")
 #: one-block-per-CU halo kernels sharing the CUs each take ~2x their isolated time (UNETSEG_WG_SERIAL_HW)
 WG_SERIAL_HW = int(os.environ.get("UNETSEG_WG_SERIAL_HW", "0"))
 #: encoder layers ("stem", "layer1", ...) whose weight gradients run on the compute stream: at the end of
-#: the backward the weight-gradient stream lags the compute stream (UNETSEG_WG_SERIAL_LAYERS, comma list)
-WG_SERIAL_LAYERS = frozenset(v for v in os.environ.get("UNETSEG_WG_SERIAL_LAYERS", "stem,layer1").split(",") if v)
+#: the backward the weight-gradient stream lags the compute stream (UNETSEG_WG_SERIAL_LAYERS, comma list).
+#: Round 4 (eager host) measured stem + layer1 best; with the step plan's replayed host (round 5, two
+#: interleaved repeats each) the stem alone: C2 1007-1011 vs 997-998 img/s, C5 807-810 vs 797-799
+#: (layer1 serial no better than stem + layer1; none equal to stem within noise)
+WG_SERIAL_LAYERS = frozenset(v for v in os.environ.get("UNETSEG_WG_SERIAL_LAYERS", "stem").split(",") if v)
 
 #: only the virtual-concat convs (the decoder's unetUp conv1) are held back (UNETSEG_WG_DEFER_CAT=0: every 3x3)
 WG_DEFER_CAT = os.environ.get("UNETSEG_WG_DEFER_CAT", "1") == "1"
