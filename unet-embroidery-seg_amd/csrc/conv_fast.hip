@@ -1211,7 +1211,8 @@ int launch_tn_cfg(const FastTNArgs& a, hipStream_t st) {
   // the gather ring; the halo-A ring is built on them
   static const bool t2d = getenv("UNETSEG_T2D") != nullptr;
   b.t2d = (HA || (t2d && a.nr * a.ns > 1 && a.wc % 32 == 0 && a.wc > 32 && a.hc % TR == 0)) ? TR : 0;
-  static const int sched = getenv("UNETSEG_TN_SCHED") ? atoi(getenv("UNETSEG_TN_SCHED")) : 0;
+  // default 1 since round 5 (with the replayed step plan: +0.1-0.2 % in the step; 0 restores the round-4 issue order)
+  static const int sched = getenv("UNETSEG_TN_SCHED") ? atoi(getenv("UNETSEG_TN_SCHED")) : 1;
   b.sched = sched;
   hipLaunchKernelGGL((tn_fast_kernel<BM, BN, NWM, NWN, ST, POST, TAPS, PRE, HA>), grid, dim3(NT), lds, st, b);
   return 0;
@@ -1477,7 +1478,8 @@ int wgrad_fast_splits(int Cout, int Ng, long Kpix) {
   const int bn = Cout <= 64 ? 256 : 128;
   const int tiles = ceil_div(Cout, bm) * ceil_div(Ng, bn);
   const long nkt = (Kpix + kWgBK - 1) / kWgBK;
-  static const int wscale = getenv("UNETSEG_WG_BLOCKS") ? atoi(getenv("UNETSEG_WG_BLOCKS")) : 0;
+  // 256 target blocks since round 5 (replayed step: +0.1-0.2 %, smaller split-K slabs; 0 = 1024 / 512)
+  static const int wscale = getenv("UNETSEG_WG_BLOCKS") ? atoi(getenv("UNETSEG_WG_BLOCKS")) : 256;
   int sp = ceil_div(wscale > 0 ? wscale : (Cout <= 64 ? 1024 : 512), tiles);  // 2-4 blocks per CU
   const long max_sp = nkt / 32 > 0 ? nkt / 32 : 1;  // >= 32 K steps per split
   if (sp > max_sp) sp = (int)max_sp;

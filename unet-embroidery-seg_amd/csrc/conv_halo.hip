@@ -1424,15 +1424,16 @@ static int launch_halo3_hs(const FastTNArgs& a, hipStream_t st) {
   return 0;
 }
 
-// The half-stage pipeline (HS) for the 8-wave kernels (UNETSEG_HALO_HS=0: the whole-tile double
-// buffer).  Isolated, a 512^2 layer (64 tiles per block) is slower with it (fwd 349-363 vs 296-312 us:
-// a second barrier per tile) and a 256^2 one faster (104.8 vs 124.6 us: the three-half prologue hides
-// the first tile's load); in the training step, beside the weight-gradient stream, HS everywhere
-// measured best: C2 972.8 vs 962.1 img/s without it and 971.2 with it on <= 16 tiles per block only,
-// C4 417.3 vs 410.7 / 411.2 (three interleaved repeats).
+// The half-stage pipeline (HS) for the 8-wave kernels (UNETSEG_HALO_HS=1; default: the whole-tile
+// double buffer; read per call, the parity tests run both).  Isolated, a 512^2 layer (64 tiles per
+// block) is slower with it (fwd 349-363 vs 296-312 us: a second barrier per tile) and a 256^2 one
+// faster (104.8 vs 124.6 us: the three-half prologue hides the first tile's load).  Round 4 (eager
+// host) measured HS everywhere best in the step (C2 972.8 vs 962.1 img/s); with the replayed step plan
+// of round 5 the double buffer is (C2 1016-1019 vs 1010-1011 on one box, 958-959 vs 957 on another).
 template <int TH, int NW, int POST, int EPI>
 static int launch_halo3_cfg(const FastTNArgs& a, hipStream_t st) {
-  static const bool hs = !getenv("UNETSEG_HALO_HS") || atoi(getenv("UNETSEG_HALO_HS")) != 0;
+  const char* e = getenv("UNETSEG_HALO_HS");
+  const bool hs = e != nullptr && atoi(e) != 0;
   if constexpr (NW == 8) {
     if (hs) return launch_halo3_hs<TH, NW, POST, EPI, true>(a, st);
   }

@@ -252,7 +252,8 @@ class Ctx:
 WG_DEFER_HW = int(os.environ.get("UNETSEG_WG_DEFER_HW", "1024"))
 #: where the flush marker sits in forward order: "decoder" (before the decoder), "layer4" / "layer3" / "layer2"
 #: (before that encoder layer: in backward the held-back gradients start once that layer's backward is done)
-WG_FLUSH = os.environ.get("UNETSEG_WG_FLUSH", "layer4")
+#: (round 5, replayed step plan: layer3 +0.1-0.3 % over layer4; round 4's eager host had layer4 best)
+WG_FLUSH = os.environ.get("UNETSEG_WG_FLUSH", "layer3")
 
 
 #: weight gradients of 3x3 convs whose output has >= this many pixels per image run on the compute stream
