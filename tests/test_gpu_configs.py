@@ -586,13 +586,23 @@ def test_bench_configs_covered(model_name, batch):
     assert not missing, f"{model_name} B={batch}: configurations without a parity case: {missing}"
 
 
+@pytest.mark.parametrize("cid", [c for c in CASES if "halo3" in c and not c.startswith("wgrad")])
+def test_halo3_case_hs(cid, monkeypatch):
+    """the halo3 cases again on the half-tile pipeline (UNETSEG_HALO_HS=1, read per launch; the
+    default since round 5 is the whole-tile double buffer)"""
+    monkeypatch.setenv("UNETSEG_HALO_HS", "1")
+    _run_case(cid, *CASES[cid])
+
+
+@pytest.mark.parametrize("hs", ["0", "1"])
 @pytest.mark.parametrize("direction", ["fwd_relu", "fwd_stats", "post1", "dgrad"])
-def test_halo3_hs_repeat_bit_identical(direction):
+def test_halo3_hs_repeat_bit_identical(direction, hs, monkeypatch):
     """the halo3 half-tile pipeline's waits are hand-counted vmcnt values (conv_halo.hip
     hs_wait); a count too high would let a tap read a half stage before its DMA landed -- a silent LDS
     race.  The same 512^2 launch, three times in one process (and at 128^2 with several tiles per
-    block), must give bit-identical outputs."""
+    block), must give bit-identical outputs -- on the half-tile pipeline and on the double buffer."""
     from unetseg_hip.lib import DT_BF16, lib
+    monkeypatch.setenv("UNETSEG_HALO_HS", hs)
     for shape in ((4, 512, 512, 64, 0, 64, 3, 1), (5, 128, 128, 64, 0, 64, 3, 1)):
         N, H, W, C1, C2, K, R, s = shape
         op = _Op(shape, RNG + 77)
