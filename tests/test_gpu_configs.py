@@ -76,8 +76,9 @@ CASES = {
     "fwd_tn64x128": ("fwd_all", (1, 64, 64, 512, 0, 128, 1, 1), ["fwd:tn64x128"]),
     # batch 8 (attention_unet / multitask_unet, BASELINE C4 / C5): layer2 conv1 512 -> 128 at 64^2
     "fwd_tn128x128": ("fwd_all", (8, 64, 64, 512, 0, 128, 1, 1), ["fwd:tn128x128"]),
-    # generic kernel: the first conv of unet_plain / attention_unet (3 input channels padded to 8)
-    "fwd_generic_cin8": ("fwd_stats", (2, 64, 64, 8, 0, 64, 3, 1), ["fwd:generic"]),
+    # generic kernel: an 8-channel first conv whose width is not a multiple of 32 (odd input sizes;
+    # the 512^2 / 128^2 configurations run first3x3, the cases above)
+    "fwd_generic_cin8": ("fwd_stats", (2, 64, 72, 8, 0, 64, 3, 1), ["fwd:generic"]),
     # ---- data gradient (plain / accumulated) ----
     "dgrad_halo3": ("dgrad", (1, 128, 128, 64, 0, 64, 3, 1), ["dgrad:halo3"]),
     "dgrad_halo3_multi": ("dgrad", (5, 128, 128, 64, 0, 64, 3, 1), ["dgrad:halo3"]),
