@@ -1418,7 +1418,11 @@ static int launch_halo3_hs(const FastTNArgs& a, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  const unsigned y_bytes = (unsigned)((long)a.M * a.ldy * 2);
+  // experiment (UNETSEG_HALO_EXP_NOSTORE=1, wrong results): a zero-extent output descriptor -- the
+  // output stores still issue (the vmcnt bookkeeping is unchanged) but the hardware drops them, so the
+  // launch time without the output's HBM writes can be measured
+  static const bool nostore = getenv("UNETSEG_HALO_EXP_NOSTORE") != nullptr;
+  const unsigned y_bytes = nostore ? 0u : (unsigned)((long)a.M * a.ldy * 2);
   hipLaunchKernelGGL((halo3_kernel<TH, NW, POST, EPI, HS>), dim3(ntn * G_per), dim3(64 * NW), lds, st, a, tiles_w, tiles_h,
                      n_sp, G_per, y_bytes);
   return 0;
