@@ -661,7 +661,8 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
   }
   if (POST == 1) {
     // mask the rounded gradient with the producer's ReLU (recomputed from aux) and reduce its
-    // backward partials over the wave's rows: q0 = sum d, q1 = sum d * xhat (BN)
+    // backward partials over the wave's rows: q0 = sum d, q1 = sum d * xhat (BN) (one reduction chain
+    // pair at a time: row16_sum_n over a channel group's 8 spills in the 5-stage 128x128 tile)
 #pragma unroll
     for (int c = 0; c < FC; ++c) {
       const int nb = n0 + wn * WTN + c * 16 + kg * 4;
@@ -710,13 +711,20 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
       *reinterpret_cast<uint2*>(tl + (p * 16 + j16) * LROW + (c * 16 + kg * 4) * 2) = *reinterpret_cast<uint2*>(ob);
     }
   if (a.stats) {
+    // (sum, M2 about the wave mean) of each of the lane's FC * 4 channels over the wave's rows; the
+    // row reductions run together (row16_sum_n)
+    float sv[FC * 4], qv[FC * 4];
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sv[c * 4 + e] = csum[c][e];
+    row16_sum_n(sv);
+    const float inv_cnt = 1.0f / (float)max(cnt, 1);
 #pragma unroll
     for (int c = 0; c < FC; ++c)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        float sm = csum[c][e];
-        sm = row16_sum(sm);
-        const float mean = sm / (float)max(cnt, 1);
+        const float mean = sv[c * 4 + e] * inv_cnt;
         float q = 0.f;
 #pragma unroll
         for (int p = 0; p < FP; ++p)
@@ -724,13 +732,18 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
             const float d = acc[c][p][e] - mean;
             q += d * d;
           }
-        q = row16_sum(q);
-        if (j16 == 0) {
-          const int col = wn * WTN + c * 16 + kg * 4 + e;
-          red[wm * BN + col] = sm;
-          red[(NWM + wm) * BN + col] = q;
-        }
+        qv[c * 4 + e] = q;
       }
+    row16_sum_n(qv);
+    if (j16 == 0)
+#pragma unroll
+      for (int c = 0; c < FC; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int col = wn * WTN + c * 16 + kg * 4 + e;
+          red[wm * BN + col] = sv[c * 4 + e];
+          red[(NWM + wm) * BN + col] = qv[c * 4 + e];
+        }
   }
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS tile is written
   __builtin_amdgcn_wave_barrier();

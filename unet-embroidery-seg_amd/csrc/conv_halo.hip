@@ -116,6 +116,8 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
                                         HK ? (unsigned)(a.M / (a.OH * a.OW)) * HK * hw_img * 4u : 0u);
   const __amdgpu_buffer_rsrc_t rmb =
       srd(kMask ? (const void*)a.mbits_out : a.y, kMask ? (unsigned)a.M * (unsigned)(a.Ng >> 3) : 0u);
+  const __amdgpu_buffer_rsrc_t rst =
+      srd(do_stats ? (const void*)a.stats : a.y, do_stats ? (unsigned)n_sp * 2u * (unsigned)a.Ng * 4u : 0u);
 
   if (kDyn && a.bias && tid < 64) sbias[tid] = a.bias[n0 + tid];
   // BN post-op coefficients of this block's 64 channels live in `red` (free in dgrad: no stats)
@@ -343,35 +345,58 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
         }
       }
     } else {
+      // 18 steps (tap jt, K half kk), software-pipelined: the fragments of step s+1 are read before
+      // the MFMAs of step s and sched_group_barrier pins that order -- left to itself the scheduler
+      // issued each read right before its MFMAs, and with 2 MFMAs per LDS round trip the waves sat on
+      // lgkmcnt (MFMA busy 45 %, SQ_LDS_IDX_ACTIVE 34 % at 512^2)
       const uint4* hs = hl + stage * HCH;
-#pragma unroll
-      for (int jt = 0; jt < 9; ++jt) {
+      auto frag_load = [&](int st, bf16x8 (&wf)[FC], bf16x8 (&pf)[FP]) {
+        const int jt = st >> 1, kk = st & 1;
         const int jr = jt / 3, js = jt - jr * 3;
         const int dh = dh0 + dhs * jr, dw = dw0 + dws * js;
+        const int ch = kk * 4 + kg;
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const int ch = kk * 4 + kg;
-          bf16x8 wf[FC], pf[FP];
-#pragma unroll
-          for (int c = 0; c < FC; ++c) {
-            const int row = jt * 64 + c * 16 + j16;
-            uint4 v = wl[row * 8 + swz8(row, ch)];
-            wf[c] = *reinterpret_cast<bf16x8*>(&v);
-          }
-#pragma unroll
-          for (int p = 0; p < FP; ++p) {
-            const int r = wid * RPW + p / (HW_TW / 16);
-            const int col = (p % (HW_TW / 16)) * 16 + j16;
-            const int hp = (r + 1 + dh) * (HW_TW + 2) + col + 1 + dw;
-            uint4 v = hs[hp * 8 + swzh(hp, ch)];
-            pf[p] = *reinterpret_cast<bf16x8*>(&v);
-          }
-#pragma unroll
-          for (int c = 0; c < FC; ++c)
-#pragma unroll
-            for (int p = 0; p < FP; ++p)
-              acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], pf[p], acc[c][p], 0, 0, 0);
+        for (int c = 0; c < FC; ++c) {
+          const int row = jt * 64 + c * 16 + j16;
+          uint4 v = wl[row * 8 + swz8(row, ch)];
+          wf[c] = *reinterpret_cast<bf16x8*>(&v);
         }
+#pragma unroll
+        for (int p = 0; p < FP; ++p) {
+          const int r = wid * RPW + p / (HW_TW / 16);
+          const int col = (p % (HW_TW / 16)) * 16 + j16;
+          const int hp = (r + 1 + dh) * (HW_TW + 2) + col + 1 + dw;
+          uint4 v = hs[hp * 8 + swzh(hp, ch)];
+          pf[p] = *reinterpret_cast<bf16x8*>(&v);
+        }
+      };
+      bf16x8 wfb[2][FC], pfb[2][FP];
+      frag_load(0, wfb[0], pfb[0]);
+      __builtin_amdgcn_sched_group_barrier(0x100, FC + FP, 0);
+#pragma unroll
+      for (int st = 0; st < 18; ++st) {
+        if (st + 1 < 18) frag_load(st + 1, wfb[(st + 1) & 1], pfb[(st + 1) & 1]);
+#pragma unroll
+        for (int c = 0; c < FC; ++c)
+#pragma unroll
+          for (int p = 0; p < FP; ++p)
+            acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfb[st & 1][c], pfb[st & 1][p], acc[c][p], 0, 0, 0);
+#if UNETSEG_HALO3_INTERLEAVE
+        // reads of step s+1 spread between the MFMAs of step s
+        if (st + 1 < 18) {
+#pragma unroll
+          for (int i = 0; i < FC + FP; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, FC * FP - (FC + FP), 0);
+        } else {
+          __builtin_amdgcn_sched_group_barrier(0x008, FC * FP, 0);
+        }
+#else
+        if (st + 1 < 18) __builtin_amdgcn_sched_group_barrier(0x100, FC + FP, 0);  // DS reads of step st+1
+        __builtin_amdgcn_sched_group_barrier(0x008, FC * FP, 0);                    // MFMAs of step st
+#endif
       }
     }
 
@@ -484,53 +509,70 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
       }
     }
     if (do_stats) {
-      // per-tile BN partials over the TH*32 pixels: column sums, then M2 about the tile mean
+      // per-tile BN partials over the TH*32 pixels (sum, M2 about the tile mean): each wave reduces its
+      // own 16 * FP pixels to (sum, M2 about the wave mean) in registers -- the 16 channel values of a
+      // lane reduced together over the row's 16 lanes (row16_sum_n) -- and wave 0 merges the NW waves
+      // (Chan: M2 = sum M2_w + n_w (mean_w - mean)^2), the sums and then the M2s passing through `red`
+      // (no room in LDS for both at once).  Until round 5 every lane fetched the tile mean of its 16
+      // channels from LDS and the 32 row reductions ran one chain at a time: the statistics epilogue
+      // cost almost half as much as the convolution (16 x 512^2: 475 vs 325 us)
+      float sv[FC * 4], qv[FC * 4];
+#pragma unroll
+      for (int c = 0; c < FC; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sv[c * 4 + e] = csum[c][e];
+      row16_sum_n(sv);
 #pragma unroll
       for (int c = 0; c < FC; ++c)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float s = csum[c][e];
-          s = row16_sum(s);
-          if (j16 == 0) red[wid * 64 + c * 16 + kg * 4 + e] = s;
-        }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      float qv[FC][4];
-#pragma unroll
-      for (int c = 0; c < FC; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int col = c * 16 + kg * 4 + e;
-          float tot = 0.f;
-#pragma unroll
-          for (int w = 0; w < NW; ++w) tot += red[w * 64 + col];
-          const float mean = tot * (1.0f / (TH * HW_TW));
+          const float mw = sv[c * 4 + e] * (1.0f / (16 * FP));
           float q = 0.f;
 #pragma unroll
           for (int p = 0; p < FP; ++p) {
-            const float d = acc[c][p][e] - mean;
+            const float d = acc[c][p][e] - mw;
             q += d * d;
           }
-          q = row16_sum(q);
-          qv[c][e] = q;
+          qv[c * 4 + e] = q;
         }
-      float stot = 0.f;
+      row16_sum_n(qv);
+      if (j16 == 0)
+#pragma unroll
+        for (int c = 0; c < FC; ++c)
+          *reinterpret_cast<float4*>(red + wid * 64 + c * 16 + kg * 4) =
+              float4{sv[c * 4], sv[c * 4 + 1], sv[c * 4 + 2], sv[c * 4 + 3]};
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      float sw[NW];
       if (tid < 64)
 #pragma unroll
-        for (int w = 0; w < NW; ++w) stot += red[w * 64 + tid];
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // sums consumed: reuse red for M2
+        for (int w = 0; w < NW; ++w) sw[w] = red[w * 64 + tid];
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // sums read: reuse red for M2
+      if (j16 == 0)
 #pragma unroll
-      for (int c = 0; c < FC; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (j16 == 0) red[wid * 64 + c * 16 + kg * 4 + e] = qv[c][e];
+        for (int c = 0; c < FC; ++c)
+          *reinterpret_cast<float4*>(red + wid * 64 + c * 16 + kg * 4) =
+              float4{qv[c * 4], qv[c * 4 + 1], qv[c * 4 + 2], qv[c * 4 + 3]};
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      float tot = 0.f, q = 0.f;
       if (tid < 64) {
-        float q = 0.f;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) q += red[w * 64 + tid];
-        a.stats[(long)sp * 2 * a.Ng + n0 + tid] = stot;
-        a.stats[(long)sp * 2 * a.Ng + a.Ng + n0 + tid] = q;
+        for (int w = 0; w < NW; ++w) {
+          tot += sw[w];
+          q += red[w * 64 + tid];
+        }
+        const float mean = tot * (1.0f / (TH * HW_TW));
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const float d = sw[w] * (1.0f / (16 * FP)) - mean;
+          q = fmaf((float)(16 * FP) * d, d, q);
+        }
       }
+      // buffer stores issued by every wave (only wave 0's land), counted in the tile's closing wait:
+      // as plain stores of wave 0 alone they were retired by that wait -- a full write round trip per
+      // tile with the whole block parked on the barrier behind it (16 x 512^2: +140 us)
+      const unsigned so = tid < 64 ? (unsigned)(sp * 2 * a.Ng + n0 + tid) * 4u : kOOB;
+      bstore32(rst, so, tot);
+      bstore32(rst, tid < 64 ? so + (unsigned)a.Ng * 4u : kOOB, q);
     }
     // output stores last: exactly FP*FC buffer stores per wave after the next tile's DMA
 #pragma unroll
@@ -544,8 +586,14 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
       for (int p = 0; p < FP; ++p) bstore64(rmb, kg == 0 ? mko[p] : kOOB, uint2{mkx[p], mky[p]});
     // next halo landed (all but this tile's stores retired) and every wave is done with both the
     // current stage (WAR for the DMA after next) and `red` (HS: the next half's wait does both)
-    if constexpr (!HS)
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(FP * FC + FP * HK + (kMask ? FP : 0)) : "memory");
+    // (HS: the two statistics stores are not in hs_wait's counts -- it waits for them too, which is
+    // only slower)
+    if constexpr (!HS) {
+      if (do_stats)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NS_ + 2) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NS_) : "memory");
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // HS: the past-the-end halves are still landing in the stages of other waves
@@ -745,48 +793,59 @@ __global__ __launch_bounds__(64 * NW) void stem_halo_kernel(const bf16* xp, unsi
         outv[c][p] = *reinterpret_cast<uint2*>(o);
       }
     }
+    // BN partials as halo3_kernel's: (sum, M2 about the wave mean) per wave in registers, merged by
+    // wave 0 (Chan), the sums and then the M2s through `red`
+    float sv[FC * 4], qv[FC * 4];
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sv[c * 4 + e] = csum[c][e];
+    row16_sum_n(sv);
 #pragma unroll
     for (int c = 0; c < FC; ++c)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float s = row16_sum(csum[c][e]);
-        if (j16 == 0) red[wid * 64 + c * 16 + kg * 4 + e] = s;
-      }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    float qv[FC][4];
-#pragma unroll
-    for (int c = 0; c < FC; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int col = c * 16 + kg * 4 + e;
-        float tot = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) tot += red[w * 64 + col];
-        const float mean = tot * (1.0f / (TH * HW_TW));
+        const float mw = sv[c * 4 + e] * (1.0f / (16 * FP));
         float q = 0.f;
 #pragma unroll
         for (int p = 0; p < FP; ++p) {
-          const float d = acc[c][p][e] - mean;
+          const float d = acc[c][p][e] - mw;
           q += d * d;
         }
-        qv[c][e] = row16_sum(q);
+        qv[c * 4 + e] = q;
       }
-    float stot = 0.f;
+    row16_sum_n(qv);
+    if (j16 == 0)
+#pragma unroll
+      for (int c = 0; c < FC; ++c)
+        *reinterpret_cast<float4*>(red + wid * 64 + c * 16 + kg * 4) =
+            float4{sv[c * 4], sv[c * 4 + 1], sv[c * 4 + 2], sv[c * 4 + 3]};
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float sw[NW], stot = 0.f;
     if (tid < 64)
 #pragma unroll
-      for (int w = 0; w < NW; ++w) stot += red[w * 64 + tid];
+      for (int w = 0; w < NW; ++w) {
+        sw[w] = red[w * 64 + tid];
+        stot += sw[w];
+      }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (j16 == 0)
 #pragma unroll
-    for (int c = 0; c < FC; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (j16 == 0) red[wid * 64 + c * 16 + kg * 4 + e] = qv[c][e];
+      for (int c = 0; c < FC; ++c)
+        *reinterpret_cast<float4*>(red + wid * 64 + c * 16 + kg * 4) =
+            float4{qv[c * 4], qv[c * 4 + 1], qv[c * 4 + 2], qv[c * 4 + 3]};
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     {
       float q = 0.f;
-      if (tid < 64)
+      if (tid < 64) {
+        const float mean = stot * (1.0f / (TH * HW_TW));
 #pragma unroll
-        for (int w = 0; w < NW; ++w) q += red[w * 64 + tid];
+        for (int w = 0; w < NW; ++w) {
+          q += red[w * 64 + tid];
+          const float d = sw[w] * (1.0f / (16 * FP)) - mean;
+          q = fmaf((float)(16 * FP) * d, d, q);
+        }
+      }
       // every wave issues both stats stores (only wave 0's lanes land): exact per-wave counts
       const unsigned so = tid < 64 ? (unsigned)(sp * 128 + tid) * 4u : kOOB;
       bstore32(rs, so, stot);

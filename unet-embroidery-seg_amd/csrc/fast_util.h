@@ -106,4 +106,19 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// row16_sum of N independent values, rotation-major: each value gets exactly row16_sum's additions,
+// but the N chains interleave -- issued one chain at a time, every dependent DPP add waited out its
+// VALU-to-DPP hazard (s_nop), and an epilogue with 32 of them spent more time there than on its stores
+template <int N>
+__device__ __forceinline__ void row16_sum_n(float (&v)[N]) {
+#define ROW16_STEP(CTL)                                                                                      \
+  _Pragma("unroll") for (int i = 0; i < N; ++i) v[i] +=                                                      \
+      __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v[i]), CTL, 0xF, 0xF, false));
+  ROW16_STEP(0x128)
+  ROW16_STEP(0x124)
+  ROW16_STEP(0x122)
+  ROW16_STEP(0x121)
+#undef ROW16_STEP
+}
+
 }  // namespace
