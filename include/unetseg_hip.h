@@ -387,6 +387,10 @@ int unetseg_augment_tables_dev(const long long* desc, int B, const double* hsv_r
 /* `waiter` waits for everything enqueued so far on `signaler` (device-scope release event; no
    reference counterpart: orders the weight-gradient stream against the compute stream) */
 int unetseg_stream_wait(void* waiter, void* signaler);
+/* a stream restricted to the CUs set in mask[0 .. n_words) (bit i of word w = CU 32 w + i); *out = the
+   hipStream_t (no reference counterpart: keeps the weight-gradient stream's persistent kernels off
+   part of the chip, UNETSEG_SIDE_CUMASK) */
+int unetseg_stream_create_cumask(const unsigned* mask, int n_words, void** out);
 
 /* ---- multitask classification head (model/unet_multitask.py:73-80) -------------------------- */
 int unetseg_gap_fwd(int dtype, const void* x, int ldx, int B, int HW, int C, float* g, void* stream);

@@ -44,6 +44,13 @@ __device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, unsigned off,
 constexpr int kEpiBias = 1, kEpiRelu = 2, kEpiStats = 4, kEpiAcc = 8, kEpiDyn = 16, kEpiHead1 = 32, kEpiHead2 = 64,
               kEpiMask = 128;
 
+// an 8-B buffer load the compiler does not track: the caller waits for it with an explicit vmcnt (so the
+// wait can leave later LDS-DMAs in flight) and then ties the value with asm volatile("" : "+v"(v))
+__device__ __forceinline__ uint2 bload64_asm(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  uint2 v;
+  asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
+  return v;
+}
 __device__ __forceinline__ void bstore32(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
   asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
 }
@@ -118,6 +125,10 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
       srd(kMask ? (const void*)a.mbits_out : a.y, kMask ? (unsigned)a.M * (unsigned)(a.Ng >> 3) : 0u);
   const __amdgpu_buffer_rsrc_t rst =
       srd(do_stats ? (const void*)a.stats : a.y, do_stats ? (unsigned)n_sp * 2u * (unsigned)a.Ng * 4u : 0u);
+  // post-op inputs: POST 4 the mask bits [M][Ng/8], POST 1 / 2 the pre-activation aux [M][ld_aux]
+  const __amdgpu_buffer_rsrc_t raux =
+      POST == 4 ? srd(a.mbits, (unsigned)a.M * (unsigned)(a.Ng >> 3))
+                : srd(POST ? a.aux : a.y, POST ? (unsigned)a.M * (unsigned)a.ld_aux * 2u : 0u);
 
   if (kDyn && a.bias && tid < 64) sbias[tid] = a.bias[n0 + tid];
   // BN post-op coefficients of this block's 64 channels live in `red` (free in dgrad: no stats)
@@ -157,6 +168,9 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     hoff[i] = (unsigned)(hr * a.W + hc) * (unsigned)a.ldc1b + swzh(hp, lane & 7) * 16u;
     hflag[i] = idx >= HCH ? 16u : (hr == 0 ? 1u : 0u) | (hr == TH + 1 ? 2u : 0u) | (hc == 0 ? 4u : 0u) | (hc == HW_TW + 1 ? 8u : 0u);
   }
+  // halo DMA instructions this wave issues per tile: HI, or HI - 1 for the waves with no slot in the
+  // last one (issue_halo skips it)
+  const bool full_dma = HCH % (64 * NW) == 0 || ((HI - 1) * NW + wid) * 64 < HCH;
   auto issue_halo = [&](int t, int stage) {
     const int sp = slot + t * G_per;
     const int tw = sp % tiles_w, rest = sp / tiles_w;
@@ -273,13 +287,36 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     if constexpr (HS) {
       half_wait(2 * t);
       issue_half(2 * t + 3, (2 * t + 3) & 3);
-    } else {
-      if (t + 1 < my_tiles) issue_halo(t + 1, stage ^ 1);
     }
     // post-op: this tile's aux values are loaded now, so their latency hides under the tap loop
     uint2 zr[FC][FP];
     uint2 zb[FP];  // POST 4: the 8 mask bytes (64 channels) of this lane's pixel
-    if (POST == 4) {
+    if (!HS && POST) {
+      // double buffer: the aux loads go out BEFORE the next tile's DMA, as buffer loads the compiler
+      // does not track, and the epilogue waits for them with vmcnt(this wave's DMA count): waiting on
+      // loads issued after the DMA (in-order counter) retired the next tile's halo inside this tile --
+      // the prefetch was gone (16 x 512^2 post 4: 397 us against 281 for the plain data gradient)
+      const int sp = slot + t * G_per;
+      const int tw = sp % tiles_w, rest = sp / tiles_w;
+      const int th = rest % tiles_h, nb = rest / tiles_h;
+#pragma unroll
+      for (int p = 0; p < FP; ++p) {
+        const int r = wid * RPW + p / (HW_TW / 16);
+        const int col = (p % (HW_TW / 16)) * 16 + j16;
+        const unsigned opix = (unsigned)((nb * a.OH + th * TH + r) * a.OW + tw * HW_TW + col);
+        if (POST == 4) {
+          zb[p] = bload64_asm(raux, opix * (unsigned)(a.Ng >> 3) + (unsigned)(n0 >> 3));
+        } else {
+#pragma unroll
+          for (int c = 0; c < FC; ++c)
+            zr[c][p] = bload64_asm(raux, (opix * (unsigned)a.ld_aux + (unsigned)(n0 + c * 16 + kg * 4)) * 2u);
+        }
+      }
+    }
+    if constexpr (!HS) {
+      if (t + 1 < my_tiles) issue_halo(t + 1, stage ^ 1);
+    }
+    if (HS && POST == 4) {
       const int sp = slot + t * G_per;
       const int tw = sp % tiles_w, rest = sp / tiles_w;
       const int th = rest % tiles_h, nb = rest / tiles_h;
@@ -290,7 +327,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
         const long opix = ((long)nb * a.OH + th * TH + r) * a.OW + tw * HW_TW + col;
         zb[p] = *reinterpret_cast<const uint2*>(a.mbits + opix * (a.Ng >> 3) + (n0 >> 3));
       }
-    } else if (POST) {
+    } else if (HS && POST) {
       const int sp = slot + t * G_per;
       const int tw = sp % tiles_w, rest = sp / tiles_w;
       const int th = rest % tiles_h, nb = rest / tiles_h;
@@ -401,6 +438,26 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     }
 
     // ================= epilogue =================
+    if (!HS && POST) {
+      // this tile's aux loads landed; the next tile's halo (this wave's DMAs, issued after them) may fly
+      if (t + 1 < my_tiles) {
+        if (full_dma)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HI) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HI - 1) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+#pragma unroll
+      for (int p = 0; p < FP; ++p) {
+        if (POST == 4) {
+          asm volatile("" : "+v"(zb[p]));
+        } else {
+#pragma unroll
+          for (int c = 0; c < FC; ++c) asm volatile("" : "+v"(zr[c][p]));
+        }
+      }
+    }
     const int sp = slot + t * G_per;
     const int tw = sp % tiles_w, rest = sp / tiles_w;
     const int th = rest % tiles_h, nb = rest / tiles_h;
@@ -1038,11 +1095,6 @@ __global__ __launch_bounds__(64 * NW) void halo3_wgrad_kernel(HaloWgradArgs a, i
 //   vmcnt values: the epilogue waits for this tile's aux loads (issued before tile t+2's DMA), the
 //   end of a tile for tile t+1's halo; tile t+2's DMA stays in flight across the barrier.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint2 bload64_asm(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  uint2 v;
-  asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
-  return v;
-}
 
 template <int NW>
 constexpr int halo3r_stage_chunks() {
@@ -1457,6 +1509,8 @@ bool halo3_ok(const FastTNArgs& a) {
   if (a.ostride != 1 || a.ph || a.pw || a.OH != a.hc || a.OW != a.wc || a.H != a.hc || a.W != a.wc) return false;
   if (a.Ng % 64 || a.hc % 8 || a.wc % HW_TW) return false;
   if ((long)a.M * a.ldy * 2 >= (1L << 31)) return false;
+  if (a.post && a.post != 4 && (long)a.M * a.ld_aux * 2 >= (1L << 31)) return false;
+  if (a.post == 4 && (long)a.M * (a.Ng >> 3) >= (1L << 31)) return false;
   return true;
 }
 

@@ -28,6 +28,22 @@ UNETSEG_API int unetseg_device_arch(char* buf, int n) {
   return 0;
 }
 
+// A stream restricted to the CUs whose bits are set in mask[0 .. n_words) (bit i of word w = CU 32 w + i):
+// the weight-gradient stream's persistent kernels hold a CU's LDS for their whole life, and a
+// compute-stream kernel that needs a large LDS image cannot start a block beside them
+// (UNETSEG_SIDE_CUMASK, ops.side_stream).  *out receives the hipStream_t.
+UNETSEG_API int unetseg_stream_create_cumask(const unsigned* mask, int n_words, void** out) {
+  US_CHECK_ARG(mask != nullptr && out != nullptr && n_words > 0, "stream_create_cumask: bad arguments");
+  hipStream_t s = nullptr;
+  const hipError_t err = hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, mask);
+  if (err != hipSuccess) {
+    unetseg_set_error("stream_create_cumask: %s", hipGetErrorString(err));
+    return 2;
+  }
+  *out = (void*)s;
+  return 0;
+}
+
 // Cross-stream ordering for the op layer's weight-gradient stream: `waiter` waits for the work
 // enqueued so far on `signaler`.  The events carry a device-scope release only (both streams are
 // on one device): the default system-scope fence costs ~6 us of idle compute stream per sync.

@@ -84,6 +84,7 @@ SIGNATURES = {
     "unetseg_ce_fwd": (I, [P, P, I, I, P, P, P]),
     "unetseg_scale_grad": (I, [P, L, P, F, P, F, P, P]),
     "unetseg_stream_wait": (I, [P, P]),
+    "unetseg_stream_create_cumask": (I, [P, I, P]),
     "unetseg_conv2d_dgrad_post": (I, [I, P, I, I, I, I, P, I, I, I, I, I, I, P, I, I, I, I, P, I, P, P, P, P, P, I,
                                       P]),
     "unetseg_bn_bwd_finalize_rows": (I, [P, I, I, L, P, P, P, P, P, P]),

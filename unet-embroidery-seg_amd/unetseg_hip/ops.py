@@ -149,10 +149,25 @@ _SIDE = {}
 SIDE_PRIORITY = int(os.environ.get("UNETSEG_SIDE_PRIORITY", "0"))
 
 
+#: UNETSEG_SIDE_CUMASK=<hex word>: the weight-gradient stream runs only on the CUs of that 32-bit
+#: pattern, repeated over the chip (e.g. 55555555: every other CU), so its persistent kernels, which
+#: hold a CU's LDS for their whole life, never keep a compute-stream kernel off every CU
+SIDE_CUMASK = os.environ.get("UNETSEG_SIDE_CUMASK")
+
+
 def side_stream(device):
     key = (device.type, device.index)
     if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device, priority=SIDE_PRIORITY)
+        if SIDE_CUMASK:
+            import ctypes
+            n = (torch.cuda.get_device_properties(device).multi_processor_count + 31) // 32
+            words = (ctypes.c_uint32 * n)(*([int(SIDE_CUMASK, 16) & 0xFFFFFFFF] * n))
+            out = ctypes.c_void_p()
+            with torch.cuda.device(device):
+                lib.stream_create_cumask(ctypes.addressof(words), n, ctypes.addressof(out))
+            _SIDE[key] = torch.cuda.ExternalStream(out.value, device=device)
+        else:
+            _SIDE[key] = torch.cuda.Stream(device, priority=SIDE_PRIORITY)
     return _SIDE[key]
 
 
