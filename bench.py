@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--extra-configs", type=int, default=1,
                     help="also time C4 (attention_unet B=8, N=1 only) and C5 (multitask_unet B=8) after the headline")
     ap.add_argument("--card-probe", type=int, default=1, help="bf16 GEMM + HBM copy rate of this card (rank 0)")
+    ap.add_argument("--host-probe", type=int, default=1,
+                    help="host enqueue cost per step (parks the GPU on a spin kernel; 0 under a profiler)")
     ap.add_argument("--plan", type=int, default=1,
                     help="replay a recorded step plan (unetseg_hip/plan.py: the eager step's launches re-issued "
                          "from the host, every kernel every step) after one eager and one recording step")
@@ -447,7 +449,7 @@ def main():
     wall, median_ms, gpu_ms, loss, card_mid = timed(run, args.steps, args.warmup, world, dev,
                                                     sample=lambda: card_state(dev))
     peak_gib = torch.cuda.max_memory_allocated(dev) / 2 ** 30  # caching-allocator peak over warmup + timed steps
-    host_ms, host_load = host_enqueue_ms(run, dev, median_ms) if world == 1 else (None, None)
+    host_ms, host_load = host_enqueue_ms(run, dev, median_ms) if world == 1 and args.host_probe else (None, None)
     ms_per_step = 1000.0 * wall / args.steps
     imgs_per_s = args.batch * world * args.steps / wall
     final_loss = float(loss.item())
@@ -520,7 +522,7 @@ def main():
                                           sample=(lambda: card_state(dev)) if rank == 0 else None)
             peak2 = torch.cuda.max_memory_allocated(dev) / 2 ** 30
             ips = batch * world * k2 / w2
-            host2 = host_enqueue_ms(run2, dev, med2) if world == 1 else (None, None)
+            host2 = host_enqueue_ms(run2, dev, med2) if world == 1 and args.host_probe else (None, None)
             configs[tag] = {"workload": f"{name} {args.size}x{args.size}, per-GPU batch {batch}, "
                                         f"{loss_name}{' + ce' if name == 'multitask_unet' else ''} + Adam",
                             "value": round(ips, 2), "unit": "images/s", "steps": k2, "ms_per_step": round(1000.0 * w2 / k2, 3),

@@ -59,7 +59,8 @@ def main():
             torch.cuda.synchronize()
             if it >= 2:
                 for kind, fl, nl, e0, e1, desc in ops.PROBE:
-                    t = times.setdefault(desc[0], [1e9, fl])
+                    # dgrad_padk / wgrad_padk / fwd_bnrelu_in ... under their direction
+                    t = times.setdefault(desc[0].split("_")[0], [1e9, fl])
                     t[0] = min(t[0], e0.elapsed_time(e1) * 1e-3)  # best of reps
             ops.PROBE = None
         line = [f"{sh:34s}"]
