@@ -313,9 +313,34 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
         }
       }
     }
+    // the next tile's halo DMA, one instruction every other tap step inside the MFMA loop below
+    // (UNETSEG_HALO3_SPREAD, default): issued all at once here, the eight waves spent their issue
+    // cycles together at the tile start with the MFMA pipes idle (16 x 512^2 fwd 313 -> 302-309 us,
+    // dgrad 311 -> 307-309; -DUNETSEG_HALO3_SPREAD=0 builds the old order)
+#ifndef UNETSEG_HALO3_SPREAD
+#define UNETSEG_HALO3_SPREAD 1
+#endif
+    const bool dma_next = t + 1 < my_tiles;
+    unsigned nx_base = 0u, nx_hb = 0u, nx_kill = 0u;
     if constexpr (!HS) {
-      if (t + 1 < my_tiles) issue_halo(t + 1, stage ^ 1);
+      if (!UNETSEG_HALO3_SPREAD) {
+        if (dma_next) issue_halo(t + 1, stage ^ 1);
+      } else if (dma_next) {
+        const int sp = slot + (t + 1) * G_per;
+        const int tw = sp % tiles_w, rest = sp / tiles_w;
+        const int th = rest % tiles_h, nb = rest / tiles_h;
+        const int h0 = th * TH, w0 = tw * HW_TW;
+        nx_base = __builtin_amdgcn_readfirstlane(lds_addr(hl + (stage ^ 1) * HCH));
+        nx_hb = __builtin_amdgcn_readfirstlane((unsigned)((nb * a.H + h0 - 1) * a.W + w0 - 1) * (unsigned)a.ldc1b);
+        nx_kill = __builtin_amdgcn_readfirstlane(16u | (h0 == 0 ? 1u : 0u) | (h0 + TH >= a.H ? 2u : 0u) |
+                                                 (w0 == 0 ? 4u : 0u) | (w0 + HW_TW >= a.W ? 8u : 0u));
+      }
     }
+    auto issue_piece = [&](int i) {
+      if (!UNETSEG_HALO3_SPREAD || !dma_next) return;
+      const unsigned off = (hflag[i] & nx_kill) ? kOOB : nx_hb + hoff[i];
+      if (i < HI - 1 || HCH % (64 * NW) == 0 || hflag[i] != 16u) dma16(rx, nx_base + (unsigned)((i * NW + wid) * 1024), off);
+    };
     if (HS && POST == 4) {
       const int sp = slot + t * G_per;
       const int tw = sp % tiles_w, rest = sp / tiles_w;
@@ -434,6 +459,7 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
         if (st + 1 < 18) __builtin_amdgcn_sched_group_barrier(0x100, FC + FP, 0);  // DS reads of step st+1
         __builtin_amdgcn_sched_group_barrier(0x008, FC * FP, 0);                    // MFMAs of step st
 #endif
+        if ((st & 1) && (st >> 1) < HI) issue_piece(st >> 1);
       }
     }
 

@@ -43,12 +43,36 @@ static inline unsigned fin_threads(int nwv) { return nwv > 1 ? 64u * nwv : 256u;
     else hipLaunchKernelGGL(KERNEL<1>, grid_, block_, 0, (hipStream_t)(stream), __VA_ARGS__);              \
   } while (0)
 
+// fp64 sum over the wave, the same value in every lane: row rotations on the VALU (each 64-bit value
+// moved as two DPP halves) leave every lane of a 16-lane row with the row's total, then the four row
+// totals are read lane-uniform and added in a fixed order.  wave_sum_d (__shfl_xor) went through
+// ds_bpermute, two LDS round trips per step for a double: the finalize kernels sat on that chain
+template <int CTL>
+__device__ __forceinline__ double row_rot_add_d(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int lo2 = __builtin_amdgcn_update_dpp(0, lo, CTL, 0xF, 0xF, false);
+  const int hi2 = __builtin_amdgcn_update_dpp(0, hi, CTL, 0xF, 0xF, false);
+  return v + __hiloint2double(hi2, lo2);
+}
+__device__ __forceinline__ double wave_sum_d_uniform(double v) {
+  v = row_rot_add_d<0x128>(v);  // row_ror:8
+  v = row_rot_add_d<0x124>(v);  // row_ror:4
+  v = row_rot_add_d<0x122>(v);  // row_ror:2
+  v = row_rot_add_d<0x121>(v);  // row_ror:1
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  double t = 0.0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    t += __hiloint2double(__builtin_amdgcn_readlane(hi, 16 * r), __builtin_amdgcn_readlane(lo, 16 * r));
+  return t;
+}
+
 // sum over the channel's lanes (one wave, or the block's NWV waves through sc[NQ][NWV]); every lane
-// gets lane 0's / the fixed-order total
+// gets the same fixed-order total
 template <int NWV, int NQ>
 __device__ __forceinline__ void fin_group_sum(double (&v)[NQ], double* sc) {
 #pragma unroll
-  for (int j = 0; j < NQ; ++j) v[j] = __shfl(wave_sum_d(v[j]), 0, 64);
+  for (int j = 0; j < NQ; ++j) v[j] = wave_sum_d_uniform(v[j]);
   if constexpr (NWV > 1) {
     const int wid = threadIdx.x >> 6;
     __syncthreads();
