@@ -189,10 +189,12 @@ class Recorder:
 def check_segment(rec, k, weights, hip_grads, emu=True, dt=F64):
     """Rebuild segment k in float64 (or ``dt``: float32 gives the accumulation-noise reference) and
     compare.  weights(p) -> the parameter's value in the forward (pre-step snapshot); hip_grads(p)
-    -> its HIP gradient.  Returns a dict of {"params": [(param, rel, reference gradient)],
+    -> its HIP gradient.  Returns a dict of {"params": [(param, rel, reference gradient)], "bias_l1":
+    {id(bias): (L1, L2) norms of its gradient's summands},
     "inputs": [(index, rel)], "fwd": [(kind, rel)]}."""
     ops_k = [op for op in rec.ops if op[0] == k]
     vals, leaves, params = {}, {}, {}
+    bias_l1 = {}  # id(conv.bias) -> (L1, L2) of d loss / d conv output (the bias gradient's summands)
     fwd = []
 
     def pleaf(p, rnd):
@@ -239,6 +241,11 @@ def check_segment(rec, k, weights, hip_grads, emu=True, dt=F64):
                 x = x[:, :w.shape[1]]
             b = pleaf(conv.bias, False) if conv.bias is not None else None
             y = F.conv2d(x, w, b, conv.stride, conv.padding)
+            if b is not None and y.requires_grad:
+                # the bias gradient is the sum of these terms: their norms size the rounding of the
+                # bf16-stored summands (the bound of an analytically zero bias gradient)
+                y.register_hook(lambda g, pid=id(conv.bias): bias_l1.__setitem__(
+                    pid, (float(g.abs().sum()), float(g.double().norm()))))
             if info["relu"]:
                 y = F.relu(y)
         elif kind == "bn":
@@ -276,6 +283,9 @@ def check_segment(rec, k, weights, hip_grads, emu=True, dt=F64):
             N, _, H, W = f.shape
             pc, pb = info["psi_conv"], info["psi_bn"]
             psi = F.conv2d(f, pleaf(pc.weight, False), pleaf(pc.bias, False))
+            if psi.requires_grad:  # the psi bias gradient's summands (see the conv branch)
+                psi.register_hook(lambda g, pid=id(pc.bias): bias_l1.__setitem__(
+                    pid, (float(g.abs().sum()), float(g.double().norm()))))
             psi = force(o, psi, info["psi"].to(dt).reshape(N, H, W, 1).permute(0, 3, 1, 2), "attn_psi", False)
             s = F.batch_norm(psi, None, None, pleaf(pb.weight, False), pleaf(pb.bias, False), True, 0.0, pb.eps)
             alpha = force(o, torch.sigmoid(s), info["alpha"].to(dt).reshape(N, H, W, 1).permute(0, 3, 1, 2),
@@ -310,7 +320,7 @@ def check_segment(rec, k, weights, hip_grads, emu=True, dt=F64):
     if outs:
         torch.autograd.backward(outs, grads)
 
-    res = {"params": [], "inputs": [], "fwd": fwd}
+    res = {"params": [], "inputs": [], "fwd": fwd, "bias_l1": bias_l1}
     for p, leaf in params.values():
         ref = leaf.grad if leaf.grad is not None else torch.zeros_like(leaf)
         res["params"].append((p, rel_l2(hip_grads(p), ref), ref.detach()))

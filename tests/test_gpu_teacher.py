@@ -12,7 +12,7 @@ teacher_tap.py), so no error is amplified across blocks.  Held per tensor:
 * every parameter gradient (fp32): relative L2 <= PARAM_REL against the float64 rebuild with bf16
   rounding where the path stores a gradient (``emu``), or <= NOISE_K x the distance between that
   rebuild run in float32 and in float64 where fp32 accumulation is ill-conditioned; the analytically
-  zero psi conv bias gradients absolutely, at <= ZERO_K x that rebuild's absolute deviation;
+  zero psi conv bias gradients absolutely, at <= ZERO_U x the L2 norm of their summands;
 * every block input's gradient contribution (bf16-stored): relative L2 <= INPUT_REL;
 * every op's forward output against float64 on the stored inputs: relative L2 <= FWD_REL (bf16
   rounding of the stored output is ~1.1e-3 rms);
@@ -44,9 +44,16 @@ PARAM_REL = 1e-3
 NOISE_K = 3.0
 #: conv biases in front of a train-mode BN (the attention gates' psi conv, model/unet_attention.py:24-25):
 #: the exact gradient is 0 (BN removes the mean), so a relative bound is vacuous (the float64 value is
-#: ~1e-17).  Held absolutely: |hip - float64| <= ZERO_K x |float32 rebuild - float64|, the size of one
-#: fp32 accumulation of the same summands (round 4: <= 0.95x).
-ZERO_K = 4.0
+#: ~1e-17).  Held absolutely: |hip - float64| <= ZERO_U x ||d loss / d psi||_2, the L2 norm of the
+#: gradient's summands (the psi path is fp32: the BN backward's per-pixel terms carry fp32 cancellation
+#: noise, summed over N/8 - N pixels).  Measured (round 5, C4): |hip - float64| / ||terms||_2 <= 2.8e-6
+#: (~47 fp32 units); ZERO_U = 2^-12 leaves ~90x, while a 1 % error of the summands -- random signs:
+#: 1e-2 x ||terms||_2, one sign: up to 1e-2 x ||terms||_1 (200-500x the L2 norm here) -- lands 40x to
+#: 10^4x above it.  The L1 / L2 norms and the ratio are in the report (`zero_abs`).  (Round 4 and early
+#: round 5 held it at <= 4x the float32 rebuild's absolute deviation: not a bound on anything the HIP
+#: path does differently -- it failed after an fp64 reduction-order change in the BN finalize, with
+#: that deviation exactly 0 in one block.)
+ZERO_U = 2.0 ** -12
 ZERO_GRAD = ("attn.psi.0.bias",)
 INPUT_REL = 1e-2
 FWD_REL = 5e-3
@@ -185,6 +192,7 @@ def _run(tag):
     bad = []
     t1 = time.time()
     refs = {}
+    zabs = {}  # segment -> {ZERO_GRAD parameter: (|hip - float64|, (L1, L2) of its summands)}
     for mode, emu, dt in (("emu", True, torch.float64), ("emu32", True, torch.float32), ("f64", False, torch.float64)):
         for k, sname in rec.segments():
             with _torch_exact():
@@ -195,6 +203,11 @@ def _run(tag):
                 for p, _, ref in r["params"]:
                     seg["emu"]["noise"][names[id(p)]] = rel_l2(ref, refs[id(p)])
                 continue
+            if emu:
+                for p, _, ref in r["params"]:
+                    if names[id(p)].endswith(ZERO_GRAD):
+                        zabs.setdefault(sname, {})[names[id(p)]] = (
+                            float((hip_grad(p).double() - ref.double()).norm()), r["bias_l1"].get(id(p)))
             pr = sorted(((rel, names[id(p)]) for p, rel, _ in r["params"]), reverse=True)
             ir = [rel for _, rel in r["inputs"]]
             fr = sorted(((rel, kind) for kind, rel in r["fwd"]), reverse=True)
@@ -214,10 +227,14 @@ def _run(tag):
         e["zero_abs"] = {}
         for n, rel in e["params"].items():
             if n.endswith(ZERO_GRAD):
-                # analytically zero: the absolute error against the fp32 rebuild's absolute deviation
-                # (both relative to the same float64 norm, so the ratio of the two rels is that of the absolutes)
-                allow = ZERO_K * e["noise"][n]
-                e["zero_abs"][n] = {"ratio": rel / max(e["noise"][n], 1e-300), "allow_ratio": ZERO_K}
+                # analytically zero: the absolute error against the bf16 rounding of its summands
+                err, norms = zabs[sname][n]
+                l1, l2 = norms if norms else (None, None)
+                e["zero_abs"][n] = {"abs_err": err, "summands_l1": l1, "summands_l2": l2,
+                                    "allow": ZERO_U * l2 if l2 else None, "ratio": err / (ZERO_U * l2) if l2 else None}
+                if l2 is None or not err <= ZERO_U * l2:
+                    bad.append((sname, n, err, ZERO_U * l2 if l2 else None))
+                continue
             else:
                 allow = max(PARAM_REL, NOISE_K * e["noise"][n])
                 if rel > PARAM_REL:
