@@ -149,6 +149,12 @@ size_t unetseg_conv2d_wgrad_workspace(int dtype, int n, int p, int q, int cout, 
 int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h,
                          int w, const void* dy, int ldy, int cout, int r, int s, int stride, int pad, float* ws,
                          size_t ws_bytes, float* dw, int dw_c, int accumulate, void* stream);
+/* the same for one source with dw holding only the first dw_rows (<= cout) GEMM rows: a padded-K conv
+   (the attention gates' theta / phi, model/unet_attention.py:12-19: cout = the 64-padded output
+   channels, whose dY columns are zero) accumulates straight into its real [dw_rows][dw_c][r][s] gradient */
+int unetseg_conv2d_wgrad_rows(int dtype, const void* x1, int c1, int ldc1, int n, int h, int w, const void* dy,
+                              int ldy, int cout, int r, int s, int stride, int pad, float* ws, size_t ws_bytes,
+                              float* dw, int dw_c, int accumulate, int dw_rows, void* stream);
 
 /* ---- ResNet stem on the fast kernels (model/resnet_backbone.py:126-131, conv 7x7/s2/p3) -------
    xp: width-padded bf16 [n][h][w+8][8] from unetseg_pack_input_stem (image column at +3);

@@ -481,13 +481,14 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 // -- is written through an LDS transpose, so both the slab reads and the dW writes are contiguous.
 template <int SL>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* ws, int splits, int Cout, int cin, int taps,
-                                                           float* dw, int dw_c, int accumulate, int cw) {
+                                                           float* dw, int dw_c, int accumulate, int cw, int rows_out) {
   constexpr int IT = 256 / SL;
   __shared__ float4 red[SL][IT];
   __shared__ float tile[1024];
   const long Ng = (long)taps * cin, slab = (long)Cout * Ng;
   const int nchunk = (dw_c + cw - 1) / cw;
   const int k = blockIdx.x / nchunk, cc0 = (blockIdx.x - k * nchunk) * cw;
+  if (k >= rows_out) return;  // whole block: a padded output channel, not written
   const int q4 = cw >> 2, items = taps * q4;
   const int it = threadIdx.x % IT, sl = threadIdx.x / IT;
   const int tap = it / q4, cl = (it - tap * q4) * 4;
@@ -537,7 +538,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* ws, int 
 // 1x1), a 1/splits share of the traffic.
 template <int SL>
 __global__ __launch_bounds__(256) void wgrad_reduce_split_kernel(const float* ws, int splits, int Cout, int cin,
-                                                                 int taps, float* dw, int dw_c, int accumulate) {
+                                                                 int taps, float* dw, int dw_c, int accumulate,
+                                                                 int rows_out) {
   constexpr int IT = 256 / SL;
   __shared__ float4 red[SL][IT];
   const long Ng = (long)taps * cin, s4 = (long)Cout * Ng / 4;
@@ -573,6 +575,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_split_kernel(const float* ws
   }
   if (q >= s4) return;
   const long k = q * 4 / Ng;
+  if (k >= rows_out) return;  // a padded output channel (after the block's last barrier)
   const int col = (int)(q * 4 - k * Ng);
   const int tap = col / cin, c0 = col - tap * cin;
   if (taps == 1 && c0 + 4 <= dw_c && dw_c % 4 == 0) {
@@ -595,15 +598,18 @@ __global__ __launch_bounds__(256) void wgrad_reduce_split_kernel(const float* ws
 
 // Few slabs of a multi-tap filter: the transposing kernel (coalesced dW runs, one lane group per
 // block); otherwise the split-parallel kernel with ~4 (up to splits / 16) slabs per lane.
+// rows_out (<= cout; -1 = cout): dW rows written -- the rest are the zero-padded output channels of a
+// padded-K GEMM (unetseg_conv2d_wgrad_rows), summed in the slabs but never stored
 static void launch_wgrad_reduce(const float* ws, int splits, int cout, int cin, int taps, float* dw, int dw_c,
-                                int accumulate, hipStream_t st) {
+                                int accumulate, hipStream_t st, int rows_out = -1) {
+  if (rows_out < 0 || rows_out > cout) rows_out = cout;
   if (taps > 1 && splits <= 8 && taps <= 256) {
     int cw = 4 * (256 / taps);
     if (cw > 1024 / taps / 4 * 4) cw = 1024 / taps / 4 * 4;  // LDS transpose tile
     if (cw > 64) cw = 64;
     if (cw > ceil_div(dw_c, 4) * 4) cw = ceil_div(dw_c, 4) * 4;
     hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(cout * ceil_div(dw_c, cw)), dim3(256), 0, st, ws, splits, cout,
-                       cin, taps, dw, dw_c, accumulate, cw);
+                       cin, taps, dw, dw_c, accumulate, cw, rows_out);
     return;
   }
   int sl = 1;  // at most 16 lanes: 16-item (256-B) runs per slab read, a short LDS combine
@@ -611,9 +617,9 @@ static void launch_wgrad_reduce(const float* ws, int splits, int cout, int cin, 
   const long s4 = (long)cout * taps * cin / 4;
   const unsigned blocks = (unsigned)((s4 + 256 / sl - 1) / (256 / sl));
   switch (sl) {
-    case 16: hipLaunchKernelGGL(wgrad_reduce_split_kernel<16>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c, accumulate); break;
-    case 4: hipLaunchKernelGGL(wgrad_reduce_split_kernel<4>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c, accumulate); break;
-    default: hipLaunchKernelGGL(wgrad_reduce_split_kernel<1>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c, accumulate); break;
+    case 16: hipLaunchKernelGGL(wgrad_reduce_split_kernel<16>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c, accumulate, rows_out); break;
+    case 4: hipLaunchKernelGGL(wgrad_reduce_split_kernel<4>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c, accumulate, rows_out); break;
+    default: hipLaunchKernelGGL(wgrad_reduce_split_kernel<1>, dim3(blocks), dim3(256), 0, st, ws, splits, cout, cin, taps, dw, dw_c, accumulate, rows_out); break;
   }
 }
 
@@ -1319,10 +1325,33 @@ UNETSEG_API size_t unetseg_conv2d_wgrad_workspace(int dtype, int n, int p, int q
 // dw: fp32 [cout][dw_c][r][s] (PyTorch layout; dw_c <= c1+c2 drops zero-padded input channels),
 // written or accumulated.  ws: fp32 workspace of
 // unetseg_conv2d_wgrad_workspace() bytes.
+static int conv2d_wgrad_impl(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h,
+                             int w, const void* dy, int ldy, int cout, int r, int s, int stride, int pad, float* ws,
+                             size_t ws_bytes, float* dw, int dw_c, int accumulate, int dw_rows, void* stream);
+
 UNETSEG_API int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2,
                                      int n, int h, int w, const void* dy, int ldy, int cout, int r, int s,
                                      int stride, int pad, float* ws, size_t ws_bytes, float* dw, int dw_c,
                                      int accumulate, void* stream) {
+  return conv2d_wgrad_impl(dtype, x1, c1, ldc1, x2, c2, ldc2, n, h, w, dy, ldy, cout, r, s, stride, pad, ws, ws_bytes,
+                           dw, dw_c, accumulate, cout, stream);
+}
+
+// The same with dW holding only the first dw_rows of the cout GEMM rows: a padded-K conv (cout = the
+// 64-padded output channels, whose padded dY columns are zero) accumulates straight into its
+// dw_rows-row gradient, without a padded fp32 copy and an add pass.
+UNETSEG_API int unetseg_conv2d_wgrad_rows(int dtype, const void* x1, int c1, int ldc1, int n, int h, int w,
+                                          const void* dy, int ldy, int cout, int r, int s, int stride, int pad,
+                                          float* ws, size_t ws_bytes, float* dw, int dw_c, int accumulate, int dw_rows,
+                                          void* stream) {
+  US_CHECK_ARG(dw_rows > 0 && dw_rows <= cout, "conv2d_wgrad_rows: bad dw_rows %d (cout %d)", dw_rows, cout);
+  return conv2d_wgrad_impl(dtype, x1, c1, ldc1, nullptr, 0, 0, n, h, w, dy, ldy, cout, r, s, stride, pad, ws, ws_bytes,
+                           dw, dw_c, accumulate, dw_rows, stream);
+}
+
+static int conv2d_wgrad_impl(int dtype, const void* x1, int c1, int ldc1, const void* x2, int c2, int ldc2, int n, int h,
+                             int w, const void* dy, int ldy, int cout, int r, int s, int stride, int pad, float* ws,
+                             size_t ws_bytes, float* dw, int dw_c, int accumulate, int dw_rows, void* stream) {
   US_CHECK_ARG(x1 && dy && ws && dw, "conv2d_wgrad: null pointer");
   US_CHECK_DTYPE(dtype, "conv2d_wgrad");
   US_CHECK_CONV_GEOM("conv2d_wgrad", n, h, w, r, s, stride, pad);
@@ -1384,7 +1413,7 @@ UNETSEG_API int unetseg_conv2d_wgrad(int dtype, const void* x1, int c1, int ldc1
   US_LAUNCH_CHECK("wgrad");
   }
   US_CHECK_ARG(dw_c > 0 && dw_c <= a.cin, "conv2d_wgrad: bad dw_c");
-  launch_wgrad_reduce(ws, splits, cout, a.cin, r * s, dw, dw_c, accumulate, st);
+  launch_wgrad_reduce(ws, splits, cout, a.cin, r * s, dw, dw_c, accumulate, st, dw_rows);
   US_LAUNCH_CHECK("wgrad_reduce");
   return 0;
 }

@@ -32,6 +32,7 @@ SIGNATURES = {
     "unetseg_conv2d_dgrad": (I, [I, P, I, I, I, I, P, I, I, I, I, I, I, P, I, I, I, I, P]),
     "unetseg_conv2d_wgrad_workspace": (SZ, [I, I, I, I, I, I, I, I]),
     "unetseg_conv2d_wgrad": (I, [I, P, I, I, P, I, I, I, I, I, P, I, I, I, I, I, I, P, SZ, P, I, I, P]),
+    "unetseg_conv2d_wgrad_rows": (I, [I, P, I, I, I, I, I, P, I, I, I, I, I, I, P, SZ, P, I, I, I, P]),
     "unetseg_pack_conv_weight": (I, [I, P, I, I, I, I, I, P, P, P]),
     "unetseg_pack_conv_weights": (I, [I, P, I, L, P]),
     "unetseg_pack_tiles": (I, [I, I, I]),

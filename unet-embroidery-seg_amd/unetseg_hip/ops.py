@@ -568,13 +568,10 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                 ws = workspace(ws_bytes, dev)
                 wst = ctx.stream
             if Kp != K:
-                dwp = torch.empty(Kp, pc.C, dtype=torch.float32, device=dev)
-                if side is not None:
-                    dwp.record_stream(side)
+                # the Kp-row GEMM (dY's padded columns are zero) reduced straight into the K-row gradient
                 with _probe("wgrad", flops, 1, ("wgrad_padk",) + desc, stream=side):
-                    lib.conv2d_wgrad(ctx.dt, P(X1), C1, ldp(X1), 0, 0, 0, N, H, W, P(dY), Kp, Kp, 1, 1, 1, 0, P(ws),
-                                     ws.numel(), P(dwp), pc.C, 0, wst)
-                    lib.add(DT_F32, P(dwp), pc.C, P(pc.conv.weight.grad), pc.C, K, pc.C, wst)
+                    lib.conv2d_wgrad_rows(ctx.dt, P(X1), C1, ldp(X1), N, H, W, P(dY), Kp, Kp, 1, 1, 1, 0, P(ws),
+                                          ws.numel(), P(pc.conv.weight.grad), pc.C, 1, K, wst)
             elif lazy is not None:
                 with _probe("wgrad", flops, 1, ("wgrad_bnrelu_in",) + desc, stream=side):
                     lib.conv2d_wgrad_bnrelu_in(ctx.dt, P(X1), C1, ldp(X1), N, H, W, P(dY), ldp(dY), K, P(lazy.sc),
