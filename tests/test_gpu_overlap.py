@@ -75,3 +75,18 @@ def test_overlap_refuses_grad_scale():
         opt.step(grad_scale=torch.ones(1, device=DEV))
     with pytest.raises(ValueError):
         FusedAdam(m, overlap=True, capturable=True)
+
+
+def test_cu_masked_weight_gradient_stream(monkeypatch):
+    """UNETSEG_SIDE_CUMASK (ops.side_stream -> unetseg_stream_create_cumask): the weight-gradient
+    stream restricted to a quarter of the CUs runs the same kernels in the same order, so the
+    overlapped step is bit-identical to the one on an unmasked side stream."""
+    from unetseg_hip import ops
+
+    a = _run("unet_resnet50", "bf16", 128, 2, True, 8.0, steps=2)
+    monkeypatch.setattr(ops, "SIDE_CUMASK", "11111111")
+    monkeypatch.setattr(ops, "_SIDE", {})
+    b = _run("unet_resnet50", "bf16", 128, 2, True, 8.0, steps=2)
+    assert ops._SIDE and all(isinstance(st, torch.cuda.ExternalStream) for st in ops._SIDE.values())
+    for what, u, v in zip(("params", "exp_avg", "exp_avg_sq", "next forward", "losses"), a[:5], b[:5]):
+        assert torch.equal(u, v), f"{what} differ with the CU-masked side stream"
