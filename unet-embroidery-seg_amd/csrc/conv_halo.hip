@@ -313,12 +313,14 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
         }
       }
     }
-    // the next tile's halo DMA, one instruction every other tap step inside the MFMA loop below
-    // (UNETSEG_HALO3_SPREAD, default): issued all at once here, the eight waves spent their issue
-    // cycles together at the tile start with the MFMA pipes idle (16 x 512^2 fwd 313 -> 302-309 us,
-    // dgrad 311 -> 307-309; -DUNETSEG_HALO3_SPREAD=0 builds the old order)
+    // the next tile's halo DMA, one instruction per tap step at the first HI steps of the MFMA
+    // loop below (UNETSEG_HALO3_SPREAD=2, default): issued all at once here, the eight waves spent
+    // their issue cycles together at the tile start with the MFMA pipes idle (16 x 512^2 fwd
+    // 313 -> 302-309 us, dgrad 311 -> 307-309; -DUNETSEG_HALO3_SPREAD=0 builds the old order).
+    // Mode 1 (every other step from step 1) left the last piece fewer steps to land before the
+    // tile-end wait: mode 2 measured fwd 311 -> 302 us, fwd + statistics 448 -> 433 us
 #ifndef UNETSEG_HALO3_SPREAD
-#define UNETSEG_HALO3_SPREAD 1
+#define UNETSEG_HALO3_SPREAD 2
 #endif
     const bool dma_next = t + 1 < my_tiles;
     unsigned nx_base = 0u, nx_hb = 0u, nx_kill = 0u;
@@ -459,7 +461,9 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
         if (st + 1 < 18) __builtin_amdgcn_sched_group_barrier(0x100, FC + FP, 0);  // DS reads of step st+1
         __builtin_amdgcn_sched_group_barrier(0x008, FC * FP, 0);                    // MFMAs of step st
 #endif
-        if ((st & 1) && (st >> 1) < HI) issue_piece(st >> 1);
+        // UNETSEG_HALO3_SPREAD 1: pieces at steps 1, 3, .. 2 HI - 1; 2: at steps 0 .. HI - 1
+        if (UNETSEG_HALO3_SPREAD == 2 ? st < HI : ((st & 1) && (st >> 1) < HI))
+          issue_piece(UNETSEG_HALO3_SPREAD == 2 ? st : st >> 1);
       }
     }
 
