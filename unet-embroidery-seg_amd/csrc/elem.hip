@@ -1618,8 +1618,9 @@ UNETSEG_API int unetseg_bn_apply_mask(int dtype, const void* y, int ldy, const f
   return 0;
 }
 
-// geometry of the channel-reduction kernels (also used by the host to size partial buffers)
-UNETSEG_API int unetseg_reduce_tiles(int dtype, long M, int C, int* tv_out, int* ppb_out) {
+// pixel-tile geometry of the per-channel kernels: ~target blocks over (pixel tiles x channel
+// groups), at least 2 unrolled groups of rows per thread
+static int tile_geom(int dtype, long M, int C, long target, int* tv_out, int* ppb_out) {
   const int V = dtype == DT_BF16 ? 8 : 4;
   if (C <= 0 || C % V != 0 || M < 0) {  // no 16-B channel vectors: no reduction geometry (host ASan driver)
     unetseg_set_error("reduce_tiles: C=%d must be a positive multiple of %d", C, V);
@@ -1629,11 +1630,7 @@ UNETSEG_API int unetseg_reduce_tiles(int dtype, long M, int C, int* tv_out, int*
   const int tv = pow2_le(cv, 64);
   const int rows = 256 / tv;
   const int groups = cv / tv;
-  // ~2048 blocks over (pixel tiles x channel groups); at least 2 unrolled groups of rows per
-  // thread so the partials stay a few % of the data
-  // UNETSEG_RED_TARGET (tests): another block count, i.e. another summation order of the same partials
-  const char* te = getenv("UNETSEG_RED_TARGET");
-  long target = (te ? atol(te) : 2048) / groups;
+  target /= groups;
   if (target < 64) target = 64;
   long per = (M + rows * target - 1) / (rows * target);
   per = (per + RU - 1) / RU * RU;
@@ -1643,6 +1640,26 @@ UNETSEG_API int unetseg_reduce_tiles(int dtype, long M, int C, int* tv_out, int*
   if (tv_out) *tv_out = tv;
   if (ppb_out) *ppb_out = ppb;
   return ceil_div(M, ppb);
+}
+
+static long env_target(const char* name, long dflt) {
+  const char* te = getenv(name);
+  return te ? atol(te) : dflt;
+}
+
+// geometry of the channel-reduction kernels (also used by the host to size partial buffers).
+// ~1024 blocks: against 2048, the BN-backward reductions at the unet_resnet50 B=16 shapes took
+// 39.0 -> 30.5 us (65536 x 512), 63.5 -> 58.5 (1M x 64 packed mask), the finalize reads half the
+// partials (tools/gpu_elem_geom.sh).  UNETSEG_RED_TARGET (tests): another block count, i.e.
+// another summation order of the same partials
+UNETSEG_API int unetseg_reduce_tiles(int dtype, long M, int C, int* tv_out, int* ppb_out) {
+  return tile_geom(dtype, M, C, env_target("UNETSEG_RED_TARGET", 1024), tv_out, ppb_out);
+}
+
+// the BN-backward apply pass has no partials, so it takes its own block count: ~4096 blocks
+// (262144 x 256: 78.4 -> 72.3 us against 2048; 1024 gave 84.5)
+static int apply_tiles(int dtype, long M, int C, int* tv_out, int* ppb_out) {
+  return tile_geom(dtype, M, C, env_target("UNETSEG_APPLY_TARGET", 4096), tv_out, ppb_out);
 }
 
 UNETSEG_API int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const void* A, int lda, const float* msc,
@@ -1699,7 +1716,7 @@ UNETSEG_API int unetseg_bn_bwd_apply(int dtype, const void* dA, int ldd, const v
                                      void* stream) {
   CHECK_VEC(dtype, C, "bn_bwd_apply");
   int tv, ppb;
-  const int G = unetseg_reduce_tiles(dtype, M, C, &tv, &ppb);
+  const int G = apply_tiles(dtype, M, C, &tv, &ppb);
   const int V = dtype == DT_BF16 ? 8 : 4;
   dim3 grid(G, C / V / tv);
   const int mask = A ? (lda == 0 ? 3 : 1) : (msc ? 2 : 0);
