@@ -186,3 +186,53 @@ def test_bn_mask_bits(M, C, mode):
     assert torch.equal(z0.view(torch.int16), z1.view(torch.int16))
     if mode == 2:
         assert torch.equal(e0.view(torch.int16), e1.view(torch.int16))
+
+
+@pytest.mark.parametrize("M,C,lda0", [(16 * 256 * 256, 64, 1), (16 * 64 * 64, 512, 0), (3 * 15 * 17, 64, 0),
+                                      (4096, 2048, 1), (5 * 7 * 9, 256, 1)])
+def test_bn_bwd_block_counts(M, C, lda0, monkeypatch):
+    """BN backward under other block counts (the reduction's ~1024 and the apply pass's own ~4096,
+    elem.hip unetseg_reduce_tiles / apply_tiles): the apply pass is bit-identical whatever its
+    geometry; the reduction's per-channel totals (model/train.py's BatchNorm2d backward: sum dz,
+    sum dz * xhat) match a float64 reference under every block count"""
+    from unetseg_hip.lib import DT_BF16, lib
+    g = torch.Generator(device=DEV).manual_seed(M + C + lda0)
+    bf = torch.bfloat16
+    y = torch.randn(M, C, generator=g, device=DEV).to(bf)
+    a = torch.relu(torch.randn(M, C, generator=g, device=DEV)).to(bf)
+    dA = torch.randn(M, C, generator=g, device=DEV).to(bf)
+    mean, inv = torch.randn(C, generator=g, device=DEV) * 0.1, torch.rand(C, generator=g, device=DEV) + 0.5
+    if lda0:  # the packed ReLU mask (lda = 0) instead of the activation
+        w = (a.float() > 0).view(M, C // 8, 8).to(torch.int32)
+        src = (w << torch.arange(8, device=DEV, dtype=torch.int32)).sum(-1).to(torch.uint8).view(-1)
+        lda = 0
+    else:
+        src, lda = a, C
+    coef = torch.randn(3, C, generator=g, device=DEV)
+    dz = torch.where(a.double() > 0, dA.double(), torch.zeros((), dtype=torch.float64, device=DEV))
+    xhat = (y.double() - mean.double()) * inv.double()
+    want = torch.stack([dz.sum(0), (dz * xhat).sum(0)])
+    scale = torch.stack([dz.abs().sum(0), (dz * xhat).abs().sum(0)])
+    applies = []
+    for red, app in ((None, None), ("512", "64"), ("4096", "100000"), ("64", "1")):
+        for k, v in (("UNETSEG_RED_TARGET", red), ("UNETSEG_APPLY_TARGET", app)):
+            if v is None:
+                monkeypatch.delenv(k, raising=False)
+            else:
+                monkeypatch.setenv(k, v)
+        Gr = lib.reduce_tiles(DT_BF16, M, C, None, None)
+        part = torch.full((2, C, Gr), float("nan"), device=DEV)
+        lib.bn_bwd_reduce(DT_BF16, dA.data_ptr(), C, src.data_ptr(), lda, 0, 0, y.data_ptr(), C, mean.data_ptr(),
+                          inv.data_ptr(), 0, 0, 0, 0, M, C, part.data_ptr(), Gr, _st())
+        dy1 = torch.full((M, C), float("nan"), dtype=bf, device=DEV)
+        dzo = torch.full((M, C), float("nan"), dtype=bf, device=DEV)
+        lib.bn_bwd_apply(DT_BF16, dA.data_ptr(), C, src.data_ptr(), lda, 0, 0, y.data_ptr(), C, mean.data_ptr(),
+                         inv.data_ptr(), dy1.data_ptr(), C, 0, 0, 0, 0, 0, 0, coef.data_ptr(), dzo.data_ptr(), C, 0,
+                         M, C, _st())
+        torch.cuda.synchronize()
+        got = part.double().sum(2)
+        assert ((got - want).abs() <= 1e-5 * scale + 1e-6).all(), (red, (got - want).abs().max().item())
+        applies.append((dy1.view(torch.int16).clone(), dzo.view(torch.int16).clone()))
+    for d, z in applies[1:]:
+        assert torch.equal(d, applies[0][0]) and torch.equal(z, applies[0][1])
+    assert torch.equal(applies[0][1], dz.to(bf).view(torch.int16))
