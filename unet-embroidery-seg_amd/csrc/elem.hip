@@ -949,7 +949,7 @@ __device__ __forceinline__ void up_taps(int i, int in, int out, int align, int& 
 // block row it feeds with that row's weight: (2R+3)*4 loads per lane instead of R*16 for the
 // per-pixel 2-D gather (+0.4% bench step at R = 4; R = 8 loses occupancy).  Row J+1's taps are
 // loaded before row J's are consumed.  Zero weights are skipped (no 0 * inf).
-template <typename T, int R>
+template <typename T, int R, int PF = 1>
 __device__ __forceinline__ void up_adjoint_rows(const T* dy, int ldy, int r0, int nr, int H, int OH, int OW,
                                                 int align, int cd0, const float (&cw)[kUpK], int c0,
                                                 float (&acc)[R][VE<T>]) {
@@ -978,9 +978,12 @@ __device__ __forceinline__ void up_adjoint_rows(const T* dy, int ldy, int r0, in
   };
   uint4 gc[kUpK];
   gather(J0, gc);
+  // PF 2: rows J+1 and J+2 in flight while row J is consumed
+  uint4 gm[kUpK];
+  if constexpr (PF == 2) gather(J0 + 1, gm);
   for (int J = J0; J <= J1; ++J) {
     uint4 gn[kUpK];
-    gather(J + 1, gn);
+    gather(J + PF, gn);
     const int n = J / OH, oh = J - n * OH;
     float cs[V];
 #pragma unroll
@@ -1002,10 +1005,20 @@ __device__ __forceinline__ void up_adjoint_rows(const T* dy, int ldy, int r0, in
       }
     }
 #pragma unroll
-    for (int kw = 0; kw < kUpK; ++kw) gc[kw] = gn[kw];
+    for (int kw = 0; kw < kUpK; ++kw) {
+      if constexpr (PF == 2) {
+        gc[kw] = gm[kw];
+        gm[kw] = gn[kw];
+      } else {
+        gc[kw] = gn[kw];
+      }
+    }
   }
 }
 
+#ifndef UNETSEG_UPBWD_PF
+#define UNETSEG_UPBWD_PF 2
+#endif
 // gather form of the adjoint: dx[h][w] (+)= sum_{oh,ow} wh(oh,h) ww(ow,w) dy[oh][ow]; row-blocked
 // like the forward (row weights wave-uniform, column weights once per lane)
 template <typename T, int R>
@@ -1021,7 +1034,7 @@ __global__ __launch_bounds__(256) void upsample_bwd_kernel(const T* dy, int ldy,
   up_taps(w, W, OW, align, cd0, cw);
   const int r0 = blockIdx.y * R, nr = min(R, N * H - r0);
   float acc[R][V];
-  up_adjoint_rows<T, R>(dy, ldy, r0, nr, H, OH, OW, align, cd0, cw, c0, acc);
+  up_adjoint_rows<T, R, UNETSEG_UPBWD_PF>(dy, ldy, r0, nr, H, OH, OW, align, cd0, cw, c0, acc);
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     if (i >= nr) break;
