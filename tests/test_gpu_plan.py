@@ -27,7 +27,7 @@ def _need_gpu():
     load()
 
 
-def _setup(name, batch, size, loss_name, seed=11):
+def _setup(name, batch, size, loss_name, seed=11, overlap=True):
     from model.model_factory import create_model
     from unetseg_hip.arena import FusedAdam
     from unetseg_hip.losses import binary_segmentation_loss, multitask_loss
@@ -37,7 +37,7 @@ def _setup(name, batch, size, loss_name, seed=11):
     with contextlib.redirect_stdout(io.StringIO()):
         model = create_model(name, weights="", **kw).to(DEV).train()
     model.compute_dtype = "bf16"
-    opt = FusedAdam(model, lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4, overlap=True, bucket_mb=8.0)
+    opt = FusedAdam(model, lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-4, overlap=overlap, bucket_mb=8.0)
     multitask = name == "multitask_unet"
 
     def step(x, y, c):
@@ -62,12 +62,20 @@ def _state(model, opt, loss):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("name,batch,size,loss_name", [
-    ("unet_resnet50", 2, 256, "lovasz_hinge"),
-    ("multitask_unet", 2, 256, "bce"),
-    ("attention_unet", 2, 128, "lovasz_hinge"),
+@pytest.mark.parametrize("name,batch,size,loss_name,overlap", [
+    ("unet_resnet50", 2, 256, "lovasz_hinge", True),
+    ("multitask_unet", 2, 256, "bce", True),
+    ("attention_unet", 2, 128, "lovasz_hinge", True),
+    # the whole-arena Adam on the compute stream (bench.py --overlap-adam 0): the step count and lr
+    # must advance on every replay
+    ("unet_resnet50", 2, 256, "lovasz_hinge", False),
+    # the timed configurations at their bench sizes (BASELINE C2 / C4 / C5): the 512^2 conv
+    # configurations, the plan's private pool with its stream-ordered reuse across three streams
+    ("unet_resnet50", 16, 512, "lovasz_hinge", True),
+    ("attention_unet", 8, 512, "lovasz_hinge", True),
+    ("multitask_unet", 8, 512, "bce", True),
 ])
-def test_plan_replay_bit_identical(name, batch, size, loss_name):
+def test_plan_replay_bit_identical(name, batch, size, loss_name, overlap):
     from unetseg_hip.plan import StepPlan
     from utils.synthetic import make_batch
 
@@ -80,13 +88,14 @@ def test_plan_replay_bit_identical(name, batch, size, loss_name):
             x, y, c = make_batch(batch, size, seed=1234 + i, with_cls=True)
             data.append((x.to(DEV), y.to(DEV), c.to(DEV)))
         nsteps = 5
-        ma, oa, sa = _setup(name, batch, size, loss_name)
+        ma, oa, sa = _setup(name, batch, size, loss_name, overlap=overlap)
         ref = []
         for i in range(nsteps):
             ref.append(_state(ma, oa, sa(*data[i % 2])))
         torch.cuda.synchronize()
         del ma, oa, sa
-        mb, ob, sb = _setup(name, batch, size, loss_name)
+        torch.cuda.empty_cache()
+        mb, ob, sb = _setup(name, batch, size, loss_name, overlap=overlap)
         got = [_state(mb, ob, sb(*data[0]))]
         # the recording runs on fresh copies of batch 1's tensors (replay rebases onto the real batches)
         rec_in = tuple(t.clone() for t in data[1])

@@ -21,6 +21,11 @@
 #include "conv_fast.h"
 #include "fast_util.h"
 
+// halo3: order of the next tile's halo DMA (see halo3_kernel; 2 = one piece per tap step from step 0)
+#ifndef UNETSEG_HALO3_SPREAD
+#define UNETSEG_HALO3_SPREAD 2
+#endif
+
 namespace {
 
 constexpr int HW_TW = 32;  // output tile width (pixels)
@@ -101,6 +106,9 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
   constexpr int WCH = 9 * 64 * 8;            // 16-B chunks of resident weights
   constexpr int WI = WCH / (64 * NW);        // weight DMA instructions per wave
   static_assert(TH % NW == 0 && WCH % (64 * NW) == 0, "tile shape");
+  // the spread halo DMA issues piece i at tap step i (mode 2) or 2 i + 1 (mode 1) of the 18-step loop:
+  // every piece must land on a step that exists, or the next tile would read a partly loaded halo
+  static_assert(HI <= 18 && (HI <= 9 || UNETSEG_HALO3_SPREAD != 1), "halo pieces exceed the tap steps");
   extern __shared__ __attribute__((aligned(16))) uint4 lds[];
   uint4* wl = lds;                           // [9*64 rows][8 chunks]
   uint4* hl = lds + WCH;                     // [2][HP][8]
@@ -319,9 +327,6 @@ __global__ __launch_bounds__(64 * NW) void halo3_kernel(FastTNArgs a, int tiles_
     // 313 -> 302-309 us, dgrad 311 -> 307-309; -DUNETSEG_HALO3_SPREAD=0 builds the old order).
     // Mode 1 (every other step from step 1) left the last piece fewer steps to land before the
     // tile-end wait: mode 2 measured fwd 311 -> 302 us, fwd + statistics 448 -> 433 us
-#ifndef UNETSEG_HALO3_SPREAD
-#define UNETSEG_HALO3_SPREAD 2
-#endif
     const bool dma_next = t + 1 < my_tiles;
     unsigned nx_base = 0u, nx_hb = 0u, nx_kill = 0u;
     if constexpr (!HS) {

@@ -111,6 +111,14 @@ class FusedAdam(torch.optim.Optimizer):
                 raise ValueError("FusedAdam(overlap=True) cannot take a grad scale (the update ran in backward)")
             py(self._commit_step)  # host state: a step plan advances the count every replay
             return loss
+        # host state (the step count, lr) is read inside a py() action, so a step plan re-reads it and
+        # advances the count on every replay instead of repeating the recording step's update
+        py(self._plain_step, grad_scale)
+        return loss
+
+    def _plain_step(self, grad_scale):
+        """the whole-arena update on the current stream (non-overlapped path)"""
+        m = self.model
         m._prepacked = None  # the weights change below: the next forward packs them
         flat, grad = m._flat, m._flat_grad
         self._state(flat)
@@ -132,7 +140,6 @@ class FusedAdam(torch.optim.Optimizer):
         else:
             lib.adam(P(flat), P(grad), P(self._m), P(self._v), flat.numel(), float(g["lr"]), float(b1), float(b2),
                      float(g["eps"]), float(g["weight_decay"]), self._step, P(grad_scale), st)
-        return loss
 
     def state_dict(self):
         sd = super().state_dict()

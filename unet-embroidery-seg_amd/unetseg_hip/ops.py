@@ -349,6 +349,14 @@ class PackedConv:
         self.dt = None
         self.kld = K
 
+    def padk(self, dt):
+        """the one place that decides whether this conv's gradients run through a 64-padded dY (conv()
+        reads it for out.kpad; the padded data gradient needs wt rows Kld wide): narrow bf16 1x1
+        stride-1 convs.  conv() also requires a single input (no virtual concat)."""
+        K = self.K
+        return (PAD_K and dt == DT_BF16 and self.R == 1 and self.S == 1 and K % 64 != 0 and K % 8 == 0 and
+                self.conv.stride in (1, (1, 1)))
+
     def ensure(self, ctx, need_t):
         """allocate the packed images for ctx's dtype/device (no launch)"""
         K, C, R, S = self.K, self.C, self.R, self.S
@@ -356,8 +364,7 @@ class PackedConv:
             self.wk = ctx.empty(K, R, S, self.cpad)
             self.wt = None
             self.dt = ctx.dt
-            padk = PAD_K and ctx.dt == DT_BF16 and R == 1 and S == 1 and K % 64 != 0 and K % 8 == 0
-            self.kld = -(-K // 64) * 64 if padk else K
+            self.kld = -(-K // 64) * 64 if self.padk(ctx.dt) else K
         if need_t and self.wt is None:
             # [Cpad][R][S][Kld]: the padded input channels' rows (and padded K columns) stay zero (the pack
             # writes C rows x K columns), so a data gradient over all Cpad channels is well defined
@@ -369,6 +376,7 @@ class PackedConv:
         if need_t and self.kld != K:  # the single-conv pack writes K-wide rows: stage, then widen
             tmp = torch.empty((self.cpad, R, S, K), dtype=ctx.tdtype, device=ctx.device)
             lib.pack_conv_weight(ctx.dt, P(self.conv.weight), K, C, R, S, self.cpad, P(self.wk), P(tmp), ctx.stream)
+            self.wt.zero_()  # lib.add accumulates: a re-pack must not add onto the previous image
             lib.add(ctx.dt, P(tmp), K, P(self.wt), self.kld, self.cpad * R * S, K, ctx.stream)
             return
         lib.pack_conv_weight(ctx.dt, P(self.conv.weight), K, C, R, S, self.cpad, P(self.wk),
@@ -505,7 +513,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                                pad, P(b), int(relu), P(y), ldp(y), P(st[0] if st else None), ctx.stream)
     out = Node(y)
     out.head = head
-    if PAD_K and ctx.dt == DT_BF16 and R == 1 and S == 1 and K % 64 != 0 and K % 8 == 0 and x2 is None and stride == 1:
+    if x2 is None and pc.padk(ctx.dt):
         out.kpad = -(-K // 64) * 64
     if mbits is not None:
         out.mbits = mbits
@@ -597,6 +605,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                     lib.conv2d_dgrad(ctx.dt, P(dY), Kp, N, Pq, Qq, P(pc.wt), Kp, C1, 1, 1, 1, 0, P(g), ldp(g), H, W,
                                      acc, ctx.stream)
         elif x2 is None:
+            assert pc.wt is None or pc.kld == K, "a plain data gradient reads K-wide wt rows (PackedConv.kld)"
             if x1.need_grad and not _dgrad_fused(ctx, x1, dY, pc, N, H, W, C1, Pq, Qq, flops, desc, last_grad):
                 g, acc = gbuf(ctx, x1)
                 with _probe("igemm_tn", flops, _dgrad_launches(ctx, ldp(dY), N, Pq, Qq, K, C1, R, S, stride, pad, H, W),
@@ -604,6 +613,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                     lib.conv2d_dgrad(ctx.dt, P(dY), ldp(dY), N, Pq, Qq, P(pc.wt), K, C1, R, S, stride, pad, P(g),
                                      ldp(g), H, W, acc, ctx.stream)
         elif x1.need_grad or x2.need_grad:
+            assert pc.wt is None or pc.kld == K, "a concat data gradient reads K-wide wt rows (PackedConv.kld)"
             g = ctx.empty(N, H, W, cin)
             with _probe("igemm_tn", flops, _dgrad_launches(ctx, ldp(dY), N, Pq, Qq, K, cin, R, S, stride, pad, H, W),
                         ("dgrad",) + desc):

@@ -145,6 +145,7 @@ class StepPlan:
         self.torch_names = []
         self.result = None
         self.thread = None
+        self.stream = None
         self._ranges = [(n, t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()) for n, t in self.inputs.items()]
         self._patched = None
 
@@ -167,6 +168,9 @@ class StepPlan:
         _libmod._WRAP = _wrap
         RECORDING = self
         self.thread = threading.get_ident()
+        # the C-ABI calls keep the recording's stream handles, while the py() actions (DDP, Adam) order
+        # their side streams against torch's current stream at replay time: the two must agree
+        self.stream = torch.cuda.current_stream()
         self.pool = torch.cuda.MemPool()
         try:
             with torch.autograd.set_multithreading_enabled(False), torch.cuda.use_mem_pool(self.pool), _Mode(self):
@@ -204,6 +208,9 @@ class StepPlan:
     # ---- replay -----------------------------------------------------------------------------------
     def replay(self, **inputs):
         """issue the recorded step again; inputs: name -> tensor replacing the recording's input"""
+        if torch.cuda.current_stream() != self.stream:
+            raise RuntimeError("StepPlan.replay: the current stream is not the recording's (the recorded launches "
+                               "would not be ordered against the replayed stream waits)")
         base = {}
         for n, t in inputs.items():
             ref = self.inputs[n]
