@@ -235,8 +235,18 @@ def covered_keys():
     # ReLU-bit data gradients (dgrad_post4): tests/test_gpu_relu_bits.py's shapes
     for N, H, W in RELU_BITS_SHAPES:
         keys.update(introspect.call_configs(("dgrad_post4", N, H, W, 64, 0, 64, 3, 3, 1, 1, 64, 0)))
-    for direction, shape, _ in HALO_CASES.values():
-        keys.update(_key_list(direction, shape))
+    for env in HALO_MODES.values():
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            for direction, shape, _ in HALO_CASES.values():
+                keys.update(_key_list(direction, shape))
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    del os.environ[k]
+                else:
+                    os.environ[k] = v
     for direction, shape, expect in CASES.values():
         if not _gather_ring(expect):
             keys.update(_key_list(direction, shape))
@@ -323,9 +333,26 @@ def _gather_ring(expect):
                                 for k in expect)
 
 
+def _persist_keys(expect):
+    """the keys of a halo-A ring case under the persistent kernel (configurations 24 / 25)"""
+    return [k.replace("ring256x128_halo", "ring256x128_hp").replace("ring256x64_halo", "ring256x64_hp")
+            if k is not None else None for k in expect]
+
+
+#: halo-A ring modes: the one-tile-per-block kernel (UNETSEG_TN_PERSIST=0) and the persistent kernel
+#: (tn_halo_persist_kernel) at a fixed 3 tiles per block -- every case then pipelines across tile
+#: boundaries (the next tile's halo and weight stages in flight through the epilogue), and the last
+#: block of most shapes gets a ragged share
+HALO_MODES = {"plain": {"UNETSEG_TN_PERSIST": "0"}, "persist3": {"UNETSEG_TN_PERSIST_T": "3"}}
+
+
+@pytest.mark.parametrize("mode", list(HALO_MODES))
 @pytest.mark.parametrize("cid", list(HALO_CASES))
-def test_halo_ring_case(cid):
-    _run_case(cid, *HALO_CASES[cid])
+def test_halo_ring_case(cid, mode, monkeypatch):
+    for k, v in HALO_MODES[mode].items():
+        monkeypatch.setenv(k, v)
+    direction, shape, expect = HALO_CASES[cid]
+    _run_case(cid, direction, shape, _persist_keys(expect) if mode == "persist3" else expect)
 
 
 @pytest.mark.parametrize("cid", list(CASES))

@@ -921,6 +921,398 @@ __global__ __launch_bounds__(64 * NWM * NWN, (tn_waves_per_simd<BM, BN, NWM, NWN
 }
 
 // ------------------------------------------------------------------------------------------
+// Persistent halo-A ring (round 6).  The halo-A ring above runs one 256-row tile per block: each
+// tile's prologue (its first chunk's halo + the first weight stages: an exposed HBM / L2 round trip)
+// and its epilogue (the transpose through LDS, one barrier, the 64 KiB write-out) sit outside the
+// MFMA loop, and at one block per CU nothing hides them -- the short-K 3x3 layers (2-4 chunks of 64
+// channels: the decoder's conv2 forwards, the concat data gradients) ran at 34-40 % of the MFMA peak.
+// Here a block runs T consecutive tiles (T * grid >= tiles; the dispatcher still balances whole
+// blocks) as ONE pipeline over (tile, chunk, tap):
+//  * the next chunk's halo -- at a tile's last chunk, the NEXT TILE's first chunk -- goes out in HA
+//    pieces during the current chunk's taps, and the weight ring runs on across the tile boundary
+//    (9 taps per chunk, 3 stages: a tap's weight stage is tap % 3 on every chunk);
+//  * the epilogue is register-direct: each lane stores its fragments (4 output channels of one
+//    pixel, 8 B) with buffer stores straight from the accumulators, so no LDS is needed and the
+//    next tile's first halo + weight stages stay in flight through it; BN statistics / post-op
+//    partials go through a 4 KiB `red` scratch;
+//  * the post-op aux values of a tile (post 1 / 2) are loaded at its epilogue; bias and post-2
+//    coefficients sit in LDS (no compiler-tracked global load in the loop: hipcc would wait vmcnt(0)
+//    for it and drain the DMA pipeline).
+// Every wave issues the same vector-memory operations in the same order (out-of-range lanes and dead
+// steps go through zero-extent descriptors / kOOB offsets), so every wait is a compile-time count:
+// the ops younger than the awaited weight stage (see wait_at).  Requires: 3x3 stride-1 pad-1, output
+// grid == input grid, hc % 8 == 0, wc % 32 == 0 (every tile full), no input prologue.
+template <int BN, int NWN>
+constexpr size_t kPersistLds() {
+  constexpr int HST = kHaloChunks<256, 4, NWN>();
+  return (size_t)2 * HST * 16 + (size_t)3 * BN * 8 * 16 + (size_t)2 * 4 * BN * 4;  // halo x2, weights x3, red
+}
+
+template <int BN, int NWN, int POST, int HA>
+__global__ __launch_bounds__(512, 2) void tn_halo_persist_kernel(FastTNArgs a, int T, int ntiles, unsigned y_bytes) {
+  constexpr int BM = 256, NWM = 4, NT = 512, NS = 3;
+  constexpr int WTN = BN / NWN, FP = 4, FC = WTN / 16;
+  constexpr int RSTEP = NT / 8;
+  constexpr int B_PER = BN / RSTEP;
+  static_assert(B_PER == 1 || B_PER == 2, "weight rows per thread");
+  constexpr int HST = kHaloChunks<BM, NWM, NWN>();
+  constexpr int HI = HST / NT;
+  constexpr int HPIX = 10 * 34;
+  constexpr int WST = BN * 8;
+  constexpr int WP = B_PER;                 // weight DMA instructions per wave per step
+  constexpr int HPC = HI / HA, TPER = 9 / HA;
+  static_assert(HI % (2 * HA) == 0 && 9 % HA == 0, "halo pieces of whole instruction pairs");
+  // per-wave vector-memory operations outside the DMA stream: the epilogue's stores
+  constexpr int NST = FC * FP;              // output stores
+  static_assert(WP + 2 * HPC + NST + 2 <= 63, "vmcnt range");
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / NWN, wn = wid % NWN;
+  const int kv = tid & 7, rb = tid >> 3;
+  const int kg = lane >> 4, j16 = lane & 15;
+  const int gy = (a.Ng + BN - 1) / BN;
+  const int tpr = a.wc >> 5;
+  const int nch = a.cin >> 6;
+
+  // LDS: [halo stage 0][halo stage 1][weight stages 0..2][red 2 x NWM x BN floats][bias | post coeffs]
+  const unsigned hbase = lds_addr(lds);
+  const unsigned wbase = hbase + 2u * HST * 16u;
+  float* red = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + 2 * HST * 16 + 3 * WST * 16);
+  float* xco = red + 2 * NWM * BN;  // bias [Ng] (fwd) or sc / sh / mean / inv [4][Ng] (post 2)
+  const bool has_bias = a.bias != nullptr;
+  if (has_bias)
+    for (int c = tid; c < a.Ng; c += NT) xco[c] = a.bias[c];
+  if (POST && a.post == 2)
+    for (int c = tid; c < a.Ng; c += NT) {
+      xco[c] = a.psc[c];
+      xco[a.Ng + c] = a.psh[c];
+      xco[2 * a.Ng + c] = a.pmean[c];
+      xco[3 * a.Ng + c] = a.pinv[c];
+    }
+  __syncthreads();
+
+  // this block's tiles: XCD-contiguous block order (dispatch id d runs on XCD d % 8), T tiles each,
+  // output-channel tiles fastest
+  const int nbk = gridDim.x, b = blockIdx.x;
+  const int xq = nbk >> 3, xr = nbk & 7, xcd = b & 7;
+  const int lb = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (b >> 3);
+  const int tfirst = lb * T;
+  const int tcount = max(0, min(T, ntiles - tfirst));
+
+  const unsigned pb1 = a.x1_bytes / (unsigned)a.ldc1b;
+  const unsigned pb2 = a.x2 ? a.x2_bytes / (unsigned)a.ldc2b : 0u;
+  const unsigned pbad = (pb1 > pb2 ? pb1 : pb2) + 1u;
+  // halo slot i of this lane is halo pixel hp = (i * 8 + wid) * 8 + lane / 8, chunk lane % 8: the LDS
+  // slot (hp, lane & 7) holds source chunk (lane & 7) ^ (hp & 7), and hp & 7 = (lane >> 3) & 7 for every i
+  const unsigned hsw = (unsigned)(((lane & 7) ^ ((lane >> 3) & 7)) * 16);
+  const int kvs16 = (kv ^ ((rb >> 1) & 7)) * 16;
+  // a tile: (row tile, first output channel, image, first row, first column), all wave-uniform
+  struct Tile {
+    int tm, n0, nb, h0, w0;
+  };
+  auto tile_of = [&](int j) -> Tile {
+    const int tl = tfirst + j;
+    Tile t;
+    t.tm = tl / gy;
+    t.n0 = (tl - t.tm * gy) * BN;
+    const int rest = t.tm / tpr, twi = t.tm - rest * tpr;
+    const int hg = rest * 8;
+    t.nb = hg / a.hc;
+    t.h0 = hg - t.nb * a.hc;
+    t.w0 = twi * 32;
+    return t;
+  };
+  // source pixel of halo slot i of tile t (pbad: outside the image or past the halo) -- computed at
+  // issue time instead of held in registers
+  auto halo_pix = [&](const Tile& t, int i) -> unsigned {
+    const int hp = (i * (NWM * NWN) + wid) * 8 + (lane >> 3);
+    const int hr = hp / 34, hc = hp - hr * 34;
+    const int h = t.h0 - 1 + hr, w = t.w0 - 1 + hc;
+    const bool ok = hp < HPIX && h >= 0 && h < a.H && w >= 0 && w < a.W;
+    return ok ? (unsigned)((t.nb * a.H + h) * a.W + w) : pbad;
+  };
+  auto wrow = [&](const Tile& t, int i) -> unsigned {
+    const int n = t.n0 + rb + RSTEP * i;
+    return n < a.Ng ? (unsigned)n * (unsigned)a.ldwb + kvs16 : kOOB;
+  };
+  unsigned tw[9];  // weight byte offset of each tap
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int jr = t / 3, js = t - jr * 3;
+    tw[t] = (unsigned)(((a.r0 + a.rs * jr) * a.S + (a.s0 + a.ss * js)) * a.cin) * 2u;
+  }
+  int hq[FP];
+#pragma unroll
+  for (int p = 0; p < FP; ++p) hq[p] = (wm * 2 + (p >> 1) + 1) * 34 + (p & 1) * 16 + j16 + 1;
+  const int chA = kg;
+  unsigned foffW[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int r = j16;
+    foffW[kk] = (unsigned)((wn * WTN + r) * 128 + ((kk * 4 + kg) ^ ((r >> 1) & 7)) * 16);
+  }
+  // halo pieces [i0, i1) of chunk cc of the tile whose halo pixels are v, into halo stage hs
+  auto issue_halo = [&](const Tile& tt, bool live, int cc, int hs, int i0, int i1) {
+    const int c64 = cc * 64;
+    const bool first = c64 < a.c1;
+    const __amdgpu_buffer_rsrc_t rx = srd_u(first ? a.x1 : a.x2, !live ? 0u : first ? a.x1_bytes : a.x2_bytes);
+    const unsigned ldcb = first ? (unsigned)a.ldc1b : (unsigned)a.ldc2b;
+    const unsigned soff = __builtin_amdgcn_readfirstlane(live ? (unsigned)(first ? c64 : c64 - a.c1) * 2u : 0u);
+    const unsigned sb = __builtin_amdgcn_readfirstlane(hbase + (unsigned)(hs * HST * 16) + (unsigned)(wid * 1024));
+#pragma unroll
+    for (int i = i0; i < i1; i += 2)
+      dma16x2<NT * 16>(rx, sb + (unsigned)(i * NT * 16), __umul24(halo_pix(tt, i), ldcb) + hsw,
+                       __umul24(halo_pix(tt, i + 1), ldcb) + hsw, soff);
+  };
+  auto issue_w = [&](const Tile& tt, bool live, int cc, int t, int stage) {
+    const __amdgpu_buffer_rsrc_t rwx = srd_u(a.wt, live ? a.w_bytes : 0u);
+    const unsigned wsoff = __builtin_amdgcn_readfirstlane(live ? tw[t] + (unsigned)(cc * 64) * 2u : 0u);
+    const unsigned sb = __builtin_amdgcn_readfirstlane(wbase + (unsigned)(stage * WST * 16) + (unsigned)(wid * 8 * 128));
+    if constexpr (B_PER == 1) {
+      dma16s(rwx, sb, wrow(tt, 0), wsoff);
+    } else {
+      dma16x2<RSTEP * 128>(rwx, sb, wrow(tt, 0), wrow(tt, 1), wsoff);
+    }
+  };
+  constexpr auto P_ = [](int t) { return ((((t % 9) + 9) % 9) % TPER == 0) ? HPC : 0; };
+
+  const __amdgpu_buffer_rsrc_t ry = srd(a.y, y_bytes);
+  // post-op aux values (POST) / the statistics or post-op partials [row tiles][2][Ng]
+  const bool do_stats = a.stats != nullptr;
+  const __amdgpu_buffer_rsrc_t raux = srd(POST ? a.aux : a.y, POST ? (unsigned)a.M * (unsigned)a.ld_aux * 2u : 0u);
+  const __amdgpu_buffer_rsrc_t rq = srd(POST ? (const void*)a.ppart : do_stats ? (const void*)a.stats : a.y,
+                                        (POST || do_stats) ? (unsigned)(a.M / BM) * 2u * (unsigned)a.Ng * 4u : 0u);
+  const int E = NST + ((POST || do_stats) ? 2 : 0);  // stores of one epilogue (per wave)
+
+  if (tcount <= 0) return;  // (the grid is sized so this never happens)
+  Tile cur = tile_of(0);
+  // prologue: chunk 0's whole halo, weight steps 0 and 1
+  issue_halo(cur, true, 0, 0, 0, HI);
+  issue_w(cur, true, 0, 0, 0);
+  issue_w(cur, true, 0, 1, 1);
+
+  int gc = 0;  // chunks started by this block (halo stage parity)
+  for (int j = 0; j < tcount; ++j) {
+    const bool has_next = j + 1 < tcount;
+    const Tile nxt = has_next ? tile_of(j + 1) : cur;
+    f32x4 acc[FC][FP];
+#pragma unroll
+    for (int c = 0; c < FC; ++c)
+#pragma unroll
+      for (int p = 0; p < FP; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint2 zr[FC][FP];
+    unsigned opix[FP];
+#pragma unroll
+    for (int p = 0; p < FP; ++p)
+      opix[p] = (unsigned)((cur.nb * a.hc + cur.h0 + wm * 2 + (p >> 1)) * a.wc + cur.w0 + (p & 1) * 16 + j16);
+
+    for (int c = 0; c < nch; ++c, ++gc) {
+      const bool last = c == nch - 1;
+      const bool tstart = c == 0 && j > 0;
+      // the chunk after this one: this tile's c + 1, or the next tile's chunk 0 (dead past the block's tiles)
+      const bool nx_same = !last;
+      const bool nx_live = nx_same || has_next;
+      const int nx_c = nx_same ? c + 1 : 0;
+      const char* hs = reinterpret_cast<const char*>(lds) + (gc & 1) * HST * 16;
+      auto step = [&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        // wait for this step's weight stage (at tap 0 also the chunk's halo, issued before it): the
+        // younger operations of this wave are the next step's weights, the halo pieces of the two
+        // previous steps and, at a tile's first two taps, the previous tile's epilogue stores
+        constexpr int base = WP + P_(t - 1) + P_(t - 2);
+        if constexpr (t <= 1) {
+          if (tstart) {
+            if (E == NST + 2)
+              asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(base + NST + 2) : "memory");
+            else
+              asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(base + NST) : "memory");
+          } else {
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(base) : "memory");
+          }
+        } else {
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(base) : "memory");
+        }
+        const int jr = t / 3, js = t - jr * 3;
+        const int shift = (a.dh0 + a.dhs * jr) * 34 + (a.dw0 + a.dws * js);
+        unsigned ab[FP];
+#pragma unroll
+        for (int p = 0; p < FP; ++p) {
+          const int hp = hq[p] + shift;
+          ab[p] = (unsigned)(hp * 128 + ((chA ^ (hp & 7)) * 16));
+        }
+        const char* ws = reinterpret_cast<const char*>(lds) + 2 * HST * 16 + (t % 3) * WST * 16;
+        bf16x8 pf[FP], wf[FC];
+#pragma unroll
+        for (int p = 0; p < FP; ++p) pf[p] = *reinterpret_cast<const bf16x8*>(hs + ab[p]);
+#pragma unroll
+        for (int cc = 0; cc < FC; ++cc) wf[cc] = *reinterpret_cast<const bf16x8*>(ws + foffW[0] + cc * 2048);
+        // weights of the step two ahead (stage (t + 2) % 3): this chunk's tap t + 2, or the next chunk's
+        if constexpr (t + 2 < 9) {
+          issue_w(cur, true, c, t + 2, (t + 2) % 3);
+        } else {
+          issue_w(nx_same ? cur : nxt, nx_live, nx_c, t + 2 - 9, (t + 2) % 3);
+        }
+        if constexpr (t % TPER == 0) {
+          issue_halo(nx_same ? cur : nxt, nx_live, nx_c, (gc + 1) & 1, (t / TPER) * HPC, (t / TPER + 1) * HPC);
+        }
+#pragma unroll
+        for (int cc = 0; cc < FC; ++cc)
+#pragma unroll
+          for (int p = 0; p < FP; ++p)
+            acc[cc][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cc], pf[p], acc[cc][p], 0, 0, 0);
+#pragma unroll
+        for (int p = 0; p < FP; ++p) pf[p] = *reinterpret_cast<const bf16x8*>(hs + (ab[p] ^ 64u));
+#pragma unroll
+        for (int cc = 0; cc < FC; ++cc) wf[cc] = *reinterpret_cast<const bf16x8*>(ws + foffW[1] + cc * 2048);
+#pragma unroll
+        for (int cc = 0; cc < FC; ++cc)
+#pragma unroll
+          for (int p = 0; p < FP; ++p)
+            acc[cc][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cc], pf[p], acc[cc][p], 0, 0, 0);
+      };
+      step(std::integral_constant<int, 0>{});
+      step(std::integral_constant<int, 1>{});
+      step(std::integral_constant<int, 2>{});
+      step(std::integral_constant<int, 3>{});
+      step(std::integral_constant<int, 4>{});
+      step(std::integral_constant<int, 5>{});
+      step(std::integral_constant<int, 6>{});
+      step(std::integral_constant<int, 7>{});
+      step(std::integral_constant<int, 8>{});
+    }
+
+    // ================= epilogue (register-direct) =================
+    if constexpr (POST) {
+      // the post-op aux values of this tile (untracked loads, then every older operation retired with
+      // them: the next tile's first halo and weight stages were issued during the last chunk and have
+      // mostly landed).  Held across the tap loop instead (issued at its last taps) they cost the
+      // 8-wave kernel its registers: 123 VGPRs spilled.
+#pragma unroll
+      for (int cc = 0; cc < FC; ++cc) {
+        const int nb = cur.n0 + wn * WTN + cc * 16 + kg * 4;
+#pragma unroll
+        for (int p = 0; p < FP; ++p)
+          zr[cc][p] = bload64_asm(raux, nb < a.Ng ? (opix[p] * (unsigned)a.ld_aux + (unsigned)nb) * 2u : kOOB);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int cc = 0; cc < FC; ++cc)
+#pragma unroll
+        for (int p = 0; p < FP; ++p) asm volatile("" : "+v"(zr[cc][p]));
+    }
+    // one 16-channel group at a time (bias / ReLU / rounding, post-op mask, stores, column partials):
+    // the whole-tile form held acc, the aux values, the packed outputs and 32 partials at once and spilled
+#pragma unroll
+    for (int cc = 0; cc < FC; ++cc) {
+      const int nb = cur.n0 + wn * WTN + cc * 16 + kg * 4;
+      const bool nok = nb < a.Ng;
+      float bias4[4], sc4[4], sh4[4], mu4[4], iv4[4], s4[4], m4[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bias4[e] = (has_bias && nok) ? xco[nb + e] : 0.f;
+        const bool bn = POST && a.post == 2 && nok;
+        sc4[e] = bn ? xco[nb + e] : 0.f;
+        sh4[e] = bn ? xco[a.Ng + nb + e] : 0.f;
+        mu4[e] = bn ? xco[2 * a.Ng + nb + e] : 0.f;
+        iv4[e] = bn ? xco[3 * a.Ng + nb + e] : 0.f;
+        s4[e] = m4[e] = 0.f;
+      }
+#pragma unroll
+      for (int p = 0; p < FP; ++p) {
+        bf16 o[4];
+        const bf16* z = reinterpret_cast<const bf16*>(&zr[cc][p]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = acc[cc][p][e] + bias4[e];
+          if (a.relu) v = fmaxf(v, 0.f);
+          v = (float)(bf16)v;  // BN statistics / post-op sums are of the stored (rounded) values
+          if constexpr (POST) {
+            const float zf = (float)z[e];
+            const bool on = a.post == 2 ? fmaf(zf, sc4[e], sh4[e]) > 0.f : zf > 0.f;
+            v = on ? v : 0.f;
+            m4[e] += v * ((zf - mu4[e]) * iv4[e]);
+          }
+          s4[e] += v;
+          acc[cc][p][e] = v;
+          o[e] = (bf16)v;
+        }
+        uint2 ov = *reinterpret_cast<uint2*>(o);
+        if (a.accumulate && nok) {  // dx += dgrad (bf16 + bf16 in fp32); hipcc drains vmcnt here: slower, correct
+          const uint2 old = *reinterpret_cast<const uint2*>((const bf16*)a.y + (long)opix[p] * a.ldy + nb);
+          const bf16* ob = reinterpret_cast<const bf16*>(&old);
+          bf16* nv = reinterpret_cast<bf16*>(&ov);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) nv[e] = (bf16)((float)nv[e] + (float)ob[e]);
+        }
+        // exactly FC * FP output stores per wave (absent channels go out of range)
+        bstore64(ry, nok ? (opix[p] * (unsigned)a.ldy + (unsigned)nb) * 2u : kOOB, ov);
+      }
+      if (POST || do_stats) {
+        // this group's column partials over the wave's 64 pixels -> red[2][NWM][BN]: (sum d, sum d xhat)
+        // for the post-op, (sum, M2 about the wave mean) for the statistics
+        row16_sum_n(s4);
+        if (!POST) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float mean = s4[e] * (1.0f / 64.f);
+            float q = 0.f;
+#pragma unroll
+            for (int p = 0; p < FP; ++p) {
+              const float d = acc[cc][p][e] - mean;
+              q += d * d;
+            }
+            m4[e] = q;
+          }
+        }
+        row16_sum_n(m4);
+        if (j16 == 0)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int col = wn * WTN + cc * 16 + kg * 4 + e;
+            red[wm * BN + col] = s4[e];
+            red[(NWM + wm) * BN + col] = m4[e];
+          }
+      }
+    }
+    if (POST || do_stats) {
+      // the NWM row-waves merged per column (plain sums for the post-op, Chan for the statistics),
+      // stored by buffer stores every wave issues (2 each; lanes without a column go out of range)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      const int col = tid;
+      const int n = cur.n0 + col;
+      const bool ok = col < BN && n < a.Ng;
+      float t0 = 0.f, t1 = 0.f;
+      if (ok) {
+        if constexpr (POST) {
+#pragma unroll
+          for (int w = 0; w < NWM; ++w) {
+            t0 += red[w * BN + col];
+            t1 += red[(NWM + w) * BN + col];
+          }
+        } else {
+#pragma unroll
+          for (int w = 0; w < NWM; ++w) t0 += red[w * BN + col];
+          const float mean = t0 * (1.0f / BM);
+#pragma unroll
+          for (int w = 0; w < NWM; ++w) {
+            const float d = red[w * BN + col] * (1.0f / 64.f) - mean;
+            t1 += red[(NWM + w) * BN + col] + 64.f * d * d;
+          }
+        }
+      }
+      const unsigned so = ok ? (unsigned)(cur.tm * 2 * a.Ng + n) * 4u : kOOB;
+      bstore32(rq, so, t0);
+      bstore32(rq, ok ? so + (unsigned)a.Ng * 4u : kOOB, t1);
+    }
+    cur = nxt;
+  }
+  // the dead DMAs issued during the last chunk land in this block's LDS: drain them before it exits
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ------------------------------------------------------------------------------------------
 // wgrad: C[cout][(tap, c)] = sum_pix dY[pix][cout] * X[n][p*st+dh][q*st+dw][c];
 // tile BM couts x BN (tap,c) columns, K step = kWgBK consecutive output pixels.  Each thread
 // tracks (image, row, col) of the pixels it stages and advances them by one step at a time, so
@@ -1303,6 +1695,73 @@ static bool halo_a_ok(const FastTNArgs& a) {
 
 static int tn_config_base(const FastTNArgs& a);
 
+// Persistent halo-A ring (tn_halo_persist_kernel): tiles per block for a halo-A ring call on BN-wide
+// column tiles, or 0 to keep the one-tile-per-block kernel.  UNETSEG_TN_PERSIST=0 turns it off (read per
+// call, so a test can run both); UNETSEG_TN_PERSIST_ROUNDS = R: T = ceil(tiles / (R x CUs)), i.e. the
+// grid covers the chip about R times (default 1: one resident block per CU runs its whole share);
+// UNETSEG_TN_PERSIST_MIN_T: below this many tiles per block the plain kernel runs (default 2);
+// UNETSEG_TN_PERSIST_T = T forces T (tests).  Reported as configurations 24 / 25 (tn_fast_config).
+static int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+static int persist_t(const FastTNArgs& a, int bn) {
+  const char* e = getenv("UNETSEG_TN_PERSIST");
+  if (e && atoi(e) == 0) return 0;
+  if (a.in_sc || a.post < 0 || a.post > 2 || (a.bias && a.post) || a.t2d < 0) return 0;
+  if (a.ostride != 1 || a.ph || a.pw || a.OH != a.hc || a.OW != a.wc || a.M % 256) return 0;
+  const size_t extra = (a.bias ? (size_t)a.Ng * 4 : 0) + (a.post == 2 ? (size_t)a.Ng * 16 : 0);
+  const size_t lds = (bn == 128 ? kPersistLds<128, 2>() : kPersistLds<64, 2>()) + extra;
+  if (lds > 160 * 1024) return 0;
+  // 32-bit buffer offsets below kOOB
+  if ((unsigned long long)a.M * (unsigned)a.ldy * 2ull >= (unsigned long long)kOOB) return 0;
+  if (a.post && (unsigned long long)a.M * (unsigned)a.ld_aux * 2ull >= (unsigned long long)kOOB) return 0;
+  if (a.stats && (unsigned long long)(a.M / 256) * 2ull * a.Ng * 4ull >= (unsigned long long)kOOB) return 0;
+  const long ntiles = (long)(a.M / 256) * ceil_div(a.Ng, bn);
+  const char* ft = getenv("UNETSEG_TN_PERSIST_T");  // tests: a fixed T (every tile count, ragged last block)
+  if (ft && atoi(ft) > 0) return atoi(ft);
+  const char* r = getenv("UNETSEG_TN_PERSIST_ROUNDS");
+  const int rounds = r && atoi(r) > 0 ? atoi(r) : 1;
+  const char* m = getenv("UNETSEG_TN_PERSIST_MIN_T");
+  const int min_t = m && atoi(m) > 0 ? atoi(m) : 2;
+  const long T = (ntiles + (long)rounds * cu_count() - 1) / ((long)rounds * cu_count());
+  return T >= min_t ? (int)T : 0;
+}
+
+template <int BN, int NWN, int HA>
+static int launch_tn_persist(const FastTNArgs& a, hipStream_t st) {
+  const int T = persist_t(a, BN);
+  const size_t extra = (a.bias ? (size_t)a.Ng * 4 : 0) + (a.post == 2 ? (size_t)a.Ng * 16 : 0);
+  const size_t lds = kPersistLds<BN, NWN>() + extra;
+  const int ntiles = (a.M / 256) * ceil_div(a.Ng, BN);
+  const int grid = ceil_div(ntiles, T);
+  const unsigned y_bytes = (unsigned)((unsigned long long)a.M * (unsigned)a.ldy * 2ull);
+  if (a.post) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_halo_persist_kernel<BN, NWN, 1, HA>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL((tn_halo_persist_kernel<BN, NWN, 1, HA>), dim3(grid), dim3(512), lds, st, a, T, ntiles, y_bytes);
+  } else {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tn_halo_persist_kernel<BN, NWN, 0, HA>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL((tn_halo_persist_kernel<BN, NWN, 0, HA>), dim3(grid), dim3(512), lds, st, a, T, ntiles, y_bytes);
+  }
+  return 0;
+}
+
 static int tn_config(const FastTNArgs& a) {
   if (a.force_cfg) return a.force_cfg;
   const int c = tn_config_base(a);
@@ -1371,6 +1830,10 @@ int tn_fast_post_rows(const FastTNArgs& a) {
 
 int tn_fast_config(const FastTNArgs& a, int* taps_out) {
   const int cfg = tn_config(a);
+  if ((cfg == 21 || cfg == 22) && !a.in_sc && a.post != 3 && a.post != 4 && persist_t(a, cfg == 21 ? 128 : 64) > 0) {
+    if (taps_out) *taps_out = 0;
+    return cfg + 3;  // 24 / 25: the persistent halo-A ring (tn_halo_persist_kernel)
+  }
   if (taps_out) *taps_out = (cfg >= 7 && cfg <= 14) ? tn_taps(a) : 0;
   return cfg;
 }
@@ -1429,6 +1892,7 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
     case 19: return a.post ? launch_tn_cfg<128, 128, 2, 2, 5, true>(a, st) : launch_tn_cfg<128, 128, 2, 2, 5>(a, st);
     case 20: return a.post ? launch_tn_cfg<128, 64, 2, 2, 5, true>(a, st) : launch_tn_cfg<128, 64, 2, 2, 5>(a, st);
     case 21: {
+      if (persist_t(a, 128) > 0) return launch_tn_persist<128, 2, 3>(a, st);
       // weight ring depth: 3 stages (144 KiB of LDS with the two halo stages); 4 fill all 160 KiB
       static const bool ns4 = getenv("UNETSEG_TN_HALO_NS4") != nullptr;
       // the next chunk's halo DMA in three pieces at taps 0, 3, 6 (A/B +0.3 %; UNETSEG_TN_HALO_SPLIT=1:
@@ -1442,7 +1906,9 @@ int launch_tn_fast(const FastTNArgs& a, hipStream_t st) {
                     : launch_tn_cfg<256, 128, 4, 2, 13, false, 9, false, 1>(a, st);
     }
     // 64 output channels or fewer: 256x64 (eight waves of 64x32), one weight row per wave and step
-    case 22: return a.post ? launch_tn_cfg<256, 64, 4, 2, 13, true, 9, false, 1>(a, st)
+    case 22:
+      if (persist_t(a, 64) > 0) return launch_tn_persist<64, 2, 1>(a, st);
+      return a.post ? launch_tn_cfg<256, 64, 4, 2, 13, true, 9, false, 1>(a, st)
                            : launch_tn_cfg<256, 64, 4, 2, 13, false, 9, false, 1>(a, st);
     // in place of the 5-stage 128x128 gather ring (one or two tiles per CU): 4 x 32 spatial tiles,
     // four waves, the weights on a 5-stage ring

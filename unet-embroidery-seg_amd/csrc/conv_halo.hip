@@ -34,9 +34,6 @@ constexpr int HW_TW = 32;  // output tile width (pixels)
 // with hp & 7 (not (hp>>1) & 7 as for aligned rows): conflict-free ds_read_b128 for every start.
 __device__ __forceinline__ int swzh(int hp, int ch) { return ch ^ (hp & 7); }
 
-__device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, unsigned off, uint2 v) {
-  asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
-}
 
 // EPI: epilogue flags fixed at compile time (kEpiBias | kEpiRelu | kEpiStats | kEpiAcc), or kEpiDyn
 // to read them from the arguments; with them fixed the tile epilogue has no uniform branches and
@@ -49,16 +46,6 @@ __device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, unsigned off,
 constexpr int kEpiBias = 1, kEpiRelu = 2, kEpiStats = 4, kEpiAcc = 8, kEpiDyn = 16, kEpiHead1 = 32, kEpiHead2 = 64,
               kEpiMask = 128;
 
-// an 8-B buffer load the compiler does not track: the caller waits for it with an explicit vmcnt (so the
-// wait can leave later LDS-DMAs in flight) and then ties the value with asm volatile("" : "+v"(v))
-__device__ __forceinline__ uint2 bload64_asm(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  uint2 v;
-  asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
-  return v;
-}
-__device__ __forceinline__ void bstore32(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
-  asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
-}
 
 // wait for half h of the HS pipeline and join the block: the vector-memory operations issued after
 // half h's DMA may stay in flight -- the next two halves (D instructions each) and the aux loads (NA)

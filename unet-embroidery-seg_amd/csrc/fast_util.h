@@ -35,12 +35,16 @@ __device__ __forceinline__ unsigned bnrelu_pair(unsigned v, f32x2 sc, f32x2 sh) 
 // LDS-DMA of 16 B per lane (64 lanes -> 1 KiB contiguous at lds_byte): issued in inline asm so
 // hipcc neither tracks it (no conservative vmcnt(0) before every ds_read) nor reuses M0 (saved and
 // restored inside the statement).  Completion is counted by the caller's explicit vmcnt.
+// Every vector-memory instruction in these statements is preceded by s_nop 4 (with the s_movs: >= 5
+// wait states): its descriptor / soffset SGPRs may have just been written by a VALU (readfirstlane in
+// srd_u, or v_readlane restoring a spilled SGPR), and hipcc pads no hazard inside an asm string -- the
+// persistent halo ring's partial stores went through a stale descriptor until this was added.
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned lds_byte, unsigned voff) {
   unsigned keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
+      "s_nop 4\n\t"
       "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
@@ -64,7 +68,7 @@ __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, unsigned lds_by
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
+      "s_nop 4\n\t"
       "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
@@ -79,7 +83,7 @@ __device__ __forceinline__ void dma16x2(__amdgpu_buffer_rsrc_t r, unsigned lds_b
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
+      "s_nop 4\n\t"
       "buffer_load_dwordx4 %3, %5, %6 offen lds\n\t"
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
@@ -88,6 +92,20 @@ __device__ __forceinline__ void dma16x2(__amdgpu_buffer_rsrc_t r, unsigned lds_b
       : "=&s"(keep)
       : "s"(lds_byte), "s"(lds_byte + STRIDE), "v"(v0), "v"(v1), "s"(r), "s"(soff)
       : "memory");
+}
+// buffer stores / an untracked load (inline asm: hipcc does not count them, the caller's explicit vmcnt does)
+__device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, unsigned off, uint2 v) {
+  asm volatile("s_nop 4\n\tbuffer_store_dwordx2 %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
+}
+// an 8-B buffer load the compiler does not track: the caller waits for it with an explicit vmcnt (so the
+// wait can leave later LDS-DMAs in flight) and then ties the value with asm volatile("" : "+v"(v))
+__device__ __forceinline__ uint2 bload64_asm(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  uint2 v;
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
+  return v;
+}
+__device__ __forceinline__ void bstore32(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
+  asm volatile("s_nop 4\n\tbuffer_store_dword %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
 }
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;

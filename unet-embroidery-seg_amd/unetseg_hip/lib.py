@@ -239,7 +239,7 @@ CFG_NAMES = {0: "halo3", 1: "tn256x64", 2: "tn256x128", 3: "tn128x128", 4: "tn12
              6: "tn128x64", 7: "ring256x128", 8: "ring128x128", 9: "ring64x128", 10: "ring128x128_5st",
              11: "ring256x64", 12: "ring128x64_4st", 13: "ring128x64", 14: "ring256x64_8w", 17: "multi128x128",
              18: "multi64x128", 19: "tn128x128_1st", 20: "tn128x64_1st", 21: "ring256x128_halo", 22: "ring256x64_halo",
-             23: "ring128x128_halo", 30: "stem_halo", 31: "first3x3", 100: "generic"}
+             23: "ring128x128_halo", 24: "ring256x128_hp", 25: "ring256x64_hp", 30: "stem_halo", 31: "first3x3", 100: "generic"}
 WG_NAMES = {0: "halo3_wgrad", 1: "wgrad64x256_row", 2: "wgrad128_row", 3: "wgrad64x256", 4: "wgrad128",
             5: "wgrad_generic", 6: "wgrad_ring64x256", 7: "wgrad_ring128"}
 
