@@ -105,9 +105,11 @@ def test_model_head_fusion_unchanged(name):
         assert (a - b).norm().item() <= 1e-2 * a.norm().item() + 1e-8
 
 
+# heights that are multiples of 8 run the row-streaming kernel (16 rows per block at 16 x 256^2 x 64, else 8;
+# half-pixel and align_corners weights), the others the row-blocked one
 @pytest.mark.parametrize("N,H,W,C,align", [(16, 256, 256, 64, 1), (16, 128, 128, 128, 1), (16, 32, 32, 512, 1),
                                            (2, 24, 40, 64, 0), (3, 5, 7, 256, 1), (4, 7, 9, 64, 1), (2, 9, 33, 128, 0),
-                                           (5, 3, 2, 64, 1), (8, 64, 64, 256, 1)])
+                                           (5, 3, 2, 64, 1), (8, 64, 64, 256, 1), (3, 16, 72, 64, 0), (2, 8, 8, 512, 1)])
 def test_upsample_bwd_relu(N, H, W, C, align):
     from unetseg_hip.lib import DT_BF16, lib
     g = torch.Generator(device=DEV).manual_seed(N * 7 + H + C)

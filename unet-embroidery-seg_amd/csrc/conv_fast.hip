@@ -1723,6 +1723,9 @@ static int persist_t(const FastTNArgs& a, int bn) {
   if ((unsigned long long)a.M * (unsigned)a.ldy * 2ull >= (unsigned long long)kOOB) return 0;
   if (a.post && (unsigned long long)a.M * (unsigned)a.ld_aux * 2ull >= (unsigned long long)kOOB) return 0;
   if (a.stats && (unsigned long long)(a.M / 256) * 2ull * a.Ng * 4ull >= (unsigned long long)kOOB) return 0;
+  // tiles of fewer 64-channel chunks than this keep the one-tile kernel (UNETSEG_TN_PERSIST_MIN_NCH)
+  const char* mc = getenv("UNETSEG_TN_PERSIST_MIN_NCH");
+  if (mc && (a.cin >> 6) < atoi(mc)) return 0;
   const long ntiles = (long)(a.M / 256) * ceil_div(a.Ng, bn);
   const char* ft = getenv("UNETSEG_TN_PERSIST_T");  // tests: a fixed T (every tile count, ragged last block)
   if (ft && atoi(ft) > 0) return atoi(ft);

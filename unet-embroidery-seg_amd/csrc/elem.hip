@@ -12,6 +12,8 @@
 // Layout: activations NHWC with an explicit pixel stride ("ld", elements) so channel slices of a
 // concat buffer are addressed in place.  Element type T is bf16 or fp32; all arithmetic is fp32.
 // Every per-channel reduction is two-stage (per-block partials -> finalize) and deterministic.
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -1106,6 +1108,149 @@ __global__ __launch_bounds__(256) void upsample_bwd_relu_kernel(const T* dy, int
   }
 }
 
+// Row-streaming form of upsample_bwd_relu (round 6): a block owns RS input rows of one image (RS | H)
+// and walks the dy rows feeding them ONCE, top to bottom, keeping only the two input rows the current
+// dy row touches (every dy row oh feeds rows i0 = floor(src) and i1 = i0 + 1, and i0 never decreases):
+// a row is finished -- masked, stored, summed -- as soon as the walk passes it.  Against the R = 4
+// row-blocked kernel above: (2 RS + 2) dy rows gathered per RS rows instead of (2 R + 3) per R
+// (1.06x instead of 1.4x of dy re-read), K = 4 column taps where no column has a fifth (the U-Net
+// sizes: up_taps_max), two rows in flight in 3 x K registers of 16 B, and the 32 accumulators of the
+// R = 4 form down to 16.  Arithmetic identical to upsample_bwd (same up_taps / up_w weights, same
+// per-row J order, same expressions): bit-identical dx.  part[g][0][c] as upsample_bwd_relu_kernel
+// (g = blockIdx.y * gridDim.x + blockIdx.x).
+template <typename T, int RS, int K, int PF>
+__global__ __launch_bounds__(256, PF == 1 ? 4 : 3) void upsample_bwd_relu_stream_kernel(const T* dy, int ldy, int N, int H, int W,
+                                                                        int C, int align, const T* A, int lda, T* dx,
+                                                                        int ldx, float* part) {
+  constexpr int V = VE<T>;
+  __shared__ float red[256 * V];
+  const int cv = C / V, OH = 2 * H, OW = 2 * W;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = idx < W * cv;
+  const int w = live ? idx / cv : 0, c0 = live ? (idx - w * cv) * V : 0;
+  float s[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) s[e] = 0.f;
+  if (live) {
+    int cd0;
+    float cw5[kUpK];
+    up_taps(w, W, OW, align, cd0, cw5);
+    float cw[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) cw[k] = cw5[k];  // K = 4: the host checked cw5[4] == 0 for every column
+    const int rb = blockIdx.y * RS;              // first stacked input row (n * H + h0), RS | H
+    const int n = rb / H, h0 = rb - n * H;
+    int lo, hi, t;
+    up_range(h0, H, OH, align, lo, t);
+    up_range(h0 + RS - 1, H, OH, align, t, hi);
+    // dy through a buffer descriptor: per-lane tap offsets are constants (kOOB for a zero tap), the
+    // dy row's offset is scalar -- no 64-bit address per tap and row
+    const __amdgpu_buffer_rsrc_t rdy =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(dy), (short)0, (int)((long)N * OH * OW * ldy * (long)sizeof(T)), 0x00020000);
+    unsigned toff[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) toff[k] = cw[k] != 0.f ? (unsigned)(((cd0 + k) * ldy + c0) * (int)sizeof(T)) : 0x80000000u;
+    auto gather = [&](int oh, uint4 (&g)[K]) {
+      const int ohc = oh <= hi ? oh : hi;  // past the block's last dy row: a re-read, never consumed
+      const int soff = (int)(((long)n * OH + ohc) * OW * ldy * (long)sizeof(T));
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        typedef int i32x4_t __attribute__((ext_vector_type(4)));
+        i32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rdy, (int)toff[k], soff, 0);
+        g[k] = *reinterpret_cast<uint4*>(&v);
+      }
+    };
+    const T* An = A + ((long)n * H * W + w) * lda + c0;
+    T* dxn = dx + ((long)n * H * W + w) * ldx + c0;
+    auto amask = [&](int r) -> uint4 {
+      return (r >= h0 && r < h0 + RS) ? *reinterpret_cast<const uint4*>(An + (long)r * W * lda) : uint4{0u, 0u, 0u, 0u};
+    };
+    // finish input row r (acc = its adjoint): mask, round as stored, partial sums
+    auto finish = [&](int r, const float (&acc)[V], const uint4& am) {
+      if (r < h0 || r >= h0 + RS) return;
+      float a[V];
+      cvt16<T>(am, a);
+      T o[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        o[e] = (T)(a[e] > 0.f ? acc[e] : 0.f);
+        s[e] += (float)o[e];
+      }
+      *reinterpret_cast<uint4*>(dxn + (long)r * W * ldx) = *reinterpret_cast<uint4*>(o);
+    };
+    int i0, i1;
+    float l1;
+    up_src(lo, H, OH, align, i0, i1, l1);
+    int ra = i0;  // rows ra (accA) and ra + 1 (accB)
+    float accA[V], accB[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) accA[e] = accB[e] = 0.f;
+    uint4 mA = amask(ra), mB = amask(ra + 1);
+    // PF dy rows in flight beyond the one being consumed (1 or 2)
+    uint4 gc[K], gm[PF == 2 ? K : 1];
+    gather(lo, gc);
+    if constexpr (PF == 2) gather(lo + 1, gm);
+    for (int oh = lo; oh <= hi; ++oh) {
+      uint4 gn[K];
+      gather(oh + PF, gn);
+      up_src(oh, H, OH, align, i0, i1, l1);
+      if (i0 > ra) {  // row ra has had its last dy row (i0 advances by at most one per dy row)
+        finish(ra, accA, mA);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          accA[e] = accB[e];
+          accB[e] = 0.f;
+        }
+        mA = mB;
+        ++ra;
+        mB = amask(ra + 1);
+      }
+      float cs[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) cs[e] = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (cw[k] != 0.f) {
+          float gv[V];
+          cvt16<T>(gc[k], gv);
+#pragma unroll
+          for (int e = 0; e < V; ++e) cs[e] += cw[k] * gv[e];
+        }
+      // the weights of upsample_bwd (up_w: rows i0 and i1, summed where they coincide)
+      const float wA = up_w(oh, ra, H, OH, align), wB = up_w(oh, ra + 1, H, OH, align);
+      if (wA != 0.f) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) accA[e] += wA * cs[e];
+      }
+      if (wB != 0.f) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) accB[e] += wB * cs[e];
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if constexpr (PF == 2) {
+          gc[k] = gm[k];
+          gm[k] = gn[k];
+        } else {
+          gc[k] = gn[k];
+        }
+      }
+    }
+    finish(ra, accA, mA);
+    finish(ra + 1, accB, mB);
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) red[threadIdx.x * V + e] = s[e];
+  __syncthreads();
+  const long g = (long)blockIdx.y * gridDim.x + blockIdx.x;
+  for (int i = threadIdx.x; i < cv * V; i += 256) {
+    const int cx = i / V, e = i - cx * V;
+    float t = 0.f;
+    for (int j = cx; j < 256; j += cv) t += red[j * V + e];
+    part[g * 2 * C + cx * V + e] = t;
+  }
+}
+
 // NCHW fp32 [N][3][H][W] -> NHWC T [N][H][W][Cpad] (zero padded)
 template <typename T>
 __global__ void pack_input_kernel(const float* x, int N, int C, int H, int W, int Cpad, T* y) {
@@ -1886,10 +2031,62 @@ UNETSEG_API int unetseg_upsample2x_bwd(int dtype, const void* dy, int ldy, int n
   return 0;
 }
 
+// host restatement of up_taps' tap count: the most nonzero column taps any input column has (4 or 5)
+static int up_taps_max(int in, int align) {
+  const int out = 2 * in;
+  int best = 0;
+  for (int i = 0; i < in; ++i) {
+    int lo, hi;
+    if (align) {
+      lo = in > 1 ? (int)floorf((float)(i - 1) * (out - 1) / (float)(in - 1)) : 0;
+      hi = in > 1 ? (int)ceilf((float)(i + 1) * (out - 1) / (float)(in - 1)) : out - 1;
+    } else {
+      lo = 2 * i - 2;
+      hi = i == in - 1 ? out - 1 : 2 * i + 2;
+    }
+    lo = std::max(lo, 0);
+    hi = std::min(hi, out - 1);
+    int cnt = 0;
+    for (int d = lo; d <= hi; ++d) {
+      float src;
+      if (align) {
+        const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+        src = scale * (float)d;
+      } else {
+        src = ((float)d + 0.5f) * 0.5f - 0.5f;
+        if (src < 0.f) src = 0.f;
+      }
+      int i0 = (int)src;
+      if (i0 > in - 1) i0 = in - 1;
+      const int i1 = i0 + 1 < in ? i0 + 1 : in - 1;
+      const float l1 = src - (float)i0;
+      float wgt = 0.f;
+      if (i0 == i) wgt += 1.f - l1;
+      if (i1 == i) wgt += l1;
+      if (wgt != 0.f) ++cnt;
+    }
+    best = std::max(best, cnt);
+  }
+  return best;
+}
+
+// rows per block of the row-streaming upsample backward (0: the row-blocked kernel): 16 where that
+// still gives >= 2048 blocks, else 8; h must be a multiple (UNETSEG_UP_STREAM=0: off)
+static int up_stream_rows(int dtype, int n, int h, int w, int c) {
+  const char* e = getenv("UNETSEG_UP_STREAM");
+  if (e && atoi(e) == 0) return 0;
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  const long xb = ceil_div((long)w * (c / V), 256);
+  for (int rs : {16, 8})
+    if (h % rs == 0 && (xb * ((long)n * h / rs) >= 2048 || rs == 8)) return rs;
+  return 0;
+}
+
 // partial rows (blocks) of unetseg_upsample2x_bwd_relu for this shape
 UNETSEG_API int unetseg_upsample2x_bwd_tiles(int dtype, int n, int h, int w, int c) {
   const int V = dtype == DT_BF16 ? 8 : 4;
-  return ceil_div((long)w * (c / V), 256) * ceil_div((long)n * h, up_rows_pb());
+  const int rs = up_stream_rows(dtype, n, h, w, c);
+  return ceil_div((long)w * (c / V), 256) * ceil_div((long)n * h, rs ? rs : up_rows_pb());
 }
 
 UNETSEG_API int unetseg_upsample2x_bwd_relu(int dtype, const void* dy, int ldy, int n, int h, int w, int c,
@@ -1904,6 +2101,32 @@ UNETSEG_API int unetseg_upsample2x_bwd_relu(int dtype, const void* dy, int ldy, 
   hipLaunchKernelGGL((upsample_bwd_relu_kernel<T, R>), dim3(ceil_div(w * (c / VE<T>), 256), ceil_div(n * h, R)),       \
                      dim3(256), 0, (hipStream_t)stream, (const T*)dy, ldy, n, h, w, c, align_corners, (const T*)a, lda, \
                      (T*)dx, ldx, part)
+  const int rs = up_stream_rows(dtype, n, h, w, c);
+  if (rs) {
+    const int K = up_taps_max(w, align_corners) <= 4 ? 4 : 5;
+    // dy rows in flight ahead of the consumed one (UNETSEG_UP_STREAM_PF=1 or 2)
+    static const int pf = getenv("UNETSEG_UP_STREAM_PF") && atoi(getenv("UNETSEG_UP_STREAM_PF")) == 2 ? 2 : 1;
+#define UP_STREAM(RS, KK)                                                                                      \
+  {                                                                                                            \
+    if (pf == 1) {                                                                                             \
+      UP_STREAM_PF(RS, KK, 1);                                                                                 \
+    } else {                                                                                                   \
+      UP_STREAM_PF(RS, KK, 2);                                                                                 \
+    }                                                                                                          \
+  }
+#define UP_STREAM_PF(RS, KK, PFV)                                                                              \
+  hipLaunchKernelGGL((upsample_bwd_relu_stream_kernel<T, RS, KK, PFV>), dim3(ceil_div(w * (c / VE<T>), 256), n * h / RS), \
+                     dim3(256), 0, (hipStream_t)stream, (const T*)dy, ldy, n, h, w, c, align_corners, (const T*)a, lda, \
+                     (T*)dx, ldx, part)
+#define UP_STREAM_K(RS) \
+  if (K == 4) UP_STREAM(RS, 4) else UP_STREAM(RS, 5)
+    DISPATCH_T(dtype, if (rs == 16) { UP_STREAM_K(16) } else { UP_STREAM_K(8) });
+#undef UP_STREAM_K
+#undef UP_STREAM
+#undef UP_STREAM_PF
+    US_LAUNCH_CHECK("upsample_bwd_relu");
+    return 0;
+  }
   const int rpb = up_rows_pb();
   DISPATCH_T(dtype, if (rpb == 2) UP_BWD_RELU(2); else if (rpb == 8) UP_BWD_RELU(8); else UP_BWD_RELU(kUpRowsPB));
 #undef UP_BWD_RELU
