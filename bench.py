@@ -41,6 +41,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "images/sec training unet_resnet50 512×512 bf16 at 1/2/4/8 GPUs; mIoU parity"
 GFLOP_PER_IMG = {"unet_resnet50": 547.46, "multitask_unet": 547.36, "attention_unet": 1374.35, "unet_plain": 83.48}
 PEAK_BF16_TFLOPS = 2516.6  # gfx950 dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
+HBM_PRACTICAL = 6.3e12  # B/s: what a streaming kernel reaches on this card (tools/hbm_bw.py), the floors' HBM rate
 
 
 def parse():
@@ -470,13 +471,16 @@ def main():
                     us = e0.elapsed_time(e1) * 1e3
                     f.write(f"{kind:9s} {us:9.1f} us {flops / max(us, 1e-3) / 1e6:8.1f} TF/s  {desc}\n")
         comp = {}
+        floor = {}  # per call max(flops / MFMA peak, compulsory bytes / practical HBM rate), summed
         for kind, flops, nl, e0, e1, desc in ops.PROBE:
             d = kinds.setdefault(kind, [0.0, 0.0, 0])
             d[0] += flops
             d[1] += e0.elapsed_time(e1) * 1e-3
             d[2] += nl
             if desc is not None:
-                comp[kind] = comp.get(kind, 0) + compulsory_bytes(desc)
+                cb = compulsory_bytes(desc)
+                comp[kind] = comp.get(kind, 0) + cb
+                floor[kind] = floor.get(kind, 0.0) + max(flops / (PEAK_BF16_TFLOPS * 1e12), cb / HBM_PRACTICAL)
         ops.PROBE = None
         dom = max(kinds, key=lambda k: kinds[k][1])
         fl, sec, n = kinds[dom]
@@ -491,8 +495,11 @@ def main():
                 "mfma_busy": mb[0] if mb else None, "mfma_busy_source": mb[1] if mb else None,
                 "launches_per_step": n, "avg_launch_us": round(1e6 * sec / n, 2),
                 "algorithmic_gflop_per_step": round(fl / 1e9, 1),
+                "floor_ms_per_step": round(1e3 * floor.get(dom, 0.0), 3),
+                "floor_rule": "sum over calls of max(algorithmic flop / MFMA peak, compulsory bytes / 6.3 TB/s)",
                 "kernels": {k: {"tflops": round(v[0] / v[1] / 1e12, 2), "ms_per_step": round(1e3 * v[1], 3),
-                                "launches": v[2]} for k, v in kinds.items()}}
+                                "launches": v[2], "floor_ms": round(1e3 * floor.get(k, 0.0), 3)}
+                            for k, v in kinds.items()}}
 
     plan_stats = plan_state["plan"].stats() if plan_state and plan_state["plan"] is not None else None
     # data-parallel consistency: after identical averaged updates every rank holds the same weights

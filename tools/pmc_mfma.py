@@ -18,7 +18,7 @@ import sys
 from collections import defaultdict
 
 GROUPS = {
-    "igemm_tn": re.compile(r"(tn_fast_kernel|halo3_kernel<|igemm_tn_kernel)"),
+    "igemm_tn": re.compile(r"(tn_fast_kernel|tn_multi_kernel|tn_halo_persist_kernel|halo3_kernel<|stem_halo_kernel|first3x3_fwd_kernel|igemm_tn_kernel)"),
     "wgrad": re.compile(r"(wgrad_fast_kernel|wgrad_ring_kernel|halo3_wgrad_kernel|wgrad_kernel<)"),
 }
 SIMDS = 256 * 4

@@ -15,7 +15,7 @@ import re
 import sys
 
 GROUPS = {
-    "igemm_tn": re.compile(r"(tn_fast_kernel|halo3_kernel<|igemm_tn_kernel)"),
+    "igemm_tn": re.compile(r"(tn_fast_kernel|tn_multi_kernel|tn_halo_persist_kernel|halo3_kernel<|stem_halo_kernel|first3x3_fwd_kernel|igemm_tn_kernel)"),
     "wgrad": re.compile(r"(wgrad_fast_kernel|wgrad_ring_kernel|wgrad_kernel|wgrad_reduce_kernel)"),
 }
 
@@ -37,7 +37,7 @@ def main():
         if not fb or not wb:
             continue
         # launches of the main GEMM kernels (reduce kernels fold into their wgrad launch)
-        main_pat = re.compile(r"(tn_fast_kernel|halo3_kernel<|igemm_tn_kernel|wgrad_fast_kernel<|wgrad_ring_kernel<|wgrad_kernel<)")
+        main_pat = re.compile(r"(tn_fast_kernel|tn_multi_kernel|tn_halo_persist_kernel|halo3_kernel<|stem_halo_kernel|first3x3_fwd_kernel|igemm_tn_kernel|wgrad_fast_kernel<|wgrad_ring_kernel<|wgrad_kernel<)")
         nl = sum(1 for n, _ in fetch if main_pat.search(n) and pat.search(n))
         f2, w = 2.0 * sum(fb), sum(wb)
         res["groups"][g] = {"launches": nl, "fetch_bytes_per_launch": f2 / nl, "write_bytes_per_launch": w / nl,
@@ -52,7 +52,7 @@ def main():
         k = n.replace("void (anonymous namespace)::", "").replace("(anonymous namespace)::", "").split("(")[0][:80]
         if k in per:
             per[k][2] += v
-    top = sorted(per.items(), key=lambda kv: -(kv[1][1] + kv[1][2]))[:25]
+    top = sorted(per.items(), key=lambda kv: -(kv[1][1] + kv[1][2]))[:120]
     res["kernels"] = {k: {"launches": c, "fetch_bytes_per_launch": f / c, "write_bytes_per_launch": w / c}
                       for k, (c, f, w) in top}
     json.dump(res, open(out, "w"), indent=1)

@@ -50,6 +50,30 @@ def main():
     print("idle before each kernel type (us/step, count/step):")
     for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:15]:
         print(f"  {t / steps:8.1f} us {c / steps:5.1f}x  {n}")
+    # which other-stream kernels ran while the compute stream sat idle: for every
+    # gap >= 20 us, the overlapping kernels of the other streams and how much of the gap each covers
+    others = [k for s, lst in by.items() if s != main_stream for k in lst]
+    held = defaultdict(lambda: [0, 0.0])
+    print("gaps >= 20 us and the other streams' kernels running inside them:")
+    shown = 0
+    for i in range(1, len(cs)):
+        g0, g1 = cs[i - 1][1], cs[i][0]
+        if g1 - g0 < 20_000:
+            continue
+        cov = []
+        for a, b, s, n in others:
+            ov = min(b, g1) - max(a, g0)
+            if ov > 0:
+                cov.append((ov, short(n)))
+                held[short(n)][0] += 1
+                held[short(n)][1] += ov / 1e3
+        if shown < 16:
+            desc = ", ".join(f"{n} {ov / 1e3:.0f}" for ov, n in sorted(cov, reverse=True)[:3]) or "nothing (host / launch)"
+            print(f"  {(g1 - g0) / 1e3:7.1f} us before {short(cs[i][3])}: {desc}")
+            shown += 1
+    print("other-stream kernels overlapping compute-stream gaps >= 20 us (us/step, gaps/step):")
+    for n, (c, t) in sorted(held.items(), key=lambda kv: -kv[1][1])[:10]:
+        print(f"  {t / steps:8.1f} us {c / steps:5.1f}x  {n}")
     print("non-library launches (per stream: before -> this -> after):")
     seen = Counter()
     for s, lst in by.items():
