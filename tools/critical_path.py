@@ -49,7 +49,13 @@ def main():
     cs = [k for k in sel if k[2] == ks[mark[-1]][2]]
     tr = json.load(open(traffic_p)).get("kernels", {})
     line = [ln for ln in open(bench_p).read().splitlines() if ln.startswith("{")][-1]
-    roof = json.loads(line).get("roofline") or {}
+    bj = json.loads(line)
+    roof = bj.get("roofline") or {}
+    wl = (bj.get("config") or {}).get("workload", "")
+    model = wl.split()[0] if wl else "unet_resnet50"
+    m = re.search(r"per-GPU batch (\d+)", wl)
+    batch = int(m.group(1)) if m else 16
+    gflop = {"unet_resnet50": 547.46, "multitask_unet": 547.36, "attention_unet": 1374.35}.get(model, 547.46)
     conv_floor = roof.get("floor_ms_per_step")
     agg = defaultdict(lambda: [0, 0.0, 0.0, 0])  # launches, ms, floor ms, launches without PMC bytes
     for a, b, _, n in cs:
@@ -82,8 +88,9 @@ def main():
     print(f"| idle between kernels | - | {idle / steps:.3f} | 0 | {idle / steps:.3f} |")
     step = tot_ms + idle / steps
     print(f"| **step (compute stream)** | {len(cs) / steps:.0f} | **{step:.3f}** | **{tot_floor:.3f}** | {step - tot_floor:.3f} |")
-    print(f"\nsum of floors {tot_floor:.3f} ms = {16 / tot_floor * 1e3:.0f} img/s at B=16 "
-          f"(step fraction {547.46 * 16 / tot_floor / 2516.6:.3f}); 0.35 needs <= 9.94 ms")
+    need = gflop * batch / 2516.6 / 0.35
+    print(f"\nsum of floors {tot_floor:.3f} ms = {batch / tot_floor * 1e3:.0f} img/s ({model}, B={batch}; "
+          f"step fraction {gflop * batch / tot_floor / 2516.6:.3f}); 0.35 needs <= {need:.2f} ms per step")
 
 
 if __name__ == "__main__":

@@ -282,6 +282,11 @@ WG_SERIAL_HW = int(os.environ.get("UNETSEG_WG_SERIAL_HW", "0"))
 #: (layer1 serial no better than stem + layer1; none equal to stem within noise)
 WG_SERIAL_LAYERS = frozenset(v for v in os.environ.get("UNETSEG_WG_SERIAL_LAYERS", "stem").split(",") if v)
 
+#: the side-stream weight gradient is enqueued after its layer's data gradient and waits for it
+#: (UNETSEG_WG_AFTER_DGRAD=1): the data gradient -- the critical path -- then gets the CUs first instead
+#: of both becoming ready on the same event and sharing them (round 6 experiment)
+WG_AFTER_DGRAD = os.environ.get("UNETSEG_WG_AFTER_DGRAD", "0") == "1"
+
 #: only the virtual-concat convs (the decoder's unetUp conv1) are held back (UNETSEG_WG_DEFER_CAT=0: every 3x3)
 WG_DEFER_CAT = os.environ.get("UNETSEG_WG_DEFER_CAT", "1") == "1"
 
@@ -594,7 +599,8 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
         serial = not deferred and ((bool(WG_SERIAL_HW) and Pq * Qq >= WG_SERIAL_HW and R * S > 1) or
                                    layer in WG_SERIAL_LAYERS)
         wstream = None
-        if not deferred and not serial:
+        after = WG_AFTER_DGRAD and not deferred and not serial
+        if not deferred and not serial and not after:
             wstream = launch_wgrad()
         # data gradient (reads the packed weight pc.wt: the parameter is reported done after it)
         if Kp != K:
@@ -621,6 +627,8 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
                                  H, W, 0, ctx.stream)
             give_grad(ctx, x1, g[..., :C1])
             give_grad(ctx, x2, g[..., C1:])
+        if after:
+            wstream = launch_wgrad()  # the side stream waits for the data gradient just enqueued
         if serial:
             launch_wgrad(serial=True)  # after the data gradient, on the compute stream
         if deferred:
