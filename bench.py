@@ -142,7 +142,8 @@ def cpu_baseline(model_name, size, batch):
     out["sample"] = (f"oracle {model_name} {size}x{size} batch {batch}, 1 warmup + 2 timed train steps "
                      f"(fwd+{'bce+ce' if multitask else 'lovasz'}+bwd+Adam) per precision, best step "
                      f"{t_main:.2f} s, {threads} threads (this process's CPU share of {visible}), "
-                     f"torch {torch.__version__} CPU")
+                     f"torch {torch.__version__} CPU; a bounded sample: the GPU line runs the same model "
+                     f"and size at its own batch, images/s per image either way")
     return out
 
 

@@ -104,7 +104,8 @@ int unetseg_conv2d_fwd_affine(int dtype, const void* x1, int c1, int ldc1, const
  * 6 128x64, 7 256x128 LDS-DMA ring, 8 128x128 ring, 9 64x128 ring, 10 128x128 5-stage ring,
  * 11-14 other rings), 17 / 18 = the parity classes of a stride-2 data gradient merged into one launch
  * on 128x128 / 64x128 tiles, 19 / 20 = short-K (2-4 steps) 128x128 / 128x64 tiles on one LDS stage,
- * 100 = generic igemm kernel (fp32 / unaligned channels).  *taps_out = the
+ * 21 / 22 / 23 = halo-A ring 256x128 / 256x64 / 128x128, 24 / 25 = the first two persistent (several tiles per
+ * block), 100 = generic igemm kernel (fp32 / unaligned channels).  *taps_out = the
  * compile-time tap count of an LDS-DMA ring (9 or 1; 0 = generic ring or not a ring). */
 int unetseg_conv2d_fwd_config(int dtype, int c1, int ldc1, int c2, int ldc2, int n, int h, int w, int cout, int r,
                               int s, int stride, int pad, int* taps_out);

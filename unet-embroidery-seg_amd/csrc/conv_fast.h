@@ -107,7 +107,8 @@ struct HaloWgradArgs {
 // kernel-configuration codes reported by the unetseg_conv2d_*_config queries (include/unetseg_hip.h)
 // 1..14: TN tile configurations of tn_config (conv_fast.hip); 17 / 18: stride-2 dgrad parity classes
 // merged into one launch on 128x128 / 64x128 register-staged tiles (launch_tn_multi); 19 / 20: short K
-// (2-4 steps) on one LDS stage, 128x128 / 128x64
+// (2-4 steps) on one LDS stage, 128x128 / 128x64; 21-23: halo-A rings 256x128 / 256x64 / 128x128; 24 / 25:
+// the 256x128 / 256x64 halo-A rings persistent (tn_halo_persist_kernel, several tiles per block)
 enum { kCfgHalo = 0, kCfgMulti128 = 17, kCfgMulti64 = 18, kCfgStemHalo = 30, kCfgFirst3x3 = 31, kCfgGeneric = 100 };
 enum { kWgHalo = 0, kWgFastRow64x256 = 1, kWgFastRow128 = 2, kWgFast64x256 = 3, kWgFast128 = 4, kWgGeneric = 5,
        kWgRing64x256 = 6, kWgRing128 = 7 };
