@@ -101,17 +101,22 @@ __device__ __forceinline__ void fin_row_sums(const float* part, long ldrow, int 
 #pragma unroll
   for (int j = 0; j < NQ; ++j) t[j] = 0.0;
   for (int g0 = 0; g0 < G; g0 += kFinRPL * NL) {
+    // every load unconditional (a row past G re-reads row G - 1, a quantity past nq the last one) and
+    // masked after it: a load under a lane condition got its own branch and a vmcnt(0) behind it, which
+    // serialised all kFinRPL x NQ round trips of the lane
     float v[NQ][kFinRPL];
 #pragma unroll
     for (int k = 0; k < kFinRPL; ++k) {
-      const int g = g0 + li + k * NL;
+      const int g = min(g0 + li + k * NL, G - 1);
 #pragma unroll
-      for (int j = 0; j < NQ; ++j) v[j][k] = (g < G && j < nq) ? part[g * ldrow + (long)(q0 + j) * C + c] : 0.f;
+      for (int j = 0; j < NQ; ++j) v[j][k] = part[g * ldrow + (long)(q0 + min(j, nq - 1)) * C + c];
     }
 #pragma unroll
-    for (int k = 0; k < kFinRPL; ++k)
+    for (int k = 0; k < kFinRPL; ++k) {
+      const bool ok = g0 + li + k * NL < G;
 #pragma unroll
-      for (int j = 0; j < NQ; ++j) t[j] += (double)v[j][k];
+      for (int j = 0; j < NQ; ++j) t[j] += (ok && j < nq) ? (double)v[j][k] : 0.0;
+    }
   }
   fin_group_sum<NWV, NQ>(t, sc);
 }
@@ -133,6 +138,9 @@ __global__ __launch_bounds__(NWV > 4 ? 64 * NWV : 256) void bn_finalize_kernel(c
   if (NWV == 1 && c >= C) return;  // whole waves: no barrier in the one-wave form
   const int li = NWV == 1 ? (threadIdx.x & 63) : threadIdx.x;
   const long st = 2L * C;
+  // the epilogue's operands loaded up front (behind the reductions each was a round trip)
+  const float gam = gamma[c], bet = beta[c];
+  const float rm0 = rmean ? rmean[c] : 0.f, rv0 = rmean ? rvar[c] : 0.f;
   // pass 1 keeps this lane's rows in registers when one round covers G (pass 2 re-reads otherwise)
   float sv[kFinRPL], qv[kFinRPL];
   double tsum[1] = {0.0};
@@ -176,13 +184,13 @@ __global__ __launch_bounds__(NWV > 4 ? 64 * NWV : 256) void bn_finalize_kernel(c
     const double inv = 1.0 / sqrt(var + (double)eps);
     mean_out[c] = (float)mean;
     invstd_out[c] = (float)inv;
-    const float sca = (float)(gamma[c] * inv);
+    const float sca = (float)(gam * inv);
     scale[c] = sca;
-    shift[c] = (float)(beta[c] - mean * gamma[c] * inv);
+    shift[c] = (float)(bet - mean * gam * inv);
     if (rmean) {
       const double unb = M > 1 ? m2v / (double)(M - 1) : var;
-      rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
-      rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+      rmean[c] = (float)((1.0 - momentum) * rm0 + momentum * mean);
+      rvar[c] = (float)((1.0 - momentum) * rv0 + momentum * unb);
     }
     if (nbt && c == 0) nbt[0] += 1;
   }
@@ -572,13 +580,15 @@ __global__ __launch_bounds__(NWV > 4 ? 64 * NWV : 256) void bn_bwd_finalize_rows
   __shared__ double sc[2 * NWV];
   const int c = NWV == 1 ? (int)blockIdx.x * 4 + (threadIdx.x >> 6) : (int)blockIdx.x;
   if (NWV == 1 && c >= C) return;
+  // the epilogue's operands loaded up front: behind the reduction each was another round trip
+  const float pg = dg1[c], pb = db1[c], k1 = g1[c] * inv1[c];
   double t[2];
   fin_row_sums<NWV, 2>(part, 2L * C, C, c, G, 2, 0, t, sc);
   if ((NWV == 1 ? (threadIdx.x & 63) : threadIdx.x) == 0) {
     const double a0 = t[0], a1 = t[1];
-    dg1[c] += (float)a1;
-    db1[c] += (float)a0;
-    coef[0 * C + c] = g1[c] * inv1[c];
+    dg1[c] = pg + (float)a1;
+    db1[c] = pb + (float)a0;
+    coef[0 * C + c] = k1;
     coef[1 * C + c] = (float)(a0 / (double)M);
     coef[2 * C + c] = (float)(a1 / (double)M);
   }
@@ -596,19 +606,26 @@ __global__ __launch_bounds__(NWV > 4 ? 64 * NWV : 256) void bn_bwd_finalize_rows
   const int c = NWV == 1 ? (int)blockIdx.x * 4 + (threadIdx.x >> 6) : (int)blockIdx.x;
   if (NWV == 1 && c >= C) return;
   const int nq = 1 + nbranch;
+  const float pg1 = dg1[c], pb1 = db1[c], k1 = g1[c] * inv1[c];
+  float pg2 = 0.f, pb2 = 0.f, k2 = 0.f;
+  if (nbranch == 2) {
+    pg2 = dg2[c];
+    pb2 = db2[c];
+    k2 = g2[c] * inv2[c];
+  }
   double t[3];
   fin_row_sums<NWV, 3>(part, (long)nq * C, C, c, G, nq, 0, t, sc);
   if ((NWV == 1 ? (threadIdx.x & 63) : threadIdx.x) == 0) {
     const double sdz = t[0];
-    dg1[c] += (float)t[1];
-    db1[c] += (float)sdz;
-    coef[0 * C + c] = g1[c] * inv1[c];
+    dg1[c] = pg1 + (float)t[1];
+    db1[c] = pb1 + (float)sdz;
+    coef[0 * C + c] = k1;
     coef[1 * C + c] = (float)(sdz / (double)M);
     coef[2 * C + c] = (float)(t[1] / (double)M);
     if (nbranch == 2) {
-      dg2[c] += (float)t[2];
-      db2[c] += (float)sdz;
-      coef[3 * C + c] = g2[c] * inv2[c];
+      dg2[c] = pg2 + (float)t[2];
+      db2[c] = pb2 + (float)sdz;
+      coef[3 * C + c] = k2;
       coef[4 * C + c] = (float)(sdz / (double)M);
       coef[5 * C + c] = (float)(t[2] / (double)M);
     }
@@ -622,9 +639,14 @@ __global__ __launch_bounds__(NWV > 4 ? 64 * NWV : 256) void colsum_rows_kernel(c
   __shared__ double sc[NWV];
   const int c = NWV == 1 ? (int)blockIdx.x * 4 + (threadIdx.x >> 6) : (int)blockIdx.x;
   if (NWV == 1 && c >= C) return;
+  const float prev = accumulate ? out[c] : 0.f;
   double t[1];
-  fin_row_sums<NWV, 1>(part, 2L * C, C, c, G, 1, k, t, sc);
-  if ((NWV == 1 ? (threadIdx.x & 63) : threadIdx.x) == 0) out[c] = accumulate ? out[c] + (float)t[0] : (float)t[0];
+  if (G > 0) {
+    fin_row_sums<NWV, 1>(part, 2L * C, C, c, G, 1, k, t, sc);
+  } else {
+    t[0] = 0.0;
+  }
+  if ((NWV == 1 ? (threadIdx.x & 63) : threadIdx.x) == 0) out[c] = accumulate ? prev + (float)t[0] : (float)t[0];
 }
 
 // out[c] (+)= sum_g part[c][g]   (fp64 accumulation, fixed order)
