@@ -833,6 +833,99 @@ __global__ void maxpool_bwd_k3s2_kernel(const T* dy, int ldy, const uint8_t* idx
   }
 }
 
+// The U-Net encoders' 2x2 / stride-2 pool (model/unet_plain.py:25, model/unet_attention.py) when the
+// windows tile the input exactly (h = 2P, w = 2Q): one thread per window and V channels, the four
+// loads issued together (the generic kernel's loop waited on each), the same comparisons in the same
+// order as maxpool_fwd_kernel (bit-identical), the argmax bytes stored with one 8-B store.
+template <typename T>
+__global__ void maxpool_fwd_k2s2_kernel(const T* x, int ldx, int N, int H, int W, int C, int P, int Q, T* y, int ldy,
+                                        uint8_t* idx) {
+  constexpr int V = VE<T>;
+  const int cv = C / V;
+  const int total = N * P * Q * cv;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    int t = i;
+    const int v = t % cv; t /= cv;
+    const int q = t % Q; t /= Q;
+    const int p = t % P;
+    const int n = t / P;
+    const int c0 = v * V;
+    float xv[4][V];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) load_vec(x + (size_t)((n * H + 2 * p + r) * W + 2 * q + u) * ldx + c0, xv[r * 2 + u]);
+    float best[V];
+    uint8_t bi[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+        if (xv[j][e] > best[e] || isnan(xv[j][e])) {
+          if (!isnan(best[e])) { best[e] = xv[j][e]; bi[e] = (uint8_t)j; }
+        }
+    const size_t opix = (size_t)((n * P + p) * Q + q);
+    store_vec(y + opix * ldy + c0, best);
+    if constexpr (V == 8) {
+      uint2 pk;
+      __builtin_memcpy(&pk, bi, 8);
+      *reinterpret_cast<uint2*>(idx + opix * C + c0) = pk;
+    } else {
+      unsigned pk;
+      __builtin_memcpy(&pk, bi, 4);
+      *reinterpret_cast<unsigned*>(idx + opix * C + c0) = pk;
+    }
+  }
+}
+
+// Its gradient: each input pixel lies in exactly one window, so one thread per window writes the
+// window's four pixels from one dy load and one argmax load (the generic gather loaded the argmax
+// bytes one at a time); values as maxpool_bwd_kernel's (0 + dy where the argmax matches, then + old).
+template <typename T>
+__global__ void maxpool_bwd_k2s2_kernel(const T* dy, int ldy, const uint8_t* idx, int N, int H, int W, int C, int P,
+                                        int Q, T* dx, int ldx, int accumulate) {
+  constexpr int V = VE<T>;
+  const int cv = C / V;
+  const int total = N * P * Q * cv;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    int t = i;
+    const int v = t % cv; t /= cv;
+    const int q = t % Q; t /= Q;
+    const int p = t % P;
+    const int n = t / P;
+    const int c0 = v * V;
+    const size_t opix = (size_t)((n * P + p) * Q + q);
+    float g[V];
+    load_vec(dy + opix * ldy + c0, g);
+    uint8_t ib[V];
+    if constexpr (V == 8) {
+      const uint2 pk = *reinterpret_cast<const uint2*>(idx + opix * C + c0);
+      __builtin_memcpy(ib, &pk, 8);
+    } else {
+      const unsigned pk = *reinterpret_cast<const unsigned*>(idx + opix * C + c0);
+      __builtin_memcpy(ib, &pk, 4);
+    }
+    float old[4][V];
+    if (accumulate)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        load_vec(dx + (size_t)((n * H + 2 * p + (j >> 1)) * W + 2 * q + (j & 1)) * ldx + c0, old[j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float o[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        o[e] = 0.f;
+        if (ib[e] == (uint8_t)j) o[e] += g[e];
+        if (accumulate) o[e] += old[j][e];
+      }
+      store_vec(dx + (size_t)((n * H + 2 * p + (j >> 1)) * W + 2 * q + (j & 1)) * ldx + c0, o);
+    }
+  }
+}
+
 // gather form: dx[h][w] (+)= sum over windows containing (h,w) whose argmax is (h,w)
 template <typename T>
 __global__ void maxpool_bwd_kernel(const T* dy, int ldy, const uint8_t* idx, int N, int H, int W, int C, int k, int s,
@@ -1316,14 +1409,11 @@ __global__ void pw_small_fwd_kernel(const T* x, int ldx, long M, int HW, int C, 
       float acc[U][K];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const long p = pbase + u * 8 + sub;
+        // unconditional (clamped) load: a load under the lane condition got a branch and a vmcnt(0)
+        // of its own, which serialised the four groups; past-the-end pixels are never stored
+        const long pc = min(pbase + u * 8 + sub, p1 - 1);
         float xv[V];
-        if (p < p1) {
-          load_vec(x + p * ldx + v * V, xv);
-        } else {
-#pragma unroll
-          for (int e = 0; e < V; ++e) xv[e] = 0.f;
-        }
+        load_vec(x + pc * ldx + v * V, xv);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           float a0 = 0.f;
@@ -1540,10 +1630,10 @@ __global__ void attn_apply_kernel(const T* skip, int lds_, const float* psi, con
 }
 
 // backward 1: d_skip (+)= dg * alpha ; dpsibn[p] = (sum_c dg*skip) * alpha*(1-alpha);
-// partials [2][1][G]: sum dpsibn, sum dpsibn * xhat(psi)
-template <typename T>
+// partials [2][1][G]: sum dpsibn, sum dpsibn * xhat(psi).  ACC: d_skip accumulates onto its buffer
+template <typename T, bool ACC>
 __global__ void attn_bwd1_kernel(const T* dg, int ldg, const T* skip, int lds_, const float* alpha, const float* psi,
-                                 const float* mean, const float* inv, T* dskip, int ldds, int ds_acc, float* dpsibn,
+                                 const float* mean, const float* inv, T* dskip, int ldds, float* dpsibn,
                                  long M, int C, int pix_per_block, float* part, int G) {
   constexpr int V = VE<T>;
   __shared__ double sred[16];
@@ -1555,44 +1645,52 @@ __global__ void attn_bwd1_kernel(const T* dg, int ldg, const T* skip, int lds_, 
   const int sub = lane / cv, v = lane % cv;
   const long p0 = (long)blockIdx.x * pix_per_block;
   const long p1 = min(M, p0 + pix_per_block);
+  const float mu = mean[0], iv = inv[0];
   double s0 = 0.0, s1 = 0.0;
   if (nchunk == 1) {
-    // one vector per lane per pixel: four pixel groups per wave in flight (loads of all four
-    // issued before the first use), the serial form kept one group's latency exposed per step
+    // one vector per lane per pixel, four pixel groups per wave in flight.  Every load of the four
+    // groups is unconditional (a pixel past the block's end re-reads its last one; only the stores are
+    // masked) and the lane reductions of the four run interleaved: a load under a lane condition got
+    // its own branch and a vmcnt(0) behind it, which serialised the groups
     constexpr int U = 4;
     const int c0 = v * V;
     const long step = (long)nw * ppw;
     for (long pb = p0 + (long)wid * ppw; pb < p1; pb += U * step) {
-      float g[U][V], sk[U][V], old[U][V], al[U];
+      float g[U][V], sk[U][V], old[U][V], al[U], ps[U], dot[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const long p = pb + u * step + sub;
-        al[u] = 0.f;
-#pragma unroll
-        for (int e = 0; e < V; ++e) g[u][e] = sk[u][e] = old[u][e] = 0.f;
-        if (p < p1) {
-          al[u] = alpha[p];
-          load_vec(dg + p * ldg + c0, g[u]);
-          load_vec(skip + p * lds_ + c0, sk[u]);
-          if (ds_acc) load_vec(dskip + p * ldds + c0, old[u]);
-        }
+        const long pc = min(pb + u * step + sub, p1 - 1);
+        al[u] = alpha[pc];
+        ps[u] = psi[pc];
+        load_vec(dg + pc * ldg + c0, g[u]);
+        load_vec(skip + pc * lds_ + c0, sk[u]);
+        if (ACC) load_vec(dskip + pc * ldds + c0, old[u]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const long p = pb + u * step + sub;
-        float dot = 0.f, o[V];
+        float o[V];
+        dot[u] = 0.f;
 #pragma unroll
         for (int e = 0; e < V; ++e) {
-          dot += g[u][e] * sk[u][e];
-          o[e] = g[u][e] * al[u] + old[u][e];
+          dot[u] += g[u][e] * sk[u][e];
+          o[e] = ACC ? g[u][e] * al[u] + old[u][e] : g[u][e] * al[u] + 0.f;
         }
         if (p < p1) store_vec(dskip + p * ldds + c0, o);
-        for (int sh = 1; sh < cv; sh <<= 1) dot += __shfl_xor(dot, sh, 64);
+      }
+#pragma unroll
+      for (int sh = 1; sh < 64; sh <<= 1)
+        if (sh < cv)
+#pragma unroll
+          for (int u = 0; u < U; ++u) dot[u] += __shfl_xor(dot[u], sh, 64);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long p = pb + u * step + sub;
         if (p < p1 && v == 0) {
-          const float d = dot * al[u] * (1.f - al[u]);
+          const float d = dot[u] * al[u] * (1.f - al[u]);
           dpsibn[p] = d;
           s0 += d;
-          s1 += (double)d * (psi[p] - mean[0]) * inv[0];
+          s1 += (double)d * (ps[u] - mu) * iv;
         }
       }
     }
@@ -1614,7 +1712,7 @@ __global__ void attn_bwd1_kernel(const T* dg, int ldg, const T* skip, int lds_, 
           o[e] = g[e] * al;
         }
         T* dp = dskip + p * ldds + c0;
-        if (ds_acc) {
+        if (ACC) {
           float old[V];
           load_vec(dp, old);
 #pragma unroll
@@ -1628,7 +1726,7 @@ __global__ void attn_bwd1_kernel(const T* dg, int ldg, const T* skip, int lds_, 
       const float d = dot * al * (1.f - al);
       dpsibn[p] = d;
       s0 += d;
-      s1 += (double)d * (psi[p] - mean[0]) * inv[0];
+      s1 += (double)d * (psi[p] - mu) * iv;
     }
   }
   s0 = block_sum(s0, sred);
@@ -1995,8 +2093,13 @@ UNETSEG_API int unetseg_maxpool_fwd(int dtype, const void* x, int ldx, int n, in
   if (p_out) *p_out = p;
   if (q_out) *q_out = q;
   if (!y) return 0;  // shape query
-  if (k == 3 && s == 2 && (long)n * h * w * c < (1L << 31) && (long)n * h * w * ldx < (1L << 31) &&
-      (long)n * p * q * ldy < (1L << 31) && !getenv("UNETSEG_MAXPOOL_GENERIC"))
+  const bool fits = (long)n * h * w * c < (1L << 31) && (long)n * h * w * ldx < (1L << 31) &&
+                    (long)n * p * q * ldy < (1L << 31) && !getenv("UNETSEG_MAXPOOL_GENERIC");
+  if (k == 2 && s == 2 && h == 2 * p && w == 2 * q && fits)
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_k2s2_kernel<T>, dim3(grid_for((long)n * p * q * c / VE<T>)),
+                                         dim3(256), 0, (hipStream_t)stream, (const T*)x, ldx, n, h, w, c, p, q, (T*)y,
+                                         ldy, idx));
+  else if (k == 3 && s == 2 && fits)
     DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_fwd_k3s2_kernel<T>, dim3(grid_for((long)n * p * q * c / VE<T>)),
                                          dim3(256), 0, (hipStream_t)stream, (const T*)x, ldx, n, h, w, c, p, q, (T*)y,
                                          ldy, idx));
@@ -2013,8 +2116,13 @@ UNETSEG_API int unetseg_maxpool_bwd(int dtype, const void* dy, int ldy, const ui
                                     void* stream) {
   CHECK_VEC(dtype, c, "maxpool_bwd");
   US_CHECK_ARG(dy && idx && dx && k >= 1 && s >= 1 && n >= 0 && h >= 0 && w >= 0, "maxpool_bwd: bad args");
-  if (k == 3 && s == 2 && (long)n * h * w * c < (1L << 31) && (long)n * h * w * ldx < (1L << 31) &&
-      (long)n * p * q * ldy < (1L << 31) && !getenv("UNETSEG_MAXPOOL_GENERIC"))
+  const bool fits = (long)n * h * w * c < (1L << 31) && (long)n * h * w * ldx < (1L << 31) &&
+                    (long)n * p * q * ldy < (1L << 31) && !getenv("UNETSEG_MAXPOOL_GENERIC");
+  if (k == 2 && s == 2 && h == 2 * p && w == 2 * q && fits)
+    DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_k2s2_kernel<T>, dim3(grid_for((long)n * p * q * c / VE<T>)),
+                                         dim3(256), 0, (hipStream_t)stream, (const T*)dy, ldy, idx, n, h, w, c, p, q,
+                                         (T*)dx, ldx, accumulate));
+  else if (k == 3 && s == 2 && fits)
     DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_k3s2_kernel<T>,
                                          dim3(grid_for((long)n * ((h + 1) / 2) * ((w + 1) / 2) * c / VE<T>)), dim3(256),
                                          0, (hipStream_t)stream, (const T*)dy, ldy, idx, n, h, w, c, p, q, (T*)dx, ldx,
@@ -2292,9 +2400,14 @@ UNETSEG_API int unetseg_attn_bwd1(int dtype, const void* dg, int ldg, const void
   const int V = dtype == DT_BF16 ? 8 : 4;
   US_CHECK_ARG(((c / V) & (c / V - 1)) == 0, "attn_bwd1: C/V must be a power of two");
   const int G = unetseg_attn_bwd1_tiles(M);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(attn_bwd1_kernel<T>, dim3(G), dim3(256), 0, (hipStream_t)stream, (const T*)dg,
-                                       ldg, (const T*)skip, lds_, alpha, psi, mean, inv, (T*)dskip, ldds, ds_acc, dpsibn,
-                                       M, c, kAttnBwd1Tile, part, G));
+  if (ds_acc)
+    DISPATCH_T(dtype, hipLaunchKernelGGL((attn_bwd1_kernel<T, true>), dim3(G), dim3(256), 0, (hipStream_t)stream,
+                                         (const T*)dg, ldg, (const T*)skip, lds_, alpha, psi, mean, inv, (T*)dskip,
+                                         ldds, dpsibn, M, c, kAttnBwd1Tile, part, G));
+  else
+    DISPATCH_T(dtype, hipLaunchKernelGGL((attn_bwd1_kernel<T, false>), dim3(G), dim3(256), 0, (hipStream_t)stream,
+                                         (const T*)dg, ldg, (const T*)skip, lds_, alpha, psi, mean, inv, (T*)dskip,
+                                         ldds, dpsibn, M, c, kAttnBwd1Tile, part, G));
   US_LAUNCH_CHECK("attn_bwd1");
   return 0;
 }
