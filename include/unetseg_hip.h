@@ -237,6 +237,12 @@ int unetseg_bn_bwd_finalize_rows_res(const float* part, int C, int G, long M, in
                                      const float* inv1, float* dg1, float* db1, const float* g2, const float* inv2,
                                      float* dg2, float* db2, float* coef, void* stream);
 int unetseg_colsum_rows(const float* part, int C, int G, int k, float* out, int accumulate, void* stream);
+/* Row partials [G][nq][C] -> [ceil(G/16)][nq][C] (16 consecutive rows merged; nq 2 or 3), run ahead of the
+   finalizes above when G is large.  tile > 0: the rows are BN statistics (sum, M2 about the row mean) of
+   `tile` pixels each (the last min(tile, M - g*tile)) merged by Chan's formula (nq == 2), so the merged
+   partials feed unetseg_bn_finalize with tile * 16; tile == 0: plain sums.  No reference operator: an
+   internal reduction stage of BatchNorm2d's statistics / backward sums. */
+int unetseg_fin_merge_rows(const float* part, int C, int G, long M, int tile, int nq, float* out, void* stream);
 
 /* ---- pooling / resampling (nn.MaxPool2d: model/resnet_backbone.py:131, model/unet_plain.py:25,
  *      model/unet_attention.py:66-69; UpsamplingBilinear2d / Upsample / interpolate:

@@ -659,6 +659,61 @@ __global__ void colsum_finalize_kernel(const float* part, int C, int G, float* o
   if (threadIdx.x == 0) out[c] = accumulate ? out[c] + (float)acc : (float)acc;
 }
 
+// Row partials [G][nq][C] -> [ceil(G/R)][nq][C], R consecutive rows merged (ahead of a finalize when G
+// is large: the one-channel-per-block finalize then reads strided rows on only C blocks).  CHAN: the
+// rows are (sum, M2 about the row's mean) of `tile` pixels each (the last min(tile, M - g*tile)),
+// merged by Chan's formula in fp64; otherwise plain fp64 sums per quantity.  One wave per output row
+// and 64 channels, all R x nq loads issued before the adds (clamped, masked after).
+template <bool CHAN, int NQ, int R>
+__global__ __launch_bounds__(256) void fin_merge_rows_kernel(const float* part, int C, int G, long M, int tile, int nq,
+                                                             float* out, int G2) {
+  const int g2 = (int)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int c = (int)blockIdx.y * 64 + (threadIdx.x & 63);
+  if (g2 >= G2) return;
+  const int cc = min(c, C - 1);
+  float v[R][NQ];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int g = min(g2 * R + r, G - 1);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) v[r][q] = part[((long)g * nq + min(q, nq - 1)) * C + cc];
+  }
+  if (c >= C) return;
+  if constexpr (CHAN) {
+    double n = 0.0, s = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const long g = (long)g2 * R + r;
+      if (g < G) {
+        n += (double)min((long)tile, M - g * tile);
+        s += (double)v[r][0];
+      }
+    }
+    const double mean = s / n;
+    double m2 = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const long g = (long)g2 * R + r;
+      if (g < G) {
+        const double cnt = (double)min((long)tile, M - g * tile);
+        const double d = (double)v[r][0] / cnt - mean;
+        m2 += (double)v[r][1] + cnt * d * d;
+      }
+    }
+    out[(long)g2 * 2 * C + c] = (float)s;
+    out[(long)g2 * 2 * C + C + c] = (float)m2;
+  } else {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (q >= nq) break;
+      double t = 0.0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) t += g2 * R + r < G ? (double)v[r][q] : 0.0;
+      out[((long)g2 * nq + q) * C + c] = (float)t;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Max pool (pad 0), NHWC.  idx = argmax position inside the k x k window (first max wins, the
 // scan order of ATen's CPU kernel), stored as uint8.
@@ -2040,6 +2095,26 @@ UNETSEG_API int unetseg_relu_bwd_bias(int dtype, const void* dA, int ldd, const 
   DISPATCH_T(dtype, hipLaunchKernelGGL(relu_bwd_bias_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream,
                                        (const T*)dA, ldd, (const T*)A, lda, (T*)dY, ldy, M, C, tv, ppb, part, G));
   US_LAUNCH_CHECK("relu_bwd_bias");
+  return 0;
+}
+
+constexpr int kFinMergeR = 16;
+UNETSEG_API int unetseg_fin_merge_rows(const float* part, int C, int G, long M, int tile, int nq, float* out,
+                                       void* stream) {
+  US_CHECK_ARG(part && out && C > 0 && G > 0 && nq >= 1 && nq <= 3, "fin_merge_rows: bad args");
+  US_CHECK_ARG(tile == 0 || (nq == 2 && M > 0), "fin_merge_rows: a statistics merge needs nq == 2 and M");
+  const int G2 = ceil_div(G, kFinMergeR);
+  const dim3 grid(ceil_div(G2, 4), ceil_div(C, 64));
+  if (tile > 0)
+    hipLaunchKernelGGL((fin_merge_rows_kernel<true, 2, kFinMergeR>), grid, dim3(256), 0, (hipStream_t)stream, part, C,
+                       G, M, tile, nq, out, G2);
+  else if (nq == 3)
+    hipLaunchKernelGGL((fin_merge_rows_kernel<false, 3, kFinMergeR>), grid, dim3(256), 0, (hipStream_t)stream, part,
+                       C, G, M, tile, nq, out, G2);
+  else
+    hipLaunchKernelGGL((fin_merge_rows_kernel<false, 2, kFinMergeR>), grid, dim3(256), 0, (hipStream_t)stream, part,
+                       C, G, M, tile, nq, out, G2);
+  US_LAUNCH_CHECK("fin_merge_rows");
   return 0;
 }
 

@@ -89,6 +89,7 @@ SIGNATURES = {
     "unetseg_conv2d_dgrad_post": (I, [I, P, I, I, I, I, P, I, I, I, I, I, I, P, I, I, I, I, P, I, P, P, P, P, P, I,
                                       P]),
     "unetseg_bn_bwd_finalize_rows": (I, [P, I, I, L, P, P, P, P, P, P]),
+    "unetseg_fin_merge_rows": (I, [P, I, I, L, I, I, P, P]),
     "unetseg_conv2d_dgrad_post_res": (I, [I, P, I, I, I, I, P, I, I, P, I, P, I, P, P, P, P, I, P, P, P, I, P]),
     "unetseg_bn_bwd_finalize_rows_res": (I, [P, I, I, L, I, P, P, P, P, P, P, P, P, P, P]),
     "unetseg_colsum_rows": (I, [P, I, I, I, P, I, P]),

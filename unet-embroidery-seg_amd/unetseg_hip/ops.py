@@ -536,6 +536,7 @@ def conv(ctx, x1, pc, x2=None, relu=False, stats=False, out=None, head=None):
             part, rows = out.fused
             dY = dA
             if b is not None:
+                part, rows, _ = _merge_rows(ctx, part, K, rows, 2)
                 lib.colsum_rows(P(part), K, rows, 0, P(b.grad), 1, ctx.stream)
         elif relu:
             Gr = _q("reduce_tiles", ctx.dt, M, K, None, None)
@@ -819,6 +820,22 @@ class BNState:
     __slots__ = ("mean", "inv", "sc", "sh")
 
 
+#: finalize row partials with more rows than this are first merged 16 to 1 (unetseg_fin_merge_rows);
+#: UNETSEG_FIN_MERGE=0 finalizes them directly
+FIN_MERGE_MIN = int(os.environ.get("UNETSEG_FIN_MERGE_MIN", "512"))
+FIN_MERGE = os.environ.get("UNETSEG_FIN_MERGE", "1") != "0"
+
+
+def _merge_rows(ctx, part, C, G, nq, M=0, tile=0):
+    """(partials, rows, tile) for a finalize: large row counts merged 16 to 1 on the device"""
+    if not FIN_MERGE or G <= FIN_MERGE_MIN:
+        return part, G, tile
+    G2 = (G + 15) // 16
+    out = ctx.f32(G2, nq, C)
+    lib.fin_merge_rows(P(part), C, G, M, tile, nq, P(out), ctx.stream)
+    return out, G2, tile * 16
+
+
 def _bn_coeffs(ctx, bn, st, M, tile=None):
     """st: (partials [G][2][C], row tile) from conv(), or a bare partials tensor with `tile` given"""
     if isinstance(st, tuple):
@@ -828,7 +845,7 @@ def _bn_coeffs(ctx, bn, st, M, tile=None):
     if ctx.training:
         # one allocation for the four coefficient vectors (the host cost of a step is per allocation)
         s.sc, s.sh, s.mean, s.inv = ctx.f32(4, C).unbind(0)
-        G = st.shape[0]
+        st, G, tile = _merge_rows(ctx, st, C, st.shape[0], 2, M, tile)
         lib.bn_finalize(P(st), C, G, M, tile, P(bn.weight), P(bn.bias), P(bn.running_mean), P(bn.running_var),
                         P(bn.num_batches_tracked), bn.momentum, bn.eps, P(s.mean), P(s.inv), P(s.sc), P(s.sh),
                         ctx.stream)
@@ -910,6 +927,7 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None, lazy=False):
             # residual BN-add-ReLU: the next block's conv1 dgrad stored dz = mask * dA in dA's buffer and
             # the (sum dz, sum dz*xhat1 [, sum dz*xhat2]) row partials (_dgrad_fused_res)
             part, rows, nq = out.fused
+            part, rows, _ = _merge_rows(ctx, part, C, rows, nq)
             coef = ctx.f32(6, C)
             b2 = res_bn[2] if res_bn is not None else None
             y2 = res_bn[0] if res_bn is not None else None
@@ -939,6 +957,7 @@ def bn(ctx, y, st, bnm, relu=True, res=None, res_bn=None, lazy=False):
         if out.fused is not None:
             # the consumer's dgrad stored dz = dA * mask and the (sum dz, sum dz*xhat) row partials
             part, rows = out.fused
+            part, rows, _ = _merge_rows(ctx, part, C, rows, 2)
             coef = ctx.f32(6, C)
             lib.bn_bwd_finalize_rows(P(part), C, rows, M, P(bnm.weight), P(s1.inv), P(bnm.weight.grad),
                                      P(bnm.bias.grad), P(coef), ctx.stream)
