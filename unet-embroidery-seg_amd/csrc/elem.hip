@@ -1809,11 +1809,11 @@ __global__ void attn_bwd2_kernel(const float* dpsibn, const float* psi, const fl
   float sb = 0.f;
 #pragma unroll
   for (int e = 0; e < V; ++e) { wv[e] = wpsi[c0 + e]; sw[e] = 0.f; }
-  for (long p = p0 + ty; p < p1; p += rows) {
-    const float xh = (psi[p] - mean[0]) * inv[0];
-    const float dp = coef[0] * (dpsibn[p] - coef[1] - xh * coef[2]);
-    float fv[V], o[V];
-    load_vec(f + p * ldf + c0, fv);
+  const float mu = mean[0], iv = inv[0], k0 = coef[0], k1 = coef[1], k2 = coef[2];
+  auto one = [&](long p, float ps, float db, const float (&fv)[V]) {
+    const float xh = (ps - mu) * iv;
+    const float dp = k0 * (db - k1 - xh * k2);
+    float o[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       sw[e] += dp * fv[e];
@@ -1821,6 +1821,27 @@ __global__ void attn_bwd2_kernel(const float* dpsibn, const float* psi, const fl
     }
     if (tx == 0) sb += dp;
     store_vec(dzf + p * lddz + c0, o);
+  };
+  // four pixels per thread per round, all their loads issued first (one pixel per round left each
+  // round's load latency exposed); the sums run in the same pixel order as before
+  constexpr int U = 4;
+  long p = p0 + ty;
+  for (; p + (long)(U - 1) * rows < p1; p += (long)U * rows) {
+    float ps[U], db[U], fv[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long q = p + (long)u * rows;
+      ps[u] = psi[q];
+      db[u] = dpsibn[q];
+      load_vec(f + q * ldf + c0, fv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(p + (long)u * rows, ps[u], db[u], fv[u]);
+  }
+  for (; p < p1; p += rows) {
+    float fv[V];
+    load_vec(f + p * ldf + c0, fv);
+    one(p, psi[p], dpsibn[p], fv);
   }
 #pragma unroll
   for (int e = 0; e < V; ++e) red[threadIdx.x][e] = sw[e];

@@ -87,6 +87,17 @@ _NO_KERNEL = {"aten::empty", "aten::empty_strided", "aten::empty_like", "aten::n
               "aten::detach", "aten::alias", "aten::lift_fresh", "aten::_to_copy_noop"}
 
 
+# out-of-place factories whose result is one constant: name -> (args, kwargs) -> fill value
+_FILL = {"aten::zeros": lambda a, k: 0, "aten::zeros_like": lambda a, k: 0, "aten::new_zeros": lambda a, k: 0,
+         "aten::ones": lambda a, k: 1, "aten::ones_like": lambda a, k: 1, "aten::new_ones": lambda a, k: 1,
+         "aten::full": lambda a, k: a[1] if len(a) > 1 else k["fill_value"],
+         "aten::full_like": lambda a, k: a[1] if len(a) > 1 else k["fill_value"]}
+
+
+def _fill_into(out, value):
+    out.fill_(value)
+
+
 class _Mode(TorchDispatchMode):
     def __init__(self, plan):
         super().__init__()
@@ -121,6 +132,10 @@ class _Mode(TorchDispatchMode):
                 raise RuntimeError(f"StepPlan: torch op {name} reads an input tensor (not rebased on replay)")
         if sch.is_mutable:
             plan.calls.append(("torch", func, args, kwargs, stream, None))
+        elif name in _FILL and isinstance(out, torch.Tensor):
+            # a constant-filled factory (e.g. a zeroed padded gradient buffer): replay fills the recorded
+            # tensor in place -- recomputing it would allocate a fresh tensor and copy it over every replay
+            plan.calls.append(("torch", _fill_into, (out, _FILL[name](args, kwargs)), {}, stream, None))
         elif isinstance(out, torch.Tensor):
             # out-of-place: replay computes a fresh result and copies it into the recorded one, which is
             # what later recorded launches read
