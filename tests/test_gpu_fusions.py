@@ -19,6 +19,8 @@ summation order: 1e-5 relative), at every decoder shape of the 512x512 bench.
 """
 import math
 
+import os
+
 import pytest
 import torch
 
@@ -115,9 +117,13 @@ def test_upsample_bwd_relu(N, H, W, C, align):
     g = torch.Generator(device=DEV).manual_seed(N * 7 + H + C)
     dy = torch.randn(N, 2 * H, 2 * W, C, generator=g, device=DEV).to(torch.bfloat16)
     a = torch.relu(torch.randn(N, H, W, C, generator=g, device=DEV)).to(torch.bfloat16)
-    # reference: the unfused kernels
+    # reference: the unfused kernels (the row-blocked adjoint: read per call, UNETSEG_UP_STREAM=0)
     da = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=DEV)
-    lib.upsample2x_bwd(DT_BF16, dy.data_ptr(), C, N, H, W, C, align, da.data_ptr(), C, 0, _st())
+    os.environ["UNETSEG_UP_STREAM"] = "0"
+    try:
+        lib.upsample2x_bwd(DT_BF16, dy.data_ptr(), C, N, H, W, C, align, da.data_ptr(), C, 0, _st())
+    finally:
+        os.environ.pop("UNETSEG_UP_STREAM", None)
     M = N * H * W
     Gr = lib.reduce_tiles(DT_BF16, M, C, None, None)
     pref = torch.zeros(C, Gr, device=DEV)
@@ -135,6 +141,33 @@ def test_upsample_bwd_relu(N, H, W, C, align):
     ref = pref.double().sum(1)
     assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-5
     assert torch.allclose(got, dx.double().sum((0, 1, 2)), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("N,H,W,C,align", [(8, 256, 256, 64, 0), (8, 32, 32, 512, 0), (16, 128, 128, 128, 1),
+                                           (2, 24, 40, 64, 0), (3, 16, 72, 64, 1), (4, 7, 9, 64, 0)])
+def test_upsample_bwd_stream(N, H, W, C, align):
+    """the plain upsample adjoint (unetseg_upsample2x_bwd: the attention U-Net decoder's Upsample,
+    model/unet_attention.py) on the row-streaming kernel, bit-identical to the row-blocked one, stored and
+    accumulated (heights that are not a multiple of 8 take the row-blocked kernel in both runs)"""
+    from unetseg_hip.lib import DT_BF16, lib
+    g = torch.Generator(device=DEV).manual_seed(N * 11 + H + C)
+    dy = torch.randn(N, 2 * H, 2 * W, C, generator=g, device=DEV).to(torch.bfloat16)
+    base = torch.randn(N, H, W, C, generator=g, device=DEV).to(torch.bfloat16)
+    outs = []
+    for stream in ("0", "1"):
+        os.environ["UNETSEG_UP_STREAM"] = stream
+        try:
+            o = []
+            for acc in (0, 1):
+                dx = base.clone() if acc else torch.full_like(base, float("nan"))
+                lib.upsample2x_bwd(DT_BF16, dy.data_ptr(), C, N, H, W, C, align, dx.data_ptr(), C, acc, _st())
+                o.append(dx)
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop("UNETSEG_UP_STREAM", None)
+        outs.append(o)
+    for a, b in zip(*outs):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
 
 
 @pytest.mark.parametrize("M,C,mode", [(16 * 128 * 128, 256, 1), (16 * 32 * 32, 1024, 2), (3 * 15 * 17, 64, 1)])

@@ -1288,10 +1288,11 @@ __global__ __launch_bounds__(256) void upsample_bwd_relu_kernel(const T* dy, int
 // R = 4 form down to 16.  Arithmetic identical to upsample_bwd (same up_taps / up_w weights, same
 // per-row J order, same expressions): bit-identical dx.  part[g][0][c] as upsample_bwd_relu_kernel
 // (g = blockIdx.y * gridDim.x + blockIdx.x).
-template <typename T, int RS, int K, int PF>
+// MASK false: the plain adjoint (unetseg_upsample2x_bwd: no ReLU, no partials, dx (+)= as upsample_bwd's).
+template <typename T, int RS, int K, int PF, bool MASK = true>
 __global__ __launch_bounds__(256, PF == 1 ? 4 : 3) void upsample_bwd_relu_stream_kernel(const T* dy, int ldy, int N, int H, int W,
                                                                         int C, int align, const T* A, int lda, T* dx,
-                                                                        int ldx, float* part) {
+                                                                        int ldx, float* part, int accumulate = 0) {
   constexpr int V = VE<T>;
   __shared__ float red[256 * V];
   const int cv = C / V, OH = 2 * H, OW = 2 * W;
@@ -1333,11 +1334,26 @@ __global__ __launch_bounds__(256, PF == 1 ? 4 : 3) void upsample_bwd_relu_stream
     const T* An = A + ((long)n * H * W + w) * lda + c0;
     T* dxn = dx + ((long)n * H * W + w) * ldx + c0;
     auto amask = [&](int r) -> uint4 {
+      if constexpr (!MASK) return uint4{0u, 0u, 0u, 0u};
       return (r >= h0 && r < h0 + RS) ? *reinterpret_cast<const uint4*>(An + (long)r * W * lda) : uint4{0u, 0u, 0u, 0u};
     };
     // finish input row r (acc = its adjoint): mask, round as stored, partial sums
     auto finish = [&](int r, const float (&acc)[V], const uint4& am) {
       if (r < h0 || r >= h0 + RS) return;
+      if constexpr (!MASK) {
+        T* o = dxn + (long)r * W * ldx;
+        float v[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) v[e] = acc[e];
+        if (accumulate) {
+          float old[V];
+          load_vec(o, old);
+#pragma unroll
+          for (int e = 0; e < V; ++e) v[e] += old[e];
+        }
+        store_vec(o, v);
+        return;
+      }
       float a[V];
       cvt16<T>(am, a);
       T o[V];
@@ -1409,6 +1425,7 @@ __global__ __launch_bounds__(256, PF == 1 ? 4 : 3) void upsample_bwd_relu_stream
     finish(ra, accA, mA);
     finish(ra + 1, accB, mB);
   }
+  if constexpr (!MASK) return;
 #pragma unroll
   for (int e = 0; e < V; ++e) red[threadIdx.x * V + e] = s[e];
   __syncthreads();
@@ -2243,6 +2260,9 @@ UNETSEG_API int unetseg_upsample2x_fwd(int dtype, const void* x, int ldx, int n,
   return 0;
 }
 
+static int up_taps_max(int in, int align);
+static int up_stream_rows(int dtype, int n, int h, int w, int c);
+
 UNETSEG_API int unetseg_upsample2x_bwd(int dtype, const void* dy, int ldy, int n, int h, int w, int c,
                                        int align_corners, void* dx, int ldx, int accumulate, void* stream) {
   CHECK_VEC(dtype, c, "upsample_bwd");
@@ -2250,8 +2270,25 @@ UNETSEG_API int unetseg_upsample2x_bwd(int dtype, const void* dy, int ldy, int n
 #define UP_BWD(R)                                                                                            \
   hipLaunchKernelGGL((upsample_bwd_kernel<T, R>), dim3(ceil_div(w * (c / VE<T>), 256), ceil_div(n * h, R)), dim3(256), \
                      0, (hipStream_t)stream, (const T*)dy, ldy, n, h, w, c, align_corners, (T*)dx, ldx, accumulate)
-  const int rpb = up_rows_pb();
-  DISPATCH_T(dtype, if (rpb == 2) UP_BWD(2); else if (rpb == 8) UP_BWD(8); else UP_BWD(kUpRowsPB));
+  const int rs = up_stream_rows(dtype, n, h, w, c);
+  if (rs) {
+    // the row-streaming adjoint without the mask (as upsample_bwd_relu's default), bit-identical
+    const int K = up_taps_max(w, align_corners) <= 4 ? 4 : 5;
+#define UP_STREAM_PLAIN(RS, KK)                                                                                  \
+  hipLaunchKernelGGL((upsample_bwd_relu_stream_kernel<T, RS, KK, 1, false>),                                     \
+                     dim3(ceil_div(w * (c / VE<T>), 256), n * h / RS), dim3(256), 0, (hipStream_t)stream,         \
+                     (const T*)dy, ldy, n, h, w, c, align_corners, (const T*)nullptr, 0, (T*)dx, ldx, (float*)nullptr, \
+                     accumulate)
+    DISPATCH_T(dtype, if (rs == 16) {
+      if (K == 4) UP_STREAM_PLAIN(16, 4); else UP_STREAM_PLAIN(16, 5);
+    } else {
+      if (K == 4) UP_STREAM_PLAIN(8, 4); else UP_STREAM_PLAIN(8, 5);
+    });
+#undef UP_STREAM_PLAIN
+  } else {
+    const int rpb = up_rows_pb();
+    DISPATCH_T(dtype, if (rpb == 2) UP_BWD(2); else if (rpb == 8) UP_BWD(8); else UP_BWD(kUpRowsPB));
+  }
 #undef UP_BWD
   US_LAUNCH_CHECK("upsample_bwd");
   return 0;
