@@ -781,17 +781,21 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
     uint4 oldv[GRP], zv[POST == 3 ? GRP : 1], z2v[POST == 3 ? GRP : 1];
     unsigned mkv[POST == 3 ? GRP : 1];
     if (POST == 3 || a.accumulate) {
+      // every load unconditional, at a valid address for the lanes whose row / chunk is absent (the
+      // tile's row 0, the last chunk; their values are never used): a load under the lane condition
+      // had its value moved across the branch and was waited on by itself -- GRP serial round trips
+      const bf16* aux2p = two ? (const bf16*)a.aux2 : (const bf16*)a.aux;
+      const long ld2 = two ? a.ld_aux2 : a.ld_aux;
+      const int ncl = nc < a.Ng ? nc : a.Ng - 8;
 #pragma unroll
       for (int j = 0; j < GRP; ++j) {
         const int r = (g0 + j) * RPI + rsub;
-        const bool ok = r < cnt && nc < a.Ng;
-        const long opx = ok ? out_pix(row0 + r) : 0;
-        oldv[j] = ok ? *reinterpret_cast<const uint4*>((const bf16*)a.y + opx * a.ldy + nc) : uint4{0u, 0u, 0u, 0u};
+        const long opx = out_pix(row0 + (r < cnt ? r : 0));
+        oldv[j] = *reinterpret_cast<const uint4*>((const bf16*)a.y + opx * a.ldy + ncl);
         if constexpr (POST == 3) {
-          zv[j] = ok ? *reinterpret_cast<const uint4*>((const bf16*)a.aux + opx * a.ld_aux + nc) : uint4{0u, 0u, 0u, 0u};
-          z2v[j] = ok && two ? *reinterpret_cast<const uint4*>((const bf16*)a.aux2 + opx * a.ld_aux2 + nc)
-                             : uint4{0u, 0u, 0u, 0u};
-          mkv[j] = ok ? (unsigned)a.mbits[opx * (a.Ng >> 3) + (nc >> 3)] : 0u;
+          zv[j] = *reinterpret_cast<const uint4*>((const bf16*)a.aux + opx * a.ld_aux + ncl);
+          z2v[j] = *reinterpret_cast<const uint4*>(aux2p + opx * ld2 + ncl);
+          mkv[j] = (unsigned)a.mbits[opx * (a.Ng >> 3) + (ncl >> 3)];
         }
       }
     }

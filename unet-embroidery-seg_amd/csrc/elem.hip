@@ -140,19 +140,23 @@ __global__ __launch_bounds__(NWV > 4 ? 64 * NWV : 256) void bn_finalize_kernel(c
   const long st = 2L * C;
   // the epilogue's operands loaded up front (behind the reductions each was a round trip)
   const float gam = gamma[c], bet = beta[c];
-  const float rm0 = rmean ? rmean[c] : 0.f, rv0 = rmean ? rvar[c] : 0.f;
+  const float rm0 = (rmean ? rmean : gamma)[c], rv0 = (rmean ? rvar : gamma)[c];  // unused without rmean
   // pass 1 keeps this lane's rows in registers when one round covers G (pass 2 re-reads otherwise)
   float sv[kFinRPL], qv[kFinRPL];
   double tsum[1] = {0.0};
+  // unconditional loads (a row past G re-reads row G - 1), masked after: see fin_row_sums
   for (int g0 = 0; g0 < G; g0 += kFinRPL * NL) {
 #pragma unroll
     for (int k = 0; k < kFinRPL; ++k) {
-      const int g = g0 + li + k * NL;
-      sv[k] = g < G ? part[g * st + c] : 0.f;
-      qv[k] = g < G ? part[g * st + C + c] : 0.f;
+      const int g = min(g0 + li + k * NL, G - 1);
+      sv[k] = part[g * st + c];
+      qv[k] = part[g * st + C + c];
     }
 #pragma unroll
-    for (int k = 0; k < kFinRPL; ++k) tsum[0] += (double)sv[k];
+    for (int k = 0; k < kFinRPL; ++k) {
+      if (g0 + li + k * NL >= G) sv[k] = qv[k] = 0.f;
+      tsum[0] += (double)sv[k];
+    }
   }
   fin_group_sum<NWV, 1>(tsum, sc);
   const double mean = tsum[0] / (double)M;
@@ -162,9 +166,9 @@ __global__ __launch_bounds__(NWV > 4 ? 64 * NWV : 256) void bn_finalize_kernel(c
     if (!one_round) {
 #pragma unroll
       for (int k = 0; k < kFinRPL; ++k) {
-        const int g = g0 + li + k * NL;
-        sv[k] = g < G ? part[g * st + c] : 0.f;
-        qv[k] = g < G ? part[g * st + C + c] : 0.f;
+        const int g = min(g0 + li + k * NL, G - 1);
+        sv[k] = part[g * st + c];
+        qv[k] = part[g * st + C + c];
       }
     }
 #pragma unroll
@@ -2417,10 +2421,15 @@ __global__ void pack_input_stem_kernel(const float* x, int N, int C, int H, int 
     const long row = i / WP;
     const int wp = (int)(i - row * WP), w = wp - 3;
     const long n = row / H, h = row - n * H;
+    // all eight loads unconditional (clamped into the image; channels past C re-read channel C - 1,
+    // the same cache line) and masked after: conditional loads were waited on one at a time
+    const int wc = min(max(w, 0), W - 1);
+    float xv[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) xv[c] = x[((n * C + min(c, C - 1)) * H + h) * (long)W + wc];
     bf16 v[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
-      v[c] = (bf16)((c < C && w >= 0 && w < W) ? x[((n * C + c) * H + h) * (long)W + w] : 0.f);
+    for (int c = 0; c < 8; ++c) v[c] = (bf16)((c < C && w >= 0 && w < W) ? xv[c] : 0.f);
     *reinterpret_cast<uint4*>(y + i * 8) = *reinterpret_cast<uint4*>(v);
   }
 }
