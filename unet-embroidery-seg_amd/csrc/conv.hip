@@ -551,6 +551,15 @@ __global__ __launch_bounds__(256) void wgrad_reduce_split_kernel(const float* ws
   if (q < s4) {
     const float4* p = reinterpret_cast<const float4*>(ws) + q;
     int z = sl * R;
+    for (; z + 7 < z1; z += 8) {  // eight slabs in flight, added in slab order
+      float4 a[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = p[(z + u) * s4];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v.x += a[u].x; v.y += a[u].y; v.z += a[u].z; v.w += a[u].w;
+      }
+    }
     for (; z + 3 < z1; z += 4) {
       const float4 a = p[z * s4], b = p[(z + 1) * s4], c = p[(z + 2) * s4], d = p[(z + 3) * s4];
       v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
@@ -674,16 +683,30 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const Unetseg
   const int vrun = max(0, min(CT, d.C - c0)) * taps;   // of which exist in the source
   const int t = threadIdx.x;
   if ((d.C * taps) % 4 == 0 && vrun % 4 == 0) {  // 16-B loads (rows start 16-B aligned)
+    // every load of the tile issued before the first LDS store: unconditional (absent rows / columns
+    // read the source's first float4 and are zeroed after); a load under the lane condition was
+    // waited on by itself, one round trip per loop iteration
     const int run4 = run >> 2;
-    for (int i = t; i < kPackK * run4; i += 256) {
+    constexpr int NIT = kPackK * 512 / 4 / 256;  // run <= 512
+    float4 v[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = t + it * 256;
       const int kl = i / run4, j = (i - kl * run4) * 4;
       const int k = k0 + kl;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (k < d.K && j < vrun) v = *reinterpret_cast<const float4*>(d.w + ((long)k * d.C + c0) * taps + j);
-      tile[kl][j] = v.x;
-      tile[kl][j + 1] = v.y;
-      tile[kl][j + 2] = v.z;
-      tile[kl][j + 3] = v.w;
+      const bool ok = i < kPackK * run4 && k < d.K && j < vrun;
+      const float4 x = *reinterpret_cast<const float4*>(ok ? d.w + ((long)k * d.C + c0) * taps + j : d.w);
+      v[it] = ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = t + it * 256;
+      if (i >= kPackK * run4) break;
+      const int kl = i / run4, j = (i - kl * run4) * 4;
+      tile[kl][j] = v[it].x;
+      tile[kl][j + 1] = v[it].y;
+      tile[kl][j + 2] = v[it].z;
+      tile[kl][j + 3] = v[it].w;
     }
   } else {
     for (int i = t; i < kPackK * run; i += 256) {

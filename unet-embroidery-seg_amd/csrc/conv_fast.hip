@@ -781,16 +781,18 @@ __device__ __forceinline__ void tn_fast_body(const FastTNArgs& a, const int did,
     uint4 oldv[GRP], zv[POST == 3 ? GRP : 1], z2v[POST == 3 ? GRP : 1];
     unsigned mkv[POST == 3 ? GRP : 1];
     if (POST == 3 || a.accumulate) {
-      // every load unconditional, at a valid address for the lanes whose row / chunk is absent (the
-      // tile's row 0, the last chunk; their values are never used): a load under the lane condition
-      // had its value moved across the branch and was waited on by itself -- GRP serial round trips
+      // every load unconditional, at a valid address for the lanes whose row / chunk is absent (this
+      // wave's first row, or the last row M - 1 when the wave has none -- the last tile's second
+      // row-wave can start past M; the last chunk; their values are never used): a load under the lane
+      // condition had its value moved across the branch and was waited on by itself -- GRP serial
+      // round trips
       const bf16* aux2p = two ? (const bf16*)a.aux2 : (const bf16*)a.aux;
       const long ld2 = two ? a.ld_aux2 : a.ld_aux;
       const int ncl = nc < a.Ng ? nc : a.Ng - 8;
 #pragma unroll
       for (int j = 0; j < GRP; ++j) {
         const int r = (g0 + j) * RPI + rsub;
-        const long opx = out_pix(row0 + (r < cnt ? r : 0));
+        const long opx = out_pix(r < cnt ? row0 + r : min(row0, a.M - 1));
         oldv[j] = *reinterpret_cast<const uint4*>((const bf16*)a.y + opx * a.ldy + ncl);
         if constexpr (POST == 3) {
           zv[j] = *reinterpret_cast<const uint4*>((const bf16*)a.aux + opx * a.ld_aux + ncl);
