@@ -25,7 +25,7 @@ CLASSES = [
     ("weight gradient on the compute stream", r"wgrad|stem_wgrad_remap"),
     ("BN apply (forward)", r"bn_apply"),
     ("BN backward apply / reduce", r"bn_bwd_apply|bn_bwd_reduce"),
-    ("BN / bias finalize", r"finalize|colsum"),
+    ("BN / bias finalize", r"finalize|colsum|fin_merge"),
     ("upsample fwd / bwd", r"upsample"),
     ("maxpool fwd / bwd", r"maxpool"),
     ("ReLU backward + bias", r"relu_bwd"),
