@@ -1831,13 +1831,15 @@ __global__ void attn_bwd2_kernel(const float* dpsibn, const float* psi, const fl
 #pragma unroll
   for (int e = 0; e < V; ++e) { wv[e] = wpsi[c0 + e]; sw[e] = 0.f; }
   const float mu = mean[0], iv = inv[0], k0 = coef[0], k1 = coef[1], k2 = coef[2];
+  // the contractions spelled out (fmaf): unrolled, the compiler packed some products into
+  // v_pk_mul_f32 + add, which rounds twice where the one-pixel loop's fma rounded once
   auto one = [&](long p, float ps, float db, const float (&fv)[V]) {
     const float xh = (ps - mu) * iv;
-    const float dp = k0 * (db - k1 - xh * k2);
+    const float dp = k0 * fmaf(-xh, k2, db - k1);
     float o[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      sw[e] += dp * fv[e];
+      sw[e] = fmaf(dp, fv[e], sw[e]);
       o[e] = fv[e] > 0.f ? dp * wv[e] : 0.f;
     }
     if (tx == 0) sb += dp;

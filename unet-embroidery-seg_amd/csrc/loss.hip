@@ -533,7 +533,21 @@ __global__ void linear_fwd_kernel(const float* x, const float* W, const float* b
   if (wave >= B * O) return;
   const int b = wave / O, o = wave - b * O;
   float s = 0.f;
-  for (int i = lane; i < I; i += 64) s += x[(long)b * I + i] * W[(long)o * I + i];
+  // eight rounds' loads in flight (the plain loop waited out one round trip per 64 inputs); the
+  // products are added in the same i order
+  constexpr int U = 8;
+  int i = lane;
+  for (; i + 64 * (U - 1) < I; i += 64 * U) {
+    float xv[U], wv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      xv[u] = x[(long)b * I + i + 64 * u];
+      wv[u] = W[(long)o * I + i + 64 * u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) s = fmaf(xv[u], wv[u], s);  // explicit: as the plain loop's contraction
+  }
+  for (; i < I; i += 64) s += x[(long)b * I + i] * W[(long)o * I + i];
   s = wave_sum(s);
   if (lane == 0) {
     s += bias ? bias[o] : 0.f;
@@ -566,7 +580,21 @@ __global__ void linear_bwd_x_kernel(const float* dyp, const float* W, int B, int
   if (t >= B * I) return;
   const int b = t / I, i = t - b * I;
   float s = 0.f;
-  for (int o = 0; o < O; ++o) s += dyp[(long)b * O + o] * W[(long)o * I + i];
+  // 32 outputs' loads in flight per round (one round trip per load left the 2048 -> 512 FC's
+  // backward at ~100 us); the products are added in the same o order as the plain loop
+  constexpr int U = 32;
+  int o = 0;
+  for (; o + U <= O; o += U) {
+    float d[U], w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      d[u] = dyp[(long)b * O + o + u];
+      w[u] = W[(long)(o + u) * I + i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) s = fmaf(d[u], w[u], s);  // explicit: the packed-multiply form rounds twice
+  }
+  for (; o < O; ++o) s += dyp[(long)b * O + o] * W[(long)o * I + i];
   dx[t] = s;
 }
 
