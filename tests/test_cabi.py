@@ -90,6 +90,11 @@ def test_argument_errors_reported_without_device():
     assert b"cpad" in raw.unetseg_last_error()
     with pytest.raises(RuntimeError, match="cpad"):
         lib.lib.pack_input(0, None, 1, 3, 4, 4, 2, None, None)
+    # the round-6 row merge: null partials, and a statistics merge without nq == 2
+    assert raw.unetseg_fin_merge_rows(None, 64, 1024, 0, 0, 2, None, None) != 0
+    assert b"fin_merge_rows" in raw.unetseg_last_error()
+    with pytest.raises(RuntimeError, match="statistics merge"):
+        lib.lib.fin_merge_rows(16, 64, 1024, 4096, 256, 3, 16, None)
 
 
 def test_fastcall_binding_matches_ctypes():
