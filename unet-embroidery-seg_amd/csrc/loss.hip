@@ -30,7 +30,9 @@ __device__ __forceinline__ float key_to_float(uint32_t k) {
 // logits source: planar fp32 [B][nch][P]; nch==2 -> z = o1 - o0, nch==1 -> z = o0
 __device__ __forceinline__ float load_z(const float* out, int nch, int b, long P, long i) {
   const float* base = out + (long)b * nch * P;
-  return nch == 2 ? base[P + i] - base[i] : base[i];
+  // both loads unconditional (a load under the nch branch was waited on inside it)
+  const float o0 = base[i], o1 = base[nch == 2 ? P + i : i];
+  return nch == 2 ? o1 - o0 : o0;
 }
 
 // has_ignore: pixels whose target is `ignore` get error -inf and label 0, so they sort after every
@@ -43,8 +45,9 @@ __global__ void lovasz_keygen_kernel(const float* out, int nch, const int64_t* t
     const int b = (int)(i / P);
     const long px = i - (long)b * P;
     const float z = load_z(out, nch, b, P, px);
-    const bool ign = has_ignore && tgt[i] == ignore;
-    const uint32_t y = (!ign && tgt[i] == 1) ? 1u : 0u;
+    const int64_t tv = tgt[i];
+    const bool ign = has_ignore && tv == ignore;
+    const uint32_t y = (!ign && tv == 1) ? 1u : 0u;
     const float e = ign ? -INFINITY : 1.0f - z * (2.0f * (float)y - 1.0f);
     keys[i] = desc_key(e);
     vals[i] = (uint32_t)px | (y << 31);
