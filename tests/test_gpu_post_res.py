@@ -48,6 +48,10 @@ SHAPES = [
     (16, 32, 32, 256, 1024, False, "tn128x128_1st", 1024),    # layer3
     (16, 16, 16, 512, 2048, True, "ring256x128_t1", 2048),    # layer4
     (1, 15, 17, 64, 256, False, None, 256),                   # ragged rows
+    # fewer than 65 rows in the last (only) tile: its second row-wave is empty and the epilogue's
+    # unconditional loads must stay inside the tensor (the 2x2 layer4 maps of a 64^2 input, M = 8)
+    (2, 2, 2, 512, 2048, True, None, 2048),
+    (1, 5, 5, 64, 256, False, None, 256),
     # a layer's block 0 conv1, fusing the previous layer's last block (its output is also the decoder's
     # skip input, up_concat2/3/4 in = 512 / 1024 / 3072 channels: dx is the first C channels of that
     # gradient, after the downsample branch accumulated onto it)
