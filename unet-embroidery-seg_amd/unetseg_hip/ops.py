@@ -820,9 +820,10 @@ class BNState:
     __slots__ = ("mean", "inv", "sc", "sh")
 
 
-#: finalize row partials with more rows than this are first merged 16 to 1 (unetseg_fin_merge_rows);
+#: finalize row partials with more rows than this (2048: measured best of 512 / 1024 / 2048) are first
+#: merged 16 to 1 (unetseg_fin_merge_rows);
 #: UNETSEG_FIN_MERGE=0 finalizes them directly
-FIN_MERGE_MIN = int(os.environ.get("UNETSEG_FIN_MERGE_MIN", "512"))
+FIN_MERGE_MIN = int(os.environ.get("UNETSEG_FIN_MERGE_MIN", "2048"))
 FIN_MERGE = os.environ.get("UNETSEG_FIN_MERGE", "1") != "0"
 
 
