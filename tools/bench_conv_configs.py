@@ -58,6 +58,14 @@ def main():
     step()
     torch.cuda.synchronize()
     table = introspect.probe_table(ops.PROBE)
+    # compulsory HBM bytes per configuration (bench.compulsory_bytes of each call, charged to the
+    # call's first key like its time): the denominator of a per-configuration traffic ratio
+    import bench
+    comp = {}
+    for kind, flops, nl, e0, e1, desc in ops.PROBE:
+        keys = introspect.call_configs(desc)
+        if keys and not desc[0].startswith("wgrad"):
+            comp[keys[0]] = comp.get(keys[0], 0) + bench.compulsory_bytes(desc)
     ops.PROBE = None
     rows = sorted(table.items(), key=lambda kv: -kv[1][1])
     lines = [f"# {args.model} {args.size}x{args.size} batch {args.batch} bf16: kernel configurations of one step"]
@@ -70,7 +78,8 @@ def main():
         with open(args.out, "w") as f:
             f.write(text + "\n")
         with open(os.path.splitext(args.out)[0] + ".json", "w") as f:
-            json.dump({k: {"calls": n, "ms": round(1e3 * t, 4)} for k, (n, t) in rows}, f, indent=1)
+            json.dump({k: {"calls": n, "ms": round(1e3 * t, 4), "compulsory_mb": round(comp.get(k, 0) / 1e6, 2)}
+                       for k, (n, t) in rows}, f, indent=1)
 
 
 if __name__ == "__main__":
