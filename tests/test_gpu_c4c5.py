@@ -165,6 +165,39 @@ def test_attention_gate_kernels_c4(N, H, Cs, Cg, Ci, tile):
     torch.testing.assert_close(pb.double().sum(), dp.sum(), rtol=1e-4, atol=2e-4 * dp.abs().sum().item())
 
 
+@pytest.mark.parametrize("M,C,K,stats", [(3102, 32, 1, True), (3102, 64, 1, True), (3102, 64, 2, False),
+                                          (2 * 512 * 512 + 77, 64, 2, False), (1000, 128, 1, False),
+                                          (129, 32, 1, True), (5, 64, 2, False)])
+def test_pw_small_fwd_ragged(M, C, K, stats):
+    """the small-Cout 1x1 forward (attention psi with its BN partials, the 64 -> 2 / -> 1 heads) at pixel
+    counts that leave a partial last block and partial four-pass groups: the clamped loads of the
+    round-6 kernels must neither fault nor leak into stored pixels; the head's 128-pixel grid without
+    statistics against pw_tile's with them"""
+    from unetseg_hip.lib import DT_BF16, lib
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + C + K)
+    N = 2 if (K == 2 and M % 2 == 0) else 1  # planar [N][K][HW] output
+    HW = M // N
+    x = torch.relu(torch.randn(M, C, generator=g, device=DEV)).to(torch.bfloat16)
+    w = (torch.randn(K, C, generator=g, device=DEV) / math.sqrt(C)).contiguous()
+    b = torch.randn(K, generator=g, device=DEV) * 0.1
+    y = torch.full((N, K, HW), float("nan"), dtype=torch.float32, device=DEV)
+    G = lib.pw_small_tiles(M)
+    part = torch.empty(G, 2, dtype=torch.float32, device=DEV) if stats else None
+    lib.pw_small_fwd(DT_BF16, _P(x), C, M, HW, C, K, _P(w), _P(b), _P(y), _P(part) if stats else 0, _st())
+    torch.cuda.synchronize()
+    x64, w64 = x.double(), w.double()
+    ref = (x64 @ w64.t() + b.double()).reshape(N, HW, K).permute(0, 2, 1)
+    mag = (x64.abs() @ w64.abs().t() + b.double().abs()).reshape(N, HW, K).permute(0, 2, 1)
+    assert not bool(torch.isnan(y).any()), "a pixel was not written"
+    err = (y.double() - ref).abs()
+    assert bool((err <= 2e-5 * mag + 1e-7).all()), f"max err {err.max().item():.3e}"
+    if stats:
+        tot, m2 = _merge(part, lib.pw_small_tile(M), M)
+        pk = y.double().reshape(-1)
+        torch.testing.assert_close(tot, pk.sum(), rtol=1e-5, atol=1e-5 * pk.abs().sum().item())
+        torch.testing.assert_close(m2 / M, pk.var(unbiased=False), rtol=1e-5, atol=1e-9)
+
+
 @pytest.mark.parametrize("N,H,Cs,Cg,Ci,tile", C4_GATES)
 def test_attention_gate_op_c4_fp32(N, H, Cs, Cg, Ci, tile):
     """ops.attention_gate (the whole gate, training mode) in fp32 at the C4 gate shapes against a

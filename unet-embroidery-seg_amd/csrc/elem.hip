@@ -1522,32 +1522,60 @@ __global__ void pw_small_fwd_kernel(const T* x, int ldx, long M, int HW, int C, 
     }
     return;
   }
-  // pass 1: outputs
-  for (long pbase = p0 + (long)wid * ppw; pbase < p1; pbase += (long)nw * ppw) {
-    const long p = pbase + sub;
-    float xv[V];
-    float acc[K];
+  // pass 1: outputs.  Four wave passes per iteration with their loads issued first at clamped (valid)
+  // pixels: the one load under `p < p1` got a branch and a vmcnt(0) of its own, one exposed round trip
+  // per pass (the attention psi conv at 8 x 512^2: 57 us for 142 MB).  The dot products are spelled out
+  // as the one-pass loop compiled them -- rounded products (v_pk_mul_f32), then adds in channel order --
+  // so the outputs stay bit-identical whatever the unrolled code would have been contracted to
+  // (the bias is loaded once up front: read under the store's lane condition it was another branch
+  // with a vmcnt(0) behind it)
+  constexpr int U = 4;
+  const long wstep = (long)nw * ppw;
+  float bk[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = 0.f;
-    if (p < p1) {
-      load_vec(x + p * ldx + v * V, xv);
+  for (int k = 0; k < K; ++k) bk[k] = b ? b[k] : 0.f;
+  for (long pbase = p0 + (long)wid * ppw; pbase < p1; pbase += U * wstep) {
+    uint4 raw[U];
 #pragma unroll
-      for (int k = 0; k < K; ++k)
-#pragma unroll
-        for (int e = 0; e < V; ++e) acc[k] += xv[e] * wv[k][e];
+    for (int u = 0; u < U; ++u) {
+      const long pc = min(pbase + u * wstep + sub, p1 - 1);
+      raw[u] = *reinterpret_cast<const uint4*>(x + pc * ldx + v * V);
     }
+    // keep the four loads together: the scheduler otherwise started unpacking the first one before the
+    // others were issued (a vmcnt(0) right behind it)
+    __builtin_amdgcn_sched_barrier(0);
+    float xv[U][V];
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-      for (int o = 1; o < cv; o <<= 1) acc[k] += __shfl_xor(acc[k], o, 64);
-    if (p < p1 && v == 0) {
-      const long n = p / HW, hw = p - n * HW;
+    for (int u = 0; u < U; ++u) cvt16<T>(raw[u], xv[u]);
+    float acc[U][K];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const float val = acc[k] + (b ? b[k] : 0.f);
-        y[(n * K + k) * HW + hw] = val;
-        if (k == 0) lsum += val;
+#pragma clang fp contract(off)
+        acc[u][k] = 0.f;
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[u][k] += xv[u][e] * wv[k][e];
       }
-    }
+    for (int o = 1; o < cv; o <<= 1)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[u][k] += __shfl_xor(acc[u][k], o, 64);
+    if (v == 0)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long p = pbase + u * wstep + sub;
+        if (p < p1) {
+          const long n = p / HW, hw = p - n * HW;
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            const float val = acc[u][k] + bk[k];
+            y[(n * K + k) * HW + hw] = val;
+            if (k == 0) lsum += val;
+          }
+        }
+      }
   }
   if (!stats) return;
   const double tot = block_sum(lsum, sred);
@@ -2464,16 +2492,22 @@ UNETSEG_API int unetseg_pw_small_fwd(int dtype, const void* x, int ldx, long M, 
   US_CHECK_ARG(c / V <= 64 && ((c / V) & (c / V - 1)) == 0, "pw_small_fwd: C/V must be a power of two <= 64");
   US_CHECK_ARG(k == 1 || k == 2, "pw_small_fwd: k must be 1 or 2");
   US_CHECK_ARG(!stats || k == 1, "pw_small_fwd: stats only for k==1");
-  const int G = unetseg_pw_small_tiles(M);
+  // without statistics the tile only sets the grid (every pixel's output is its own): 128-pixel blocks,
+  // twice the resident waves of pw_tile's for the latency-bound head -- the attention U-Net's 64 -> 2
+  // head at 8 x 512^2: 105.6 (2048) / 95.7 (512) / 87.7 (256) / 82.0 us (128).  UNETSEG_PW_FWD_TILE = T
+  // sets it (0: pw_tile); the statistics' partial rows keep pw_tile, which the BN finalize is sized by
+  static const long nostat_tile = getenv("UNETSEG_PW_FWD_TILE") ? atol(getenv("UNETSEG_PW_FWD_TILE")) : 128;
+  const long tile = (!stats && nostat_tile > 0) ? nostat_tile : pw_tile(M);
+  const int G = (int)ceil_div(M, tile);
   hipStream_t st = (hipStream_t)stream;
   static const int pw_sign = getenv("UNETSEG_PW_GENERIC") ? -1 : 1;  // A/B: generic shuffle path
   DISPATCH_T(dtype, {
     if (k == 1)
       hipLaunchKernelGGL((pw_small_fwd_kernel<T, 1>), dim3(G), dim3(256), 0, st, (const T*)x, ldx, M, hw, c, w, b, y,
-                         stats, (int)pw_tile(M) * pw_sign);
+                         stats, (int)tile * pw_sign);
     else
       hipLaunchKernelGGL((pw_small_fwd_kernel<T, 2>), dim3(G), dim3(256), 0, st, (const T*)x, ldx, M, hw, c, w, b, y,
-                         stats, (int)pw_tile(M) * pw_sign);
+                         stats, (int)tile * pw_sign);
   });
   US_LAUNCH_CHECK("pw_small_fwd");
   return 0;
