@@ -320,11 +320,11 @@ __device__ __forceinline__ void store_partials(float (&s)[NQ][V], int tv, int c0
 // produced A, 3 the packed mask bn_apply wrote (A = mbits [M][C/V] bytes).  Y2: second BN branch
 // (downsample shortcut) present.
 template <typename T, int MASK, bool Y2>
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dA, int ldd, const T* A, int lda,
-                                                            const float* msc, const float* msh, const T* y1, int ld1,
-                                                            const float* mean1, const float* inv1, const T* y2, int ld2,
-                                                            const float* mean2, const float* inv2, long M, int C,
-                                                            int tv, int pix_per_block, float* part, int G) {
+__device__ __forceinline__ void bn_bwd_reduce_body(const T* dA, int ldd, const T* A, int lda, const float* msc,
+                                                   const float* msh, const T* y1, int ld1, const float* mean1,
+                                                   const float* inv1, const T* y2, int ld2, const float* mean2,
+                                                   const float* inv2, long M, int C, int tv, int pix_per_block,
+                                                   float* part, int G) {
   constexpr int V = VE<T>;
   constexpr int NQ = Y2 ? 3 : 2;
   __shared__ float red[4 * 3 * 64 * V];
@@ -401,6 +401,27 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dA, int ldd
   }
   store_partials<NQ, V>(s, tv, c0, C, G, part, red);
 }
+
+#define BN_RED_PARAMS                                                                                             \
+  const T *dA, int ldd, const T *A, int lda, const float *msc, const float *msh, const T *y1, int ld1,            \
+      const float *mean1, const float *inv1, const T *y2, int ld2, const float *mean2, const float *inv2, long M, \
+      int C, int tv, int pix_per_block, float *part, int G
+#define BN_RED_ARGS dA, ldd, A, lda, msc, msh, y1, ld1, mean1, inv1, y2, ld2, mean2, inv2, M, C, tv, pix_per_block, part, G
+template <typename T, int MASK, bool Y2>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BN_RED_PARAMS) {
+  bn_bwd_reduce_body<T, MASK, Y2>(BN_RED_ARGS);
+}
+// the packed-mask variant (one branch) with a register budget of four waves per SIMD: under the
+// default target the scheduler serialised its main loop -- each of the 12 loads of an RU group waited on
+// before the next was issued: 19.7 -> 14.5 us (C2's call), 17.1 -> 10.2 (C5's two).  With the second
+// branch (Y2) the budget measured slower (12.2 -> 13.9 us): that one keeps the plain kernel
+template <typename T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void bn_bwd_reduce_bits_kernel(
+    BN_RED_PARAMS) {
+  bn_bwd_reduce_body<T, 3, false>(BN_RED_ARGS);
+}
+#undef BN_RED_PARAMS
+#undef BN_RED_ARGS
 
 // pass 2: coefficients.  For branch b (1 or 2): dgamma_b += sum dz*xhat_b, dbeta_b += sum dz;
 // coef[b][0][c] = gamma_b*invstd_b, coef[b][1][c] = mean(dz), coef[b][2][c] = mean(dz*xhat_b)
@@ -2083,6 +2104,9 @@ UNETSEG_API int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const 
 #define BN_RED_LAUNCH(MK, Y2)                                                                                     \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MK, Y2>), grid, dim3(256), 0, st, (const T*)dA, ldd, (const T*)A, lda, \
                      msc, msh, (const T*)y1, ld1, mean1, inv1, (const T*)y2, ld2, mean2, inv2, M, C, tv, ppb, part, G)
+#define BN_RED_BITS()                                                                                             \
+  hipLaunchKernelGGL((bn_bwd_reduce_bits_kernel<T>), grid, dim3(256), 0, st, (const T*)dA, ldd, (const T*)A, lda, \
+                     msc, msh, (const T*)y1, ld1, mean1, inv1, (const T*)y2, ld2, mean2, inv2, M, C, tv, ppb, part, G)
   DISPATCH_T(dtype, {
     if (y2) {
       if (mask == 3) BN_RED_LAUNCH(3, true);
@@ -2090,13 +2114,14 @@ UNETSEG_API int unetseg_bn_bwd_reduce(int dtype, const void* dA, int ldd, const 
       else if (mask == 2) BN_RED_LAUNCH(2, true);
       else BN_RED_LAUNCH(0, true);
     } else {
-      if (mask == 3) BN_RED_LAUNCH(3, false);
+      if (mask == 3) BN_RED_BITS();
       else if (mask == 1) BN_RED_LAUNCH(1, false);
       else if (mask == 2) BN_RED_LAUNCH(2, false);
       else BN_RED_LAUNCH(0, false);
     }
   });
 #undef BN_RED_LAUNCH
+#undef BN_RED_BITS
   US_LAUNCH_CHECK("bn_bwd_reduce");
   return 0;
 }
