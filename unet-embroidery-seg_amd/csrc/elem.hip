@@ -857,6 +857,19 @@ __global__ void maxpool_bwd_k3s2_kernel(const T* dy, int ldy, const uint8_t* idx
     for (int k = 0; k < 4; ++k)
 #pragma unroll
       for (int e = 0; e < V; ++e) acc[k][e] = 0.f;
+    // the four windows' dy and argmax bytes loaded first, at clamped (valid) windows: under the
+    // window-range conditions each window's loads were a branch with a vmcnt(0) behind it; windows out
+    // of range are skipped below, in the same (p, q) order
+    uint4 graw[4];
+    uint2 iraw[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = min(max(bi - 1 + (k >> 1), 0), P - 1), q = min(max(bj - 1 + (k & 1), 0), Q - 1);
+      const size_t opix = (size_t)((n * P + p) * Q + q);
+      graw[k] = *reinterpret_cast<const uint4*>(dy + opix * ldy + c0);
+      if constexpr (V == 8) iraw[k] = *reinterpret_cast<const uint2*>(idx + opix * C + c0);
+      else iraw[k].x = *reinterpret_cast<const unsigned*>(idx + opix * C + c0);
+    }
 #pragma unroll
     for (int dp = 0; dp < 2; ++dp) {
       const int p = bi - 1 + dp;
@@ -865,17 +878,10 @@ __global__ void maxpool_bwd_k3s2_kernel(const T* dy, int ldy, const uint8_t* idx
       for (int dq = 0; dq < 2; ++dq) {
         const int q = bj - 1 + dq;
         if (q < 0 || q >= Q) continue;
-        const size_t opix = (size_t)((n * P + p) * Q + q);
         float g[V];
-        load_vec(dy + opix * ldy + c0, g);
+        cvt16<T>(graw[dp * 2 + dq], g);
         uint8_t ib[V];
-        if constexpr (V == 8) {
-          const uint2 pk = *reinterpret_cast<const uint2*>(idx + opix * C + c0);
-          __builtin_memcpy(ib, &pk, 8);
-        } else {
-          const unsigned pk = *reinterpret_cast<const unsigned*>(idx + opix * C + c0);
-          __builtin_memcpy(ib, &pk, 4);
-        }
+        __builtin_memcpy(ib, &iraw[dp * 2 + dq], V);
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
           const int r = dp ? a : a + 2;
@@ -892,6 +898,13 @@ __global__ void maxpool_bwd_k3s2_kernel(const T* dy, int ldy, const uint8_t* idx
         }
       }
     }
+    uint4 oraw[4];  // the block's old gradient (accumulate), likewise loaded up front at clamped pixels
+    if (accumulate)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int h = min(2 * bi + (k >> 1), H - 1), w = min(2 * bj + (k & 1), W - 1);
+        oraw[k] = *reinterpret_cast<const uint4*>(dx + (size_t)((n * H + h) * W + w) * ldx + c0);
+      }
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
       const int h = 2 * bi + a;
@@ -903,7 +916,7 @@ __global__ void maxpool_bwd_k3s2_kernel(const T* dy, int ldy, const uint8_t* idx
         T* o = dx + (size_t)((n * H + h) * W + w) * ldx + c0;
         if (accumulate) {
           float old[V];
-          load_vec(o, old);
+          cvt16<T>(oraw[a * 2 + b], old);
 #pragma unroll
           for (int e = 0; e < V; ++e) acc[a * 2 + b][e] += old[e];
         }
