@@ -303,6 +303,21 @@ def test_upsample(dtname, align, H, W):
 
 @pytest.mark.parametrize("dtname", ["fp32", "bf16"])
 @pytest.mark.parametrize("align", [True, False])
+@pytest.mark.parametrize("N,H,W", [(1, 5, 7), (1, 3, 3), (3, 7, 2)])
+def test_upsample_fwd_partial_rows(dtname, align, N, H, W):
+    """output row counts N * 2H that leave a partial last row block of upsample_fwd_kernel (2 of its 4
+    rows; the model tests' N = 2 never do)"""
+    ops, DT_BF16, DT_F32 = _ops()
+    dt = DT_BF16 if dtname == "bf16" else DT_F32
+    g = torch.Generator().manual_seed(13 + H)
+    x = _round(torch.randn(N, 16, H, W, generator=g), dt)
+    y = ops.upsample2x(_ctx(dt), _node(x, dt), align)
+    ref = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=align)
+    assert _rel(_nchw(y.data), ref) < (1e-2 if dt == DT_BF16 else 1e-6)
+
+
+@pytest.mark.parametrize("dtname", ["fp32", "bf16"])
+@pytest.mark.parametrize("align", [True, False])
 @pytest.mark.parametrize("H,C", [(4, 1024), (16, 256), (32, 64)])
 def test_upsample_strided_grad(dtname, align, H, C):
     """model-shaped upsample whose gradient arrives as a channel slice of a concat gradient
